@@ -1,0 +1,1254 @@
+// fi_api.cpp -- the C-ABI runtime of libflyimg_hip.so (include/flyimg_hip.h).
+//
+// One fi_ctx per process per GPU.  A batch call:
+//   1. plans every image on the host (fi_plan.cpp): ImageMagick geometry,
+//      merged tap tables, Pillow prescale tables, smartcrop crop windows and
+//      importance tables -- deduplicated per geometry and cached across calls;
+//   2. packs descriptors + tables into ONE pinned blob and uploads it with
+//      one hipMemcpyAsync;
+//   3. launches the kernels of each stage once for the whole batch (per-image
+//      descriptors, flat tile index -> image by prefix search);
+//   4. reads back the per-image result records.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "fi_internal.h"
+#include "fi_plan.h"
+
+namespace fi {
+// kernels (fi_kernels.hip)
+__global__ void k_rs_v_u8(const ResizeDesc *, const int32_t *, int, const int32_t *, const float *);
+__global__ void k_rs_h_final(const ResizeDesc *, const int32_t *, int, const int32_t *, const float *);
+__global__ void k_rs_h_u8(const ResizeDesc *, const int32_t *, int, const int32_t *, const float *);
+__global__ void k_rs_v_final(const ResizeDesc *, const int32_t *, int, const int32_t *, const float *);
+__global__ void k_rs_copy(const ResizeDesc *, const int32_t *, int);
+__global__ void k_sc_reduce(const ScDesc *, const int32_t *, int);
+__global__ void k_sc_hpass(const ScDesc *, const int32_t *, int, const int32_t *);
+__global__ void k_sc_vpass(const ScDesc *, const int32_t *, int, const int32_t *);
+__global__ void k_sc_maps(const ScDesc *, const int32_t *, int, const ScParamsDev);
+__global__ void k_sc_score(const ScDesc *, const DevCrop *, const double *, CropScore *, ScResult *,
+                           const ScParamsDev);
+__global__ void k_crop_apply(const ApplyDesc *, const int32_t *, int, const DevCrop *, const ScResult *);
+__global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
+}  // namespace fi
+
+using namespace fi;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int set_err(int code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return set_err(FI_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                     __LINE__);                                                                \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+struct Stat {
+  double ms = 0;
+  int64_t launches = 0;
+  double bytes = 0;
+};
+struct TimedRange {
+  std::string name;
+  hipEvent_t a, b;
+  double bytes;
+};
+
+struct fi_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevBuf arena, work, io;
+  void *pinned = nullptr;
+  size_t pinned_cap = 0;
+  bool timing = false;
+  std::map<std::string, Stat> stats;
+  std::vector<hipEvent_t> event_pool;
+  std::vector<TimedRange> pending;
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+  // caches (host planning is deterministic, keyed by geometry)
+  std::map<std::tuple<int, uint64_t, int, int, int, int, int, int>, AxisTable> axis_cache;
+  std::map<std::tuple<int, int, int, int, uint64_t>, ScPlan> sc_cache;
+  std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
+};
+
+static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
+  if (b->cap >= bytes) return FI_OK;
+  if (b->p) hipFree(b->p);
+  b->p = nullptr;
+  b->cap = 0;
+  size_t cap = std::max(bytes + bytes / 4, (size_t)1 << 20);
+  if (hipMalloc(&b->p, cap) != hipSuccess) {
+    b->p = nullptr;
+    return set_err(FI_ENOMEM, "hipMalloc(%zu) failed on device %d", cap, c->device);
+  }
+  b->cap = cap;
+  return FI_OK;
+}
+static int ensure_pinned(fi_ctx *c, size_t bytes) {
+  if (c->pinned_cap >= bytes) return FI_OK;
+  if (c->pinned) hipHostFree(c->pinned);
+  c->pinned = nullptr;
+  c->pinned_cap = 0;
+  size_t cap = std::max(bytes + bytes / 4, (size_t)1 << 20);
+  if (hipHostMalloc(&c->pinned, cap, hipHostMallocDefault) != hipSuccess)
+    return set_err(FI_ENOMEM, "hipHostMalloc(%zu) failed", cap);
+  c->pinned_cap = cap;
+  return FI_OK;
+}
+
+static hipEvent_t get_event(fi_ctx *c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+struct Timer {
+  fi_ctx *c;
+  TimedRange r;
+  bool on;
+  Timer(fi_ctx *c_, const char *name, double bytes) : c(c_), on(c_->timing) {
+    if (!on) return;
+    r.name = name;
+    r.bytes = bytes;
+    r.a = get_event(c);
+    r.b = get_event(c);
+    hipEventRecord(r.a, c->stream);
+  }
+  ~Timer() {
+    if (!on) return;
+    hipEventRecord(r.b, c->stream);
+    c->pending.push_back(r);
+  }
+};
+static void collect_timers(fi_ctx *c) {
+  for (auto &r : c->pending) {
+    float ms = 0;
+    hipEventSynchronize(r.b);
+    hipEventElapsedTime(&ms, r.a, r.b);
+    Stat &s = c->stats[r.name];
+    s.ms += ms;
+    s.launches += 1;
+    s.bytes += r.bytes;
+    c->event_pool.push_back(r.a);
+    c->event_pool.push_back(r.b);
+  }
+  c->pending.clear();
+}
+
+// ---------------------------------------------------------------------------
+// upload blob
+// ---------------------------------------------------------------------------
+struct Blob {
+  std::vector<uint8_t> b;
+  size_t add(const void *p, size_t n, size_t align = 256) {
+    size_t off = (b.size() + align - 1) / align * align;
+    b.resize(off + n);
+    if (n) memcpy(b.data() + off, p, n);
+    return off;
+  }
+  template <class T>
+  size_t addv(const std::vector<T> &v) {
+    return add(v.data(), v.size() * sizeof(T));
+  }
+};
+struct Work {  // workspace sub-allocator (device offsets)
+  size_t size = 0;
+  size_t take(size_t n, size_t align = 256) {
+    size_t off = (size + align - 1) / align * align;
+    size = off + n;
+    return off;
+  }
+};
+
+static uint64_t dbits(double d) {
+  uint64_t u;
+  memcpy(&u, &d, 8);
+  return u;
+}
+
+static ScParamsDev to_dev(const fi_smartcrop_params &p) {
+  ScParamsDev d{};
+  d.detail_weight = p.detail_weight;
+  d.edge_radius = p.edge_radius;
+  d.edge_weight = p.edge_weight;
+  d.outside_importance = p.outside_importance;
+  d.saturation_bias = p.saturation_bias;
+  d.saturation_brightness_max = p.saturation_brightness_max;
+  d.saturation_brightness_min = p.saturation_brightness_min;
+  d.saturation_threshold = p.saturation_threshold;
+  d.saturation_weight = p.saturation_weight;
+  d.skin_bias = p.skin_bias;
+  d.skin_brightness_max = p.skin_brightness_max;
+  d.skin_brightness_min = p.skin_brightness_min;
+  for (int i = 0; i < 3; i++) d.skin_color[i] = p.skin_color[i];
+  d.skin_threshold = p.skin_threshold;
+  d.skin_weight = p.skin_weight;
+  d.rule_of_thirds = p.rule_of_thirds;
+  return d;
+}
+static uint64_t params_hash(const fi_smartcrop_params &p) {
+  const uint8_t *b = reinterpret_cast<const uint8_t *>(&p);
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < sizeof p; i++) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+
+// ---------------------------------------------------------------------------
+// batch executor
+// ---------------------------------------------------------------------------
+struct ScItem {       // one smartcrop job
+  const uint8_t *img;  // device
+  int64_t stride;
+  int W, H, C;
+  int tw, th;
+  int result;          // index into results
+  fi_smartcrop_options opt;
+};
+
+struct Exec {
+  fi_ctx *c;
+  Blob blob;
+  Work work;
+  std::vector<int32_t> ai;
+  std::vector<float> af;
+  std::vector<double> ad;
+  fi_smartcrop_params params;
+};
+
+static void add_axis(fi_ctx *c, Exec &E, int filter, double factor, int in_sampled, int out_size, int o0, int o1,
+                     bool sample, int in_src, DevAxis *out, std::map<const AxisTable *, DevAxis> &placed) {
+  auto key = std::make_tuple(filter, dbits(factor), in_sampled, out_size, o0, o1, (int)sample, in_src);
+  auto it = c->axis_cache.find(key);
+  if (it == c->axis_cache.end()) {
+    if (c->axis_cache.size() > 4096) c->axis_cache.clear();
+    AxisTable t;
+    build_axis(filter, factor, in_sampled, out_size, o0, o1, sample, in_src, &t);
+    it = c->axis_cache.emplace(key, std::move(t)).first;
+  }
+  const AxisTable *t = &it->second;
+  auto pit = placed.find(t);
+  if (pit != placed.end()) {
+    *out = pit->second;
+    return;
+  }
+  DevAxis d{};
+  d.n = (int32_t)t->start.size();
+  d.start = (int32_t)E.ai.size();
+  E.ai.insert(E.ai.end(), t->start.begin(), t->start.end());
+  d.count = (int32_t)E.ai.size();
+  E.ai.insert(E.ai.end(), t->count.begin(), t->count.end());
+  d.woff = (int32_t)E.ai.size();
+  const int32_t wbase = (int32_t)E.af.size();
+  for (int32_t w : t->woff) E.ai.push_back(w + wbase);
+  E.af.insert(E.af.end(), t->w.begin(), t->w.end());
+  d.maxtaps = t->maxtaps;
+  d.src_lo = t->src_lo;
+  d.src_hi = t->src_hi;
+  placed[t] = d;
+  *out = d;
+}
+
+struct ScLaunchData {
+  std::vector<ScDesc> descs;
+  std::vector<DevCrop> crops;
+  int ncrop_total = 0;
+  // per image: where its crops live, for result decoding
+  std::vector<const ScPlan *> plans;
+};
+
+// Plan the smartcrop stage of `items` into E (descriptors, crops, tables,
+// workspace).  Returns FI_OK or per-item status in status[].
+static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items, ScLaunchData *L,
+                           std::vector<int> *status, std::vector<std::string> *errs) {
+  const uint64_t ph = params_hash(E.params);
+  std::map<std::pair<const std::vector<double> *, int>, int32_t> imp_placed;
+  std::map<const ScPlan *, std::tuple<int32_t, int32_t, int32_t, int32_t>> tab_placed;
+  for (size_t k = 0; k < items.size(); k++) {
+    const ScItem &it = items[k];
+    const fi_smartcrop_options &o = it.opt;
+    uint64_t okey = dbits(o.max_scale) ^ (dbits(o.min_scale) * 3) ^ (dbits(o.scale_step) * 7) ^
+                    ((uint64_t)o.step << 40) ^ ((uint64_t)o.prescale << 56);
+    auto key = std::make_tuple(it.W, it.H, it.tw, it.th, okey);
+    auto pit = c->sc_cache.find(key);
+    if (pit == c->sc_cache.end()) {
+      if (c->sc_cache.size() > 4096) c->sc_cache.clear();
+      ScPlan p;
+      plan_sc(it.W, it.H, it.tw, it.th, o, &p);
+      pit = c->sc_cache.emplace(key, std::move(p)).first;
+    }
+    const ScPlan &P = pit->second;
+    L->plans.push_back(&P);
+    if (P.status != FI_OK) {
+      (*status)[k] = P.status;
+      (*errs)[k] = P.err;
+      L->descs.push_back(ScDesc{});
+      L->descs.back().ncrops = 0;
+      L->descs.back().result = it.result;
+      continue;
+    }
+    ScDesc d{};
+    d.img = it.img;
+    d.stride = it.stride;
+    d.W = it.W;
+    d.H = it.H;
+    d.C = it.C;
+    d.fx = P.fx;
+    d.fy = P.fy;
+    d.rw = P.rw;
+    d.rh = P.rh;
+    d.need_h = P.need_h;
+    d.need_v = P.need_v;
+    d.aw = P.aw;
+    d.ah = P.ah;
+    d.ybox_first = P.ybox_first;
+    d.hrows = P.hrows;
+    d.ksh = P.ksh;
+    d.ksv = P.ksv;
+    d.prescale = P.prescale;
+    d.result = it.result;
+    d.exact_all = o.exact_all;
+    if (P.thumb) {
+      auto tp = tab_placed.find(&P);
+      if (tp == tab_placed.end()) {
+        int32_t hb = (int32_t)E.ai.size();
+        E.ai.insert(E.ai.end(), P.hb.begin(), P.hb.end());
+        int32_t hk = (int32_t)E.ai.size();
+        E.ai.insert(E.ai.end(), P.hk.begin(), P.hk.end());
+        int32_t vb = (int32_t)E.ai.size();
+        E.ai.insert(E.ai.end(), P.vb.begin(), P.vb.end());
+        int32_t vk = (int32_t)E.ai.size();
+        E.ai.insert(E.ai.end(), P.vk.begin(), P.vk.end());
+        tp = tab_placed.emplace(&P, std::make_tuple(hb, hk, vb, vk)).first;
+      }
+      d.hb = std::get<0>(tp->second);
+      d.hk = std::get<1>(tp->second);
+      d.vb = std::get<2>(tp->second);
+      d.vk = std::get<3>(tp->second);
+      // workspace (offsets; converted to pointers after allocation)
+      d.red = (P.fx > 1 || P.fy > 1) ? (uint8_t *)(uintptr_t)(E.work.take((size_t)P.rw * P.rh * 3) + 1) : nullptr;
+      d.hbuf = P.need_h ? (uint8_t *)(uintptr_t)(E.work.take((size_t)P.aw * std::max(P.hrows, 1) * 3) + 1) : nullptr;
+      d.pre = (uint8_t *)(uintptr_t)(E.work.take((size_t)P.aw * P.ah * 3) + 1);
+    }
+    d.maps = (uint32_t *)(uintptr_t)(E.work.take((size_t)P.aw * P.ah * 4) + 1);
+    d.crop0 = L->ncrop_total;
+    d.ncrops = (int32_t)P.crops.size();
+    // crops + importance tables (one table per distinct window size)
+    std::map<std::pair<uint64_t, uint64_t>, std::pair<int, int>> sizes;
+    for (const CropHost &ch : P.crops) {
+      auto &e = sizes[{dbits(ch.fw), dbits(ch.fh)}];
+      e.first = std::max(e.first, ch.nin_x);
+      e.second = std::max(e.second, ch.nin_y);
+    }
+    std::map<std::pair<uint64_t, uint64_t>, std::pair<int32_t, int32_t>> tab_of;
+    for (auto &s : sizes) {
+      double fw, fh;
+      memcpy(&fw, &s.first.first, 8);
+      memcpy(&fh, &s.first.second, 8);
+      const int nx = std::max(s.second.first, 1), ny = std::max(s.second.second, 1);
+      auto ikey = std::make_tuple(s.first.first, s.first.second, nx, ny, ph);
+      auto iit = c->imp_cache.find(ikey);
+      if (iit == c->imp_cache.end()) {
+        if (c->imp_cache.size() > 1024) c->imp_cache.clear();
+        std::vector<double> t;
+        sc_importance_table(E.params, fw, fh, nx, ny, &t);
+        iit = c->imp_cache.emplace(ikey, std::move(t)).first;
+      }
+      auto pk = std::make_pair(&iit->second, nx);
+      auto ip = imp_placed.find(pk);
+      int32_t off;
+      if (ip == imp_placed.end()) {
+        off = (int32_t)E.ad.size();
+        E.ad.insert(E.ad.end(), iit->second.begin(), iit->second.end());
+        imp_placed[pk] = off;
+      } else {
+        off = ip->second;
+      }
+      tab_of[s.first] = {off, nx};
+    }
+    for (const CropHost &ch : P.crops) {
+      DevCrop dc{};
+      dc.fx = ch.fx;
+      dc.fy = ch.fy;
+      dc.fw = ch.fw;
+      dc.fh = ch.fh;
+      dc.x0 = ch.x0;
+      dc.y0 = ch.y0;
+      dc.nin_x = ch.nin_x;
+      dc.nin_y = ch.nin_y;
+      auto t = tab_of[{dbits(ch.fw), dbits(ch.fh)}];
+      dc.table = t.first;
+      dc.table_w = t.second;
+      dc.rx = ch.rx;
+      dc.ry = ch.ry;
+      dc.rw = ch.rw;
+      dc.rh = ch.rh;
+      L->crops.push_back(dc);
+    }
+    L->ncrop_total += d.ncrops;
+    L->descs.push_back(d);
+  }
+}
+
+template <class D>
+static void fix_ptr(D *&p, uint8_t *base) {
+  if (p) p = reinterpret_cast<D *>(base + ((uintptr_t)p - 1));
+}
+
+struct Launch {  // one kernel launch over a subset of descriptors
+  size_t desc_off = 0, prefix_off = 0;
+  int n = 0, tiles = 0;
+};
+template <class Desc, class TileFn>
+static Launch add_launch(Blob &blob, const std::vector<Desc> &all, const std::vector<int> &members, TileFn tiles) {
+  Launch L;
+  std::vector<Desc> sub;
+  std::vector<int32_t> prefix;
+  int32_t acc = 0;
+  for (int m : members) {
+    const int t = tiles(all[m]);
+    if (t <= 0) continue;
+    sub.push_back(all[m]);
+    prefix.push_back(acc);
+    acc += t;
+  }
+  prefix.push_back(acc);
+  L.n = (int)sub.size();
+  L.tiles = acc;
+  L.desc_off = blob.addv(sub);
+  L.prefix_off = blob.addv(prefix);
+  return L;
+}
+
+// Enqueue smartcrop kernels for a planned batch.
+struct ScRun {
+  Launch red, hp, vp, maps;
+  size_t desc_all = 0, crops_off = 0;
+  size_t results_off = 0, scores_off = 0;  // workspace
+  int n = 0;
+};
+
+static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) {
+  (void)device_ptrs_ok;
+  Exec E;
+  E.c = c;
+  fi_smartcrop_default_params(&E.params);
+  std::vector<ImPlan> plans(n);
+  std::vector<int> status(n, FI_OK);
+  std::vector<std::string> errs(n);
+  std::vector<ResizeDesc> rd;
+  std::vector<int> rd_of(n, -1);
+  std::vector<ScItem> sitems;
+  std::vector<int> sc_of(n, -1);
+  std::map<const AxisTable *, DevAxis> placed;
+  // per image resized-buffer workspace offsets (for smartcrop-apply)
+  std::vector<size_t> res_off(n, 0);
+  double resize_bytes = 0, sc_bytes = 0;
+  for (int i = 0; i < n; i++) {
+    fi_image &im = imgs[i];
+    int rc = plan_im(im, &plans[i]);
+    const ImPlan &P = plans[i];
+    if (rc != FI_OK) {
+      status[i] = rc;
+      errs[i] = P.err;
+      continue;
+    }
+    if (!im.src) {
+      status[i] = FI_EINVAL;
+      errs[i] = "src is NULL";
+      continue;
+    }
+    const bool smc = (im.flags & FI_OP_SMARTCROP) != 0;
+    const bool apply = smc && (im.flags & FI_OP_SMARTCROP_APPLY);
+    im.out_w = P.out_w;
+    im.out_h = P.out_h;
+    im.out_channels = P.out_c;
+    im.out_stride = P.out_w * P.out_c;
+    const int64_t need = (int64_t)im.out_stride * im.out_h;
+    if (!im.dst || im.dst_capacity < need) {
+      status[i] = FI_ECAPACITY;
+      errs[i] = "dst NULL or dst_capacity < out_stride*out_h";
+      continue;
+    }
+    ResizeDesc d{};
+    d.src = im.src;
+    d.src_stride = im.src_stride;
+    d.C = 3;
+    d.ew = P.ew;
+    d.eh = P.eh;
+    d.ex0 = P.ex0;
+    d.ey0 = P.ey0;
+    d.gray = P.gray;
+    d.rot = P.rot;
+    d.out_w = P.out_w;
+    d.out_h = P.out_h;
+    d.out_c = P.out_c;
+    d.dst_stride = im.out_stride;
+    if (apply) {
+      res_off[i] = E.work.take((size_t)need);
+      d.dst = (uint8_t *)(uintptr_t)(res_off[i] + 1);  // workspace, fixed below
+    } else {
+      d.dst = im.dst;
+    }
+    int64_t src_bytes;
+    if (!P.resize) {
+      d.mode = 0;
+      src_bytes = (int64_t)P.ew * P.eh * 3;
+    } else {
+      add_axis(c, E, P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &d.v, placed);
+      add_axis(c, E, P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &d.h, placed);
+      if (!P.hfirst) {
+        d.mode = 1;
+        const int64_t b_lo = (int64_t)3 * d.h.src_lo / 8 * 8;
+        const int64_t b_hi = std::min<int64_t>((int64_t)3 * P.W, ((int64_t)3 * d.h.src_hi + 7) / 8 * 8);
+        d.mid_c0 = (int32_t)b_lo;
+        d.mid_cols = (int32_t)(b_hi - b_lo);
+        d.mid_rows = P.eh;
+        d.mid_stride = (d.mid_cols + 7) / 8 * 8;
+      } else {
+        d.mode = 2;
+        d.mid_r0 = d.v.src_lo;
+        d.mid_rows = d.v.src_hi - d.v.src_lo;
+        d.mid_cols = P.ew;
+        d.mid_stride = (3 * P.ew + 7) / 8 * 8;
+      }
+      d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
+      src_bytes = (int64_t)(d.v.src_hi - d.v.src_lo) * (d.h.src_hi - d.h.src_lo) * 3;
+    }
+    resize_bytes += (double)src_bytes + (double)need;
+    rd_of[i] = (int)rd.size();
+    rd.push_back(d);
+    if (smc) {
+      ScItem it{};
+      it.img = (const uint8_t *)(uintptr_t)0;  // resolved after workspace allocation
+      it.stride = im.out_stride;
+      it.W = P.out_w;
+      it.H = P.out_h;
+      it.C = P.out_c;
+      it.tw = im.smartcrop_w > 0 ? im.smartcrop_w : 100;
+      it.th = im.smartcrop_h > 0 ? im.smartcrop_h : 100;
+      it.result = (int)sitems.size();
+      fi_smartcrop_default_options(&it.opt);
+      sc_of[i] = (int)sitems.size();
+      sitems.push_back(it);
+      sc_bytes += (double)need + 16.0;
+    }
+  }
+  // smartcrop planning
+  ScLaunchData SL;
+  std::vector<int> sstatus(sitems.size(), FI_OK);
+  std::vector<std::string> serrs(sitems.size());
+  for (int i = 0; i < n; i++)
+    if (sc_of[i] >= 0) {
+      // smartcrop input: the resized image (workspace if apply, else dst)
+      ScItem &it = sitems[sc_of[i]];
+      const ResizeDesc &d = rd[rd_of[i]];
+      it.img = d.dst;  // may still be a workspace offset (+1 tagged); fixed below
+    }
+  plan_smartcrop(c, E, sitems, &SL, &sstatus, &serrs);
+  const size_t results_off = E.work.take(sizeof(ScResult) * std::max<size_t>(sitems.size(), 1));
+  const size_t scores_off = E.work.take(sizeof(CropScore) * std::max(SL.ncrop_total, 1));
+  const size_t outwh_off = E.work.take(sizeof(int32_t) * 2 * std::max(n, 1));
+  int rc = ensure(c, &c->work, E.work.size + 256);
+  if (rc) return rc;
+  uint8_t *wb = (uint8_t *)c->work.p;
+  // resolve tagged workspace offsets
+  for (int i = 0; i < n; i++) {
+    if (rd_of[i] < 0) continue;
+    ResizeDesc &d = rd[rd_of[i]];
+    if (d.mid) fix_ptr(d.mid, wb);
+    const bool apply = (imgs[i].flags & FI_OP_SMARTCROP) && (imgs[i].flags & FI_OP_SMARTCROP_APPLY);
+    if (apply) fix_ptr(d.dst, wb);
+  }
+  for (size_t k = 0; k < SL.descs.size(); k++) {
+    ScDesc &d = SL.descs[k];
+    fix_ptr(d.red, wb);
+    fix_ptr(d.hbuf, wb);
+    fix_ptr(d.pre, wb);
+    fix_ptr(d.maps, wb);
+  }
+  for (int i = 0; i < n; i++)
+    if (sc_of[i] >= 0) SL.descs[sc_of[i]].img = rd[rd_of[i]].dst;
+  // ---- build launches
+  std::vector<int> m0, m1, m2;
+  for (size_t k = 0; k < rd.size(); k++) (rd[k].mode == 0 ? m0 : rd[k].mode == 1 ? m1 : m2).push_back((int)k);
+  Blob &B = E.blob;
+  auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
+  auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
+  Launch L0 = add_launch(B, rd, m0, eh_tiles);
+  Launch L1a = add_launch(B, rd, m1, eh_tiles);
+  Launch L2a = add_launch(B, rd, m2, mid_tiles);
+  Launch L2b = add_launch(B, rd, m2, eh_tiles);
+  std::vector<int> sall, sred, shp, svp;
+  for (size_t k = 0; k < SL.descs.size(); k++) {
+    if (sstatus[k] != FI_OK) continue;
+    const ScDesc &d = SL.descs[k];
+    sall.push_back((int)k);
+    if (d.red) sred.push_back((int)k);
+    if (d.hbuf) shp.push_back((int)k);
+    if (d.pre) svp.push_back((int)k);
+  }
+  Launch Sred = add_launch(B, SL.descs, sred, [](const ScDesc &d) { return d.rh; });
+  Launch Shp = add_launch(B, SL.descs, shp, [](const ScDesc &d) { return d.hrows; });
+  Launch Svp = add_launch(B, SL.descs, svp, [](const ScDesc &d) { return d.ah; });
+  Launch Smaps = add_launch(B, SL.descs, sall, [](const ScDesc &d) { return d.ah; });
+  std::vector<ScDesc> score_descs;
+  for (int k : sall) score_descs.push_back(SL.descs[k]);
+  const size_t score_desc_off = B.addv(score_descs);
+  const size_t crops_off = B.addv(SL.crops);
+  std::vector<ApplyDesc> apply;
+  std::vector<int> apply_img;
+  for (int i = 0; i < n; i++) {
+    if (rd_of[i] < 0 || sc_of[i] < 0) continue;
+    if (!(imgs[i].flags & FI_OP_SMARTCROP_APPLY)) continue;
+    if (sstatus[sc_of[i]] != FI_OK) continue;
+    const ResizeDesc &d = rd[rd_of[i]];
+    ApplyDesc a{};
+    a.src = d.dst;
+    a.src_stride = d.dst_stride;
+    a.W = d.out_w;
+    a.H = d.out_h;
+    a.C = d.out_c;
+    a.result = sc_of[i];
+    a.crop0 = SL.descs[sc_of[i]].crop0;
+    a.dst = imgs[i].dst;
+    a.out_wh = (int32_t *)(wb + outwh_off + 8 * (size_t)i);
+    apply.push_back(a);
+    apply_img.push_back(i);
+  }
+  std::vector<int> all_apply(apply.size());
+  for (size_t k = 0; k < apply.size(); k++) all_apply[k] = (int)k;
+  Launch Lap = add_launch(B, apply, all_apply, [](const ApplyDesc &a) { return a.H; });
+  const size_t ai_off = B.addv(E.ai), af_off = B.addv(E.af), ad_off = B.addv(E.ad);
+  // ---- upload
+  rc = ensure(c, &c->arena, B.b.size() + 256);
+  if (rc) return rc;
+  rc = ensure_pinned(c, B.b.size() + 256);
+  if (rc) return rc;
+  memcpy(c->pinned, B.b.data(), B.b.size());
+  HIP_TRY(hipMemcpyAsync(c->arena.p, c->pinned, B.b.size(), hipMemcpyHostToDevice, c->stream));
+  uint8_t *ab = (uint8_t *)c->arena.p;
+  const int32_t *ai = (const int32_t *)(ab + ai_off);
+  const float *af = (const float *)(ab + af_off);
+  const double *ad = (const double *)(ab + ad_off);
+  const ScParamsDev PD = to_dev(E.params);
+  auto desc_p = [&](const Launch &L) { return ab + L.desc_off; };
+  auto pre_p = [&](const Launch &L) { return (const int32_t *)(ab + L.prefix_off); };
+  // ---- resample kernels
+  {
+    Timer tb(c, "batch", 0);
+    {
+      Timer t(c, "resize", resize_bytes);
+      if (L0.tiles)
+        hipLaunchKernelGGL(k_rs_copy, dim3(L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L0),
+                           pre_p(L0), L0.n);
+      if (L1a.tiles) {
+        hipLaunchKernelGGL(k_rs_v_u8, dim3(L1a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L1a),
+                           pre_p(L1a), L1a.n, ai, af);
+        hipLaunchKernelGGL(k_rs_h_final, dim3(L1a.tiles), dim3(256), 0, c->stream,
+                           (const ResizeDesc *)desc_p(L1a), pre_p(L1a), L1a.n, ai, af);
+      }
+      if (L2a.tiles) {
+        hipLaunchKernelGGL(k_rs_h_u8, dim3(L2a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L2a),
+                           pre_p(L2a), L2a.n, ai, af);
+        hipLaunchKernelGGL(k_rs_v_final, dim3(L2b.tiles), dim3(256), 0, c->stream,
+                           (const ResizeDesc *)desc_p(L2b), pre_p(L2b), L2b.n, ai, af);
+      }
+    }
+    HIP_TRY(hipGetLastError());
+    if (!score_descs.empty()) {
+      {
+        Timer t(c, "sc_prescale", 0);
+        if (Sred.tiles)
+          hipLaunchKernelGGL(k_sc_reduce, dim3(Sred.tiles), dim3(256), 0, c->stream, (const ScDesc *)desc_p(Sred),
+                             pre_p(Sred), Sred.n);
+        if (Shp.tiles)
+          hipLaunchKernelGGL(k_sc_hpass, dim3(Shp.tiles), dim3(256), 0, c->stream, (const ScDesc *)desc_p(Shp),
+                             pre_p(Shp), Shp.n, ai);
+        if (Svp.tiles)
+          hipLaunchKernelGGL(k_sc_vpass, dim3(Svp.tiles), dim3(256), 0, c->stream, (const ScDesc *)desc_p(Svp),
+                             pre_p(Svp), Svp.n, ai);
+      }
+      {
+        Timer t(c, "sc_maps", 0);
+        hipLaunchKernelGGL(k_sc_maps, dim3(Smaps.tiles), dim3(256), 0, c->stream, (const ScDesc *)desc_p(Smaps),
+                           pre_p(Smaps), Smaps.n, PD);
+      }
+      {
+        Timer t(c, "sc_score", 0);
+        hipLaunchKernelGGL(k_sc_score, dim3((unsigned)score_descs.size()), dim3(256), 0, c->stream,
+                           (const ScDesc *)(ab + score_desc_off), (const DevCrop *)(ab + crops_off), ad,
+                           (CropScore *)(wb + scores_off), (ScResult *)(wb + results_off), PD);
+      }
+      if (Lap.tiles) {
+        Timer t(c, "crop_apply", 0);
+        hipLaunchKernelGGL(k_crop_apply, dim3(Lap.tiles), dim3(256), 0, c->stream, (const ApplyDesc *)desc_p(Lap),
+                           pre_p(Lap), Lap.n, (const DevCrop *)(ab + crops_off), (const ScResult *)(wb + results_off));
+      }
+      HIP_TRY(hipGetLastError());
+    }
+  }
+  // ---- results
+  std::vector<ScResult> res(sitems.size());
+  std::vector<int32_t> outwh(2 * (size_t)std::max(n, 1), 0);
+  if (!sitems.empty())
+    HIP_TRY(hipMemcpyAsync(res.data(), wb + results_off, sizeof(ScResult) * res.size(), hipMemcpyDeviceToHost,
+                           c->stream));
+  if (!apply.empty())
+    HIP_TRY(hipMemcpyAsync(outwh.data(), wb + outwh_off, sizeof(int32_t) * 2 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  collect_timers(c);
+  int first_bad = FI_OK;
+  std::string first_err;
+  for (int i = 0; i < n; i++) {
+    fi_image &im = imgs[i];
+    im.n_candidates = 0;
+    if (status[i] == FI_OK && sc_of[i] >= 0) {
+      const int k = sc_of[i];
+      if (sstatus[k] != FI_OK) {
+        status[i] = sstatus[k];
+        errs[i] = serrs[k];
+      } else {
+        const ScResult &r = res[k];
+        if (r.top < 0) {
+          status[i] = FI_EUNSUPPORTED;
+          errs[i] = "smartcrop: too many crop windows for the scoring kernel";
+        } else {
+          const DevCrop &dc = SL.crops[SL.descs[k].crop0 + r.top];
+          im.crop_x = dc.rx;
+          im.crop_y = dc.ry;
+          im.crop_w = dc.rw;
+          im.crop_h = dc.rh;
+          im.crop_score = r.total;
+          im.n_candidates = r.n_candidates;
+          if (im.flags & FI_OP_SMARTCROP_APPLY) {
+            im.out_w = outwh[2 * i];
+            im.out_h = outwh[2 * i + 1];
+            im.out_stride = im.out_w * im.out_channels;
+          }
+        }
+      }
+    }
+    im.status = status[i];
+    if (status[i] != FI_OK && first_bad == FI_OK) {
+      first_bad = status[i];
+      first_err = "image " + std::to_string(i) + ": " + errs[i];
+    }
+  }
+  if (first_bad != FI_OK) return set_err(first_bad, "%s", first_err.c_str());
+  return FI_OK;
+}
+
+// ---------------------------------------------------------------------------
+// smartcrop-only path (fi_smartcrop / fi_smartcrop_ex)
+// ---------------------------------------------------------------------------
+static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t stride, int C, int tw, int th,
+                         const fi_smartcrop_params &params, const fi_smartcrop_options &opt,
+                         std::vector<CropScore> *scores, ScResult *result, ScPlan *plan_out,
+                         std::vector<uint8_t> *prescaled, std::vector<uint8_t> *maps) {
+  Exec E;
+  E.c = c;
+  E.params = params;
+  std::vector<ScItem> items(1);
+  items[0].img = d_img;
+  items[0].stride = stride;
+  items[0].W = W;
+  items[0].H = H;
+  items[0].C = C;
+  items[0].tw = tw;
+  items[0].th = th;
+  items[0].result = 0;
+  items[0].opt = opt;
+  ScLaunchData SL;
+  std::vector<int> st(1, FI_OK);
+  std::vector<std::string> errs(1);
+  plan_smartcrop(c, E, items, &SL, &st, &errs);
+  if (st[0] != FI_OK) return set_err(st[0], "%s", errs[0].c_str());
+  if (SL.descs[0].ncrops > 2048) return set_err(FI_EUNSUPPORTED, "smartcrop: %d crop windows (max 2048)", SL.descs[0].ncrops);
+  *plan_out = *SL.plans[0];
+  const size_t results_off = E.work.take(sizeof(ScResult));
+  const size_t scores_off = E.work.take(sizeof(CropScore) * std::max(SL.ncrop_total, 1));
+  int rc = ensure(c, &c->work, E.work.size + 256);
+  if (rc) return rc;
+  uint8_t *wb = (uint8_t *)c->work.p;
+  ScDesc &d = SL.descs[0];
+  fix_ptr(d.red, wb);
+  fix_ptr(d.hbuf, wb);
+  fix_ptr(d.pre, wb);
+  fix_ptr(d.maps, wb);
+  Blob &B = E.blob;
+  std::vector<int> all{0};
+  Launch Sred = add_launch(B, SL.descs, d.red ? all : std::vector<int>{}, [](const ScDesc &x) { return x.rh; });
+  Launch Shp = add_launch(B, SL.descs, d.hbuf ? all : std::vector<int>{}, [](const ScDesc &x) { return x.hrows; });
+  Launch Svp = add_launch(B, SL.descs, d.pre ? all : std::vector<int>{}, [](const ScDesc &x) { return x.ah; });
+  Launch Smaps = add_launch(B, SL.descs, all, [](const ScDesc &x) { return x.ah; });
+  const size_t score_desc_off = B.addv(SL.descs);
+  const size_t crops_off = B.addv(SL.crops);
+  const size_t ai_off = B.addv(E.ai), ad_off = B.addv(E.ad);
+  rc = ensure(c, &c->arena, B.b.size() + 256);
+  if (rc) return rc;
+  rc = ensure_pinned(c, B.b.size() + 256);
+  if (rc) return rc;
+  memcpy(c->pinned, B.b.data(), B.b.size());
+  HIP_TRY(hipMemcpyAsync(c->arena.p, c->pinned, B.b.size(), hipMemcpyHostToDevice, c->stream));
+  uint8_t *ab = (uint8_t *)c->arena.p;
+  const int32_t *ai = (const int32_t *)(ab + ai_off);
+  const double *ad = (const double *)(ab + ad_off);
+  const ScParamsDev PD = to_dev(params);
+  {
+    Timer t(c, "sc_prescale", 0);
+    if (Sred.tiles)
+      hipLaunchKernelGGL(k_sc_reduce, dim3(Sred.tiles), dim3(256), 0, c->stream, (const ScDesc *)(ab + Sred.desc_off),
+                         (const int32_t *)(ab + Sred.prefix_off), Sred.n);
+    if (Shp.tiles)
+      hipLaunchKernelGGL(k_sc_hpass, dim3(Shp.tiles), dim3(256), 0, c->stream, (const ScDesc *)(ab + Shp.desc_off),
+                         (const int32_t *)(ab + Shp.prefix_off), Shp.n, ai);
+    if (Svp.tiles)
+      hipLaunchKernelGGL(k_sc_vpass, dim3(Svp.tiles), dim3(256), 0, c->stream, (const ScDesc *)(ab + Svp.desc_off),
+                         (const int32_t *)(ab + Svp.prefix_off), Svp.n, ai);
+  }
+  {
+    Timer t(c, "sc_maps", 0);
+    hipLaunchKernelGGL(k_sc_maps, dim3(Smaps.tiles), dim3(256), 0, c->stream, (const ScDesc *)(ab + Smaps.desc_off),
+                       (const int32_t *)(ab + Smaps.prefix_off), Smaps.n, PD);
+  }
+  {
+    Timer t(c, "sc_score", 0);
+    hipLaunchKernelGGL(k_sc_score, dim3(1), dim3(256), 0, c->stream, (const ScDesc *)(ab + score_desc_off),
+                       (const DevCrop *)(ab + crops_off), ad, (CropScore *)(wb + scores_off),
+                       (ScResult *)(wb + results_off), PD);
+  }
+  HIP_TRY(hipGetLastError());
+  scores->resize(SL.ncrop_total);
+  HIP_TRY(hipMemcpyAsync(scores->data(), wb + scores_off, sizeof(CropScore) * SL.ncrop_total, hipMemcpyDeviceToHost,
+                         c->stream));
+  HIP_TRY(hipMemcpyAsync(result, wb + results_off, sizeof(ScResult), hipMemcpyDeviceToHost, c->stream));
+  const size_t na = (size_t)d.aw * d.ah;
+  if (prescaled) {
+    prescaled->resize(na * 3);
+    if (d.pre) {
+      HIP_TRY(hipMemcpyAsync(prescaled->data(), d.pre, na * 3, hipMemcpyDeviceToHost, c->stream));
+    } else {
+      // no prescale: the analysed image is the input (C may be 1)
+      std::vector<uint8_t> tmp((size_t)stride * H);
+      HIP_TRY(hipMemcpyAsync(tmp.data(), d_img, tmp.size(), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+          for (int k = 0; k < 3; k++) (*prescaled)[((size_t)y * W + x) * 3 + k] = tmp[(size_t)y * stride + x * C + (C == 3 ? k : 0)];
+    }
+  }
+  std::vector<uint32_t> pm;
+  if (maps) {
+    pm.resize(na);
+    HIP_TRY(hipMemcpyAsync(pm.data(), d.maps, na * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  collect_timers(c);
+  if (maps) {
+    maps->resize(na * 3);
+    for (size_t i = 0; i < na; i++) {
+      (*maps)[i * 3 + 0] = pm[i] & 255;
+      (*maps)[i * 3 + 1] = (pm[i] >> 8) & 255;
+      (*maps)[i * 3 + 2] = (pm[i] >> 16) & 255;
+    }
+  }
+  if (result->top < 0) return set_err(FI_EUNSUPPORTED, "smartcrop: scoring kernel rejected the crop count");
+  return FI_OK;
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int32_t fi_abi_version(void) { return FI_ABI_VERSION; }
+const char *fi_last_error(void) { return g_err.c_str(); }
+
+int fi_device_count(int32_t *count) {
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  *count = n;
+  return FI_OK;
+}
+
+int fi_create(fi_ctx **out, int32_t device) {
+  if (!out) return set_err(FI_EINVAL, "out is NULL");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return set_err(FI_EINVAL, "device %d out of range (%d visible)", device, n);
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(FI_EDEVICE, "device %d is %s; libflyimg_hip.so is built for gfx950 only", device, prop.gcnArchName);
+  fi_ctx *c = new fi_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return set_err(FI_EDEVICE, "hipStreamCreate failed");
+  }
+  *out = c;
+  return FI_OK;
+}
+
+void fi_destroy(fi_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  for (DevBuf *b : {&c->arena, &c->work, &c->io})
+    if (b->p) hipFree(b->p);
+  if (c->pinned) hipHostFree(c->pinned);
+  for (auto e : c->event_pool) hipEventDestroy(e);
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int fi_plan(fi_image *imgs, int32_t n) {
+  if (n < 0 || (n > 0 && !imgs)) return set_err(FI_EINVAL, "bad image array");
+  int first = FI_OK;
+  for (int i = 0; i < n; i++) {
+    ImPlan p;
+    const int rc = plan_im(imgs[i], &p);
+    imgs[i].status = rc;
+    if (rc == FI_OK) {
+      imgs[i].out_w = p.out_w;
+      imgs[i].out_h = p.out_h;
+      imgs[i].out_channels = p.out_c;
+      imgs[i].out_stride = p.out_w * p.out_c;
+    } else if (first == FI_OK) {
+      first = set_err(rc, "image %d: %s", i, p.err.c_str());
+    }
+  }
+  return first;
+}
+
+int fi_process_batch_device(fi_ctx *c, fi_image *imgs, int32_t n) {
+  if (!c || n < 0 || (n > 0 && !imgs)) return set_err(FI_EINVAL, "bad arguments");
+  if (n == 0) return FI_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  return run_batch(c, imgs, n, true);
+}
+
+int fi_process_batch(fi_ctx *c, fi_image *imgs, int32_t n) {
+  if (!c || n < 0 || (n > 0 && !imgs)) return set_err(FI_EINVAL, "bad arguments");
+  if (n == 0) return FI_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  // stage host images into device memory with 16-byte aligned rows
+  std::vector<fi_image> dev(imgs, imgs + n);
+  std::vector<size_t> soff(n), doff(n);
+  size_t total = 0;
+  for (int i = 0; i < n; i++) {
+    fi_image p = imgs[i];
+    ImPlan pl;
+    plan_im(p, &pl);
+    const int64_t sstride = ((int64_t)imgs[i].src_w * 3 + 15) / 16 * 16;
+    soff[i] = total;
+    total += (size_t)std::max<int64_t>(sstride * imgs[i].src_h, 0);
+    total = (total + 255) / 256 * 256;
+    doff[i] = total;
+    total += (size_t)std::max<int64_t>(imgs[i].dst_capacity, 0);
+    total = (total + 255) / 256 * 256;
+    dev[i].src_stride = (int32_t)sstride;
+  }
+  int rc = ensure(c, &c->io, total + 256);
+  if (rc) return rc;
+  uint8_t *io = (uint8_t *)c->io.p;
+  for (int i = 0; i < n; i++) {
+    if (!imgs[i].src || imgs[i].src_w <= 0 || imgs[i].src_h <= 0 || imgs[i].src_channels != 3) {
+      dev[i].src = nullptr;
+      continue;
+    }
+    HIP_TRY(hipMemcpy2DAsync(io + soff[i], dev[i].src_stride, imgs[i].src, imgs[i].src_stride,
+                             (size_t)imgs[i].src_w * 3, imgs[i].src_h, hipMemcpyHostToDevice, c->stream));
+    dev[i].src = io + soff[i];
+    dev[i].dst = imgs[i].dst ? io + doff[i] : nullptr;
+  }
+  rc = run_batch(c, dev.data(), n, true);
+  for (int i = 0; i < n; i++) {
+    fi_image &o = imgs[i];
+    const fi_image &d = dev[i];
+    o.out_w = d.out_w;
+    o.out_h = d.out_h;
+    o.out_channels = d.out_channels;
+    o.out_stride = d.out_stride;
+    o.crop_x = d.crop_x;
+    o.crop_y = d.crop_y;
+    o.crop_w = d.crop_w;
+    o.crop_h = d.crop_h;
+    o.crop_score = d.crop_score;
+    o.status = d.status;
+    o.n_candidates = d.n_candidates;
+    if (d.status == FI_OK && o.dst) {
+      const size_t bytes = (size_t)d.out_stride * d.out_h;
+      if (hipMemcpyAsync(o.dst, io + doff[i], bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return set_err(FI_EDEVICE, "D2H of image %d failed", i);
+    }
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return rc;
+}
+
+void fi_smartcrop_default_params(fi_smartcrop_params *p) {
+  memset(p, 0, sizeof *p);
+  p->detail_weight = 0.2;
+  p->edge_radius = 0.4;
+  p->edge_weight = -10;
+  p->outside_importance = -0.5;
+  p->rule_of_thirds = 1;
+  p->saturation_bias = 0.2;
+  p->saturation_brightness_max = 0.9;
+  p->saturation_brightness_min = 0.05;
+  p->saturation_threshold = 0.4;
+  p->saturation_weight = 0.3;
+  p->score_down_sample = 1;
+  p->skin_bias = 0.01;
+  p->skin_brightness_max = 1;
+  p->skin_brightness_min = 0.2;
+  p->skin_color[0] = 0.78;
+  p->skin_color[1] = 0.57;
+  p->skin_color[2] = 0.44;
+  p->skin_threshold = 0.8;
+  p->skin_weight = 1.8;
+}
+void fi_smartcrop_default_options(fi_smartcrop_options *o) {
+  memset(o, 0, sizeof *o);
+  o->prescale = 1;
+  o->max_scale = 1;
+  o->min_scale = 0.9;
+  o->scale_step = 0.1;
+  o->step = 8;
+  o->exact_all = 0;
+}
+
+int fi_smartcrop_ex(fi_ctx *c, const uint8_t *rgb, int32_t w, int32_t h, int32_t stride, int32_t tw, int32_t th,
+                    const fi_smartcrop_params *params, const fi_smartcrop_options *opts, fi_crop_score *crops,
+                    int32_t crops_cap, int32_t *n_crops, int32_t *top_index, int32_t analyse_wh[2], double *prescale,
+                    uint8_t *prescaled_out, uint8_t *maps_out, int64_t out_cap) {
+  if (!c || !rgb || w <= 0 || h <= 0 || stride < 3 * w) return set_err(FI_EINVAL, "bad image arguments");
+  fi_smartcrop_params P;
+  fi_smartcrop_default_params(&P);
+  if (params) P = *params;
+  if (P.score_down_sample != 1) return set_err(FI_EUNSUPPORTED, "score_down_sample != 1 is not supported");
+  fi_smartcrop_options O;
+  fi_smartcrop_default_options(&O);
+  if (opts) O = *opts;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t dstride = ((int64_t)w * 3 + 15) / 16 * 16;
+  int rc = ensure(c, &c->io, (size_t)dstride * h + 256);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy2DAsync(c->io.p, dstride, rgb, stride, (size_t)w * 3, h, hipMemcpyHostToDevice, c->stream));
+  std::vector<CropScore> scores;
+  ScResult res{};
+  ScPlan plan;
+  std::vector<uint8_t> pre, maps;
+  rc = run_smartcrop(c, (const uint8_t *)c->io.p, w, h, dstride, 3, tw, th, P, O, &scores, &res, &plan,
+                     prescaled_out ? &pre : nullptr, maps_out ? &maps : nullptr);
+  if (rc) return rc;
+  const int nc = (int)plan.crops.size();
+  if (n_crops) *n_crops = nc;
+  if (top_index) *top_index = res.top;
+  if (analyse_wh) {
+    analyse_wh[0] = plan.aw;
+    analyse_wh[1] = plan.ah;
+  }
+  if (prescale) *prescale = plan.prescale;
+  if (crops) {
+    for (int k = 0; k < nc && k < crops_cap; k++) {
+      const CropHost &ch = plan.crops[k];
+      fi_crop_score &o = crops[k];
+      o.x = ch.rx;
+      o.y = ch.ry;
+      o.width = ch.rw;
+      o.height = ch.rh;
+      o.fx = ch.fx;
+      o.fy = ch.fy;
+      o.fw = ch.fw;
+      o.fh = ch.fh;
+      o.detail = scores[k].detail;
+      o.saturation = scores[k].saturation;
+      o.skin = scores[k].skin;
+      o.total = scores[k].total;
+      o.exact = scores[k].exact;
+      o.pad = 0;
+    }
+  }
+  const size_t na = (size_t)plan.aw * plan.ah * 3;
+  if (prescaled_out) {
+    if ((int64_t)na > out_cap) return set_err(FI_ECAPACITY, "out_cap < analyse_w*analyse_h*3");
+    memcpy(prescaled_out, pre.data(), na);
+  }
+  if (maps_out) {
+    if ((int64_t)na > out_cap) return set_err(FI_ECAPACITY, "out_cap < analyse_w*analyse_h*3");
+    memcpy(maps_out, maps.data(), na);
+  }
+  return FI_OK;
+}
+
+int fi_smartcrop(fi_ctx *c, const uint8_t *rgb, int32_t w, int32_t h, int32_t stride, int32_t tw, int32_t th,
+                 const fi_smartcrop_params *params, int32_t out_xywh[4], double *out_score) {
+  int32_t n = 0, top = -1;
+  int32_t awh[2];
+  double pre;
+  // crops are needed to decode the top index
+  std::vector<fi_crop_score> crops(1);
+  {
+    // first call with a small buffer just to learn the crop count is wasteful;
+    // the planner is cheap, so plan here directly
+    fi_smartcrop_options O;
+    fi_smartcrop_default_options(&O);
+    ScPlan p;
+    if (plan_sc(w, h, tw, th, O, &p) != FI_OK) return set_err(p.status, "%s", p.err.c_str());
+    crops.resize(p.crops.size());
+  }
+  int rc = fi_smartcrop_ex(c, rgb, w, h, stride, tw, th, params, nullptr, crops.data(), (int32_t)crops.size(), &n,
+                           &top, awh, &pre, nullptr, nullptr, 0);
+  if (rc) return rc;
+  if (top < 0 || top >= n) return set_err(FI_EDEVICE, "smartcrop: no top crop");
+  out_xywh[0] = crops[top].x;
+  out_xywh[1] = crops[top].y;
+  out_xywh[2] = crops[top].width;
+  out_xywh[3] = crops[top].height;
+  if (out_score) *out_score = crops[top].total;
+  return FI_OK;
+}
+
+int fi_device_malloc(fi_ctx *c, void **ptr, uint64_t bytes) {
+  if (!c || !ptr) return set_err(FI_EINVAL, "bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  if (hipMalloc(ptr, bytes) != hipSuccess) return set_err(FI_ENOMEM, "hipMalloc(%llu) failed", (unsigned long long)bytes);
+  return FI_OK;
+}
+int fi_device_free(fi_ctx *c, void *ptr) {
+  if (!c) return set_err(FI_EINVAL, "bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipFree(ptr));
+  return FI_OK;
+}
+int fi_memcpy_h2d(fi_ctx *c, void *dst, const void *src, uint64_t bytes) {
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return FI_OK;
+}
+int fi_memcpy_d2h(fi_ctx *c, void *dst, const void *src, uint64_t bytes) {
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return FI_OK;
+}
+int fi_fill_synthetic(fi_ctx *c, uint8_t *dev, int32_t w, int32_t h, int32_t stride, uint32_t seed) {
+  if (!c || !dev || w <= 0 || h <= 0 || stride < 3 * w) return set_err(FI_EINVAL, "bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t n = (int64_t)w * h;
+  hipLaunchKernelGGL(k_synth, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, dev, w, h, (int64_t)stride,
+                     seed);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return FI_OK;
+}
+
+int fi_set_timing(fi_ctx *c, int32_t enable) {
+  if (!c) return set_err(FI_EINVAL, "ctx is NULL");
+  c->timing = enable != 0;
+  return FI_OK;
+}
+int fi_reset_stats(fi_ctx *c) {
+  if (!c) return set_err(FI_EINVAL, "ctx is NULL");
+  c->stats.clear();
+  return FI_OK;
+}
+int fi_kernel_stats(fi_ctx *c, const char *name, double *total_ms, int64_t *launches, double *bytes) {
+  if (!c || !name) return set_err(FI_EINVAL, "bad arguments");
+  auto it = c->stats.find(name);
+  const Stat s = it == c->stats.end() ? Stat{} : it->second;
+  if (total_ms) *total_ms = s.ms;
+  if (launches) *launches = s.launches;
+  if (bytes) *bytes = s.bytes;
+  return FI_OK;
+}
+
+int fi_rccl_get_unique_id(uint8_t id[128]) {
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return set_err(FI_EDEVICE, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  memcpy(id, &u, 128);
+  return FI_OK;
+}
+int fi_rccl_init(fi_ctx *c, int32_t rank, int32_t world, const uint8_t id[128]) {
+  if (!c || rank < 0 || world < 1 || rank >= world) return set_err(FI_EINVAL, "bad rank/world");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  ncclUniqueId u;
+  memcpy(&u, id, 128);
+  const ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
+  if (r != ncclSuccess) return set_err(FI_EDEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  c->rank = rank;
+  c->world = world;
+  return FI_OK;
+}
+int fi_rccl_gather_records(fi_ctx *c, const fi_record *send, int32_t count, fi_record *recv) {
+  if (!c || !c->comm || count < 0) return set_err(FI_EINVAL, "RCCL not initialised");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bytes = sizeof(fi_record) * (size_t)count;
+  const size_t total = bytes * (1 + (c->rank == 0 ? c->world : 0));
+  int rc = ensure(c, &c->io, total + 256);
+  if (rc) return rc;
+  uint8_t *sb = (uint8_t *)c->io.p, *rb = sb + bytes;
+  HIP_TRY(hipMemcpyAsync(sb, send, bytes, hipMemcpyHostToDevice, c->stream));
+  ncclResult_t r = ncclGroupStart();
+  if (c->rank == 0) {
+    HIP_TRY(hipMemcpyAsync(rb, sb, bytes, hipMemcpyDeviceToDevice, c->stream));
+    for (int p = 1; p < c->world && r == ncclSuccess; p++)
+      r = ncclRecv(rb + bytes * p, bytes, ncclUint8, p, c->comm, c->stream);
+  } else if (r == ncclSuccess) {
+    r = ncclSend(sb, bytes, ncclUint8, 0, c->comm, c->stream);
+  }
+  if (r == ncclSuccess) r = ncclGroupEnd();
+  if (r != ncclSuccess) return set_err(FI_EDEVICE, "RCCL gather: %s", ncclGetErrorString(r));
+  if (c->rank == 0 && recv)
+    HIP_TRY(hipMemcpyAsync(recv, rb, bytes * c->world, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return FI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,136 @@
+// fi_internal.h -- structures shared by the host planner (fi_plan.cpp), the
+// runtime (fi_api.cpp) and the gfx950 kernels (fi_kernels.hip).
+//
+// Data layout in HBM (see DESIGN.md "Data layout"):
+//   * images: RGB8 HWC rows, caller stride;
+//   * one "arena" per batch holding every device-side table: tap tables
+//     (int32 start/count/offset + fp32 weights), Pillow int32 coefficient
+//     tables, crop lists and f64 importance tables -- uploaded with one copy;
+//   * one "workspace" per batch: Q16 intermediates of the generic two-pass
+//     path, resized images feeding smartcrop, prescale scratch, packed maps,
+//     per-crop score slots.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/flyimg_hip.h"
+
+namespace fi {
+
+constexpr int kMaxChannels = 3;
+constexpr int kFusedLanes = 256;  // threads per workgroup of the fused resample kernel
+
+// One separable axis in the *source* index domain (the ImageMagick sample
+// pre-step is folded in by merging taps that map to one source index).
+struct DevAxis {
+  int32_t n;      // output indices covered
+  int32_t start;  // arena offset (int32 units) of start[n]
+  int32_t count;  // arena offset of count[n]
+  int32_t woff;   // arena offset of woff[n] (float units in weight area)
+  int32_t maxtaps;
+  int32_t src_lo;  // min over start
+  int32_t src_hi;  // max over start+count (exclusive)
+  int32_t pad;
+};
+
+// Per-image descriptor of the resample path (generic two-pass kernels and
+// the fused vertical-first kernel).
+struct ResizeDesc {
+  const uint8_t *src;
+  int64_t src_stride;  // bytes
+  int32_t C;           // 3
+  int32_t mode;        // 0 = copy/epilogue only, 1 = V then H, 2 = H then V
+  DevAxis v;           // output rows  (extent window) <- source rows
+  DevAxis h;           // output cols  (extent window) <- source cols
+  uint16_t *mid;       // Q16 intermediate of the generic path
+  int64_t mid_stride;  // elements per row
+  int32_t mid_rows, mid_cols;  // rows x pixels of the intermediate
+  int32_t mid_r0, mid_c0;      // source row/col of intermediate origin
+  int32_t ex0, ey0;            // extent offset (copy mode only)
+  int32_t ew, eh;              // extent (= pre-rotate output) dims
+  int32_t gray, rot;           // epilogue
+  uint8_t *dst;
+  int64_t dst_stride;
+  int32_t out_w, out_h, out_c;  // post-rotate dims
+  int32_t fused_k;              // ring slots for the fused kernel (0 = not fused)
+  int32_t vring;                // arena offset of per-source-row slot weights (fused)
+  int32_t vring_rows;           // number of source rows in ring table
+  int32_t vring_r0;             // first source row
+  int32_t pad2;
+};
+
+// Fused-kernel work item: one (image, column strip, row band).
+struct FusedTile {
+  int32_t image;
+  int32_t x0, x1;      // output columns [x0, x1) of the extent window
+  int32_t y0, y1;      // output rows    [y0, y1)
+  int32_t b0, nbytes;  // source byte range (16-B aligned start, length) of the strip
+  int32_t r0, r1;      // source rows streamed
+};
+
+// smartcrop crop window in the analysed image (smartcrop.py crops()).
+struct DevCrop {
+  double fx, fy, fw, fh;  // as Python holds them
+  int32_t x0, y0;         // integer origin
+  int32_t nin_x, nin_y;   // inside extents (x < fl(x0+fw))
+  int32_t table;          // arena offset (double units) of importance table
+  int32_t table_w;        // row pitch of the table
+  int32_t rx, ry, rw, rh; // rescaled ints (crop() :184-190)
+};
+
+struct ScDesc {
+  const uint8_t *img;  // smartcrop input (resized output or user image)
+  int64_t stride;
+  int32_t W, H, C;     // C = 1 (gray, pasted into RGB) or 3
+  int32_t fx, fy;      // reduce factors (1 = none)
+  int32_t rw, rh;      // reduced dims
+  int32_t need_h, need_v;
+  int32_t aw, ah;      // analysed dims
+  int32_t ybox_first, hrows;
+  int32_t hb, hk, ksh; // arena offsets: H bounds (pairs), H coeffs (int32), ksize
+  int32_t vb, vk, ksv;
+  uint8_t *red;        // reduce scratch rw*rh*3
+  uint8_t *hbuf;       // H-pass scratch aw*hrows*3
+  uint8_t *pre;        // prescaled image aw*ah*3
+  uint32_t *maps;      // packed skin | edge<<8 | sat<<16
+  int32_t crop0, ncrops;  // into the batch crop array
+  double prescale;
+  double T[3];         // unused on host; device scratch
+  int32_t result;      // index into result array
+  int32_t exact_all;
+};
+
+struct ScParamsDev {
+  double detail_weight, edge_radius, edge_weight, outside_importance;
+  double saturation_bias, saturation_brightness_max, saturation_brightness_min,
+      saturation_threshold, saturation_weight;
+  double skin_bias, skin_brightness_max, skin_brightness_min;
+  double skin_color[3];
+  double skin_threshold, skin_weight;
+  int32_t rule_of_thirds;
+  int32_t pad;
+};
+
+struct ScResult {
+  int32_t top;          // index within the image's crops, -1 on failure
+  int32_t n_candidates;
+  double total;
+};
+
+// convert -crop of the smartcrop box (SmartCropProcessor.php:30-34)
+struct ApplyDesc {
+  const uint8_t *src;
+  int64_t src_stride;
+  int32_t W, H, C;
+  int32_t result, crop0;
+  uint8_t *dst;
+  int32_t *out_wh;  // [2] written by the kernel
+};
+
+struct CropScore {  // per crop (batch-global index)
+  double detail, saturation, skin, total;
+  double bound;
+  int32_t exact;
+  int32_t pad;
+};
+
+}  // namespace fi

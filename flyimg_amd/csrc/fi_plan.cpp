@@ -1,0 +1,464 @@
+// fi_plan.cpp -- host planner.  Every floating-point expression mirrors the
+// reference's evaluation order (built with -ffp-contract=off):
+//   * ImageMagick 6.9 geometry.c ParseMetaGeometry / GravityAdjustGeometry,
+//     resize.c ThumbnailImage / SampleImage / ResizeImage contribution lists
+//     (flyimg emits them from ImageProcessor.php:66-110);
+//   * Pillow 12.2 Image.thumbnail/resize/reduce (PIL/Image.py:2831-2915,
+//     :2328-2470) and Resample.c precompute_coeffs, used by
+//     python/smartcrop.py:157-172;
+//   * smartcrop.py crop() geometry (:137-191), crops() (:193-229) and
+//     importance()/thirds() (:276-298, :30-34).
+#include "fi_plan.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+
+namespace fi {
+
+static constexpr double kImEpsilon = 1.0e-12;  // MagickEpsilon
+
+// ---------------------------------------------------------------------------
+// ImageMagick geometry
+// ---------------------------------------------------------------------------
+static void meta_geometry(int W, int H, int tw, int th, bool fill, bool shrink, int *ow, int *oh) {
+  double scale;
+  const bool has_w = tw > 0, has_h = th > 0;
+  if (has_w && has_h) {
+    scale = (double)tw / (double)W;
+    if (!fill) {
+      if (scale > ((double)th / (double)H)) scale = (double)th / (double)H;
+    } else if (scale < ((double)th / (double)H)) {
+      scale = (double)th / (double)H;
+    }
+  } else if (has_w) {
+    scale = (double)tw / (double)W;
+    if (fill && scale < ((double)tw / (double)H)) scale = (double)tw / (double)H;
+  } else {
+    scale = (double)th / (double)H;
+    if (fill && scale < ((double)th / (double)W)) scale = (double)th / (double)W;
+  }
+  long w = (long)floor(scale * W + 0.5), h = (long)floor(scale * H + 0.5);
+  if (w < 1) w = 1;
+  if (h < 1) h = 1;
+  if (shrink) {
+    if (W < w) w = W;
+    if (H < h) h = H;
+  }
+  *ow = (int)w;
+  *oh = (int)h;
+}
+
+static void gravity_offset(int W, int H, int ew, int eh, int gravity, int *x, int *y) {
+  long ox = 0, oy = 0;
+  switch (gravity) {
+    case FI_GRAVITY_NORTHEAST: case FI_GRAVITY_EAST: case FI_GRAVITY_SOUTHEAST:
+      ox = (long)((unsigned long)W - (unsigned long)ew);
+      break;
+    case FI_GRAVITY_NORTH: case FI_GRAVITY_SOUTH: case FI_GRAVITY_CENTER:
+      ox = (long)((unsigned long)W / 2 - (unsigned long)ew / 2);
+      break;
+    default: break;
+  }
+  switch (gravity) {
+    case FI_GRAVITY_SOUTHWEST: case FI_GRAVITY_SOUTH: case FI_GRAVITY_SOUTHEAST:
+      oy = (long)((unsigned long)H - (unsigned long)eh);
+      break;
+    case FI_GRAVITY_EAST: case FI_GRAVITY_WEST: case FI_GRAVITY_CENTER:
+      oy = (long)((unsigned long)H / 2 - (unsigned long)eh / 2);
+      break;
+    default: break;
+  }
+  *x = (int)ox;
+  *y = (int)oy;
+}
+
+int plan_im(const fi_image &img, ImPlan *p) {
+  *p = ImPlan();
+  p->W = img.src_w;
+  p->H = img.src_h;
+  p->C = img.src_channels;
+  auto fail = [&](int code, const char *m) {
+    p->status = code;
+    p->err = m;
+    return code;
+  };
+  if (img.src_w <= 0 || img.src_h <= 0) return fail(FI_EINVAL, "source dimensions must be positive");
+  if (img.src_channels != 3) return fail(FI_EUNSUPPORTED, "only RGB8 sources (src_channels=3) are supported");
+  if ((int64_t)img.src_stride < (int64_t)img.src_w * 3) return fail(FI_EINVAL, "src_stride < 3*src_w");
+  const uint32_t f = img.flags;
+  if ((f & FI_OP_THUMBNAIL) && (f & FI_OP_RESIZE)) return fail(FI_EINVAL, "both -thumbnail and -resize");
+  if (f & FI_OP_MONOCHROME) return fail(FI_EUNSUPPORTED, "-monochrome is not implemented on the GPU path yet");
+  const bool has_geom = img.target_w > 0 || img.target_h > 0;
+  p->tw = p->W;
+  p->th = p->H;
+  if (has_geom) {
+    if (!(f & (FI_OP_THUMBNAIL | FI_OP_RESIZE))) return fail(FI_EINVAL, "geometry without a resize operator");
+    meta_geometry(p->W, p->H, img.target_w, img.target_h, f & FI_GEOM_FILL, f & FI_GEOM_SHRINK_ONLY, &p->tw,
+                  &p->th);
+  }
+  p->resize = (p->tw != p->W || p->th != p->H);
+  p->sw = p->W;
+  p->sh = p->H;
+  if (p->resize && (f & FI_OP_THUMBNAIL)) {
+    // ThumbnailImage: area factor <= 0.1 and 5*w, 5*h >= 128 -> SampleImage
+    const double xf = (double)p->tw / (double)p->W, yf = (double)p->th / (double)p->H;
+    if (!((xf * yf) > 0.1) && !((5 * p->tw) < 128 || (5 * p->th) < 128)) {
+      p->sample = true;
+      p->sw = 5 * p->tw;
+      p->sh = 5 * p->th;
+    }
+  }
+  if (p->resize) {
+    p->xf = (double)p->tw / (double)p->sw;
+    p->yf = (double)p->th / (double)p->sh;
+    p->filter = ((p->xf * p->yf) > 1.0) ? kFilterMitchell : kFilterLanczos;
+    p->hfirst = p->xf > p->yf;
+  }
+  p->ex0 = p->ey0 = 0;
+  p->ew = p->tw;
+  p->eh = p->th;
+  if (f & FI_OP_EXTENT) {
+    const int ew = img.target_w > 0 ? img.target_w : p->tw;
+    const int eh = img.target_h > 0 ? img.target_h : p->th;
+    int gx, gy;
+    gravity_offset(p->tw, p->th, ew, eh, img.gravity ? img.gravity : FI_GRAVITY_CENTER, &gx, &gy);
+    if (gx < 0 || gy < 0 || gx + ew > p->tw || gy + eh > p->th)
+      return fail(FI_EUNSUPPORTED, "-extent larger than the resized image (background fill) is not supported");
+    p->ex0 = gx;
+    p->ey0 = gy;
+    p->ew = ew;
+    p->eh = eh;
+  }
+  p->gray = (f & FI_OP_GRAY) != 0;
+  p->rot = 0;
+  if (f & FI_OP_ROTATE) {
+    if (img.rotate % 90) return fail(FI_EUNSUPPORTED, "only -rotate by multiples of 90 (IntegralRotateImage)");
+    p->rot = ((img.rotate % 360) + 360) % 360;
+  }
+  p->out_c = p->gray ? 1 : 3;
+  const bool swap = p->rot == 90 || p->rot == 270;
+  p->out_w = swap ? p->eh : p->ew;
+  p->out_h = swap ? p->ew : p->eh;
+  return FI_OK;
+}
+
+// --- resize.c filters --------------------------------------------------------
+static double sinc(double x) {
+  if (x != 0.0) {
+    const double alpha = 3.14159265358979323846264338327950288419716939937510 * x;
+    return sin(alpha) / alpha;
+  }
+  return 1.0;
+}
+static double sincfast(double x) {
+  if (x > 4.0) return sinc(x);
+  const double xx = x * x;
+  const double c0 = 0.173611107357320220183368594093166520811e-2;
+  const double c1 = -0.384240921114946632192116762889211361285e-3;
+  const double c2 = 0.394201182359318128221229891724947048771e-4;
+  const double c3 = -0.250963301609117217660068889165550534856e-5;
+  const double c4 = 0.111902032818095784414237782071368805120e-6;
+  const double c5 = -0.372895101408779549368465614321137048875e-8;
+  const double c6 = 0.957694196677572570319816780188718518330e-10;
+  const double c7 = -0.187208577776590710853865174371617338991e-11;
+  const double c8 = 0.253524321426864752676094495396308636823e-13;
+  const double c9 = -0.177084805010701112639035485248501049364e-15;
+  const double p =
+      c0 + xx * (c1 + xx * (c2 + xx * (c3 + xx * (c4 + xx * (c5 + xx * (c6 + xx * (c7 + xx * (c8 + xx * c9))))))));
+  return (xx - 1.0) * (xx - 4.0) * (xx - 9.0) * (xx - 16.0) * p;
+}
+static double mitchell(double x) {
+  const double B = 1.0 / 3.0, C = 1.0 / 3.0, twoB = B + B;
+  const double k0 = 1.0 - (1.0 / 3.0) * B, k1 = -3.0 + twoB + C, k2 = 2.0 - 1.5 * B - C;
+  const double k3 = (4.0 / 3.0) * B + 4.0 * C, k4 = -8.0 * C - twoB, k5 = B + 5.0 * C,
+               k6 = (-1.0 / 6.0) * B - C;
+  if (x < 1.0) return k0 + x * (x * (k1 + x * k2));
+  if (x < 2.0) return k3 + x * (k4 + x * (k5 + x * k6));
+  return 0.0;
+}
+static double filter_weight(int filter, double x) {
+  const double xb = fabs(x) / 1.0;
+  if (filter == kFilterLanczos) {
+    const double scale = 1.0 / 3.0;
+    const double win = sincfast(xb * scale);
+    return win * sincfast(xb);
+  }
+  return 1.0 * mitchell(xb);
+}
+static double perceptible_reciprocal(double x) {
+  const double sign = x < 0.0 ? -1.0 : 1.0;
+  if ((sign * x) >= kImEpsilon) return 1.0 / x;
+  return sign / kImEpsilon;
+}
+
+void build_axis(int filter, double factor, int in_sampled, int out_size, int o0, int o1, bool sample,
+                int in_src, AxisTable *t) {
+  (void)out_size;
+  *t = AxisTable();
+  double scale = fmax(1.0 / factor + kImEpsilon, 1.0);
+  double support = scale * (filter == kFilterLanczos ? 3.0 : 2.0);
+  if (support < 0.5) {
+    support = 0.5;
+    scale = 1.0;
+  }
+  scale = perceptible_reciprocal(scale);
+  std::vector<double> w;
+  std::vector<double> merged;
+  t->src_lo = 1 << 30;
+  t->src_hi = 0;
+  for (int o = o0; o < o1; o++) {
+    const double bisect = (double)(o + 0.5) / factor + kImEpsilon;
+    const long s = (long)fmax(bisect - support + 0.5, 0.0);
+    const long e = (long)fmin(bisect + support + 0.5, (double)in_sampled);
+    const int n = (int)(e - s);
+    w.assign(n > 0 ? n : 0, 0.0);
+    double density = 0.0;
+    for (int i = 0; i < n; i++) {
+      w[i] = filter_weight(filter, scale * ((double)(s + i) - bisect + 0.5));
+      density += w[i];
+    }
+    if (density != 0.0 && density != 1.0) {
+      density = perceptible_reciprocal(density);
+      for (int i = 0; i < n; i++) w[i] *= density;
+    }
+    // map sampled taps to source indices (SampleImage offsets) and merge
+    auto src_of = [&](long j) -> long {
+      if (!sample) return j;
+      return (long)((((double)j + (0.5 - kImEpsilon)) * in_src) / in_sampled);
+    };
+    const long m0 = n > 0 ? src_of(s) : 0;
+    const long m1 = n > 0 ? src_of(s + n - 1) : -1;
+    const int cnt = (int)(m1 - m0 + 1);
+    merged.assign(cnt > 0 ? cnt : 0, 0.0);
+    for (int i = 0; i < n; i++) merged[src_of(s + i) - m0] += w[i];
+    t->start.push_back((int32_t)m0);
+    t->count.push_back(cnt);
+    t->woff.push_back((int32_t)t->w.size());
+    for (int i = 0; i < cnt; i++) t->w.push_back((float)merged[i]);
+    t->maxtaps = std::max(t->maxtaps, cnt);
+    t->src_lo = std::min<int32_t>(t->src_lo, (int32_t)m0);
+    t->src_hi = std::max<int32_t>(t->src_hi, (int32_t)(m0 + cnt));
+  }
+  if (o1 <= o0) t->src_lo = 0;
+}
+
+// ---------------------------------------------------------------------------
+// Pillow
+// ---------------------------------------------------------------------------
+static double pil_sinc(double x) {
+  if (x == 0.0) return 1.0;
+  x = x * M_PI;
+  return sin(x) / x;
+}
+static double pil_lanczos(double x) {
+  if (-3.0 <= x && x < 3.0) return pil_sinc(x) * pil_sinc(x / 3);
+  return 0.0;
+}
+
+int pil_coeffs(int in_size, float in0, float in1, int out_size, std::vector<int32_t> *bounds,
+               std::vector<int32_t> *kk) {
+  double scale, filterscale;
+  filterscale = scale = (double)(in1 - in0) / out_size;
+  if (filterscale < 1.0) filterscale = 1.0;
+  const double support = 3.0 * filterscale;
+  const int ksize = (int)ceil(support) * 2 + 1;
+  std::vector<double> k(ksize);
+  bounds->assign((size_t)out_size * 2, 0);
+  kk->assign((size_t)out_size * ksize, 0);
+  for (int xx = 0; xx < out_size; xx++) {
+    const double center = in0 + (xx + 0.5) * scale;
+    double ww = 0.0;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    int x;
+    for (x = 0; x < xmax; x++) {
+      const double w = pil_lanczos((x + xmin - center + 0.5) * ss);
+      k[x] = w;
+      ww += w;
+    }
+    for (x = 0; x < xmax; x++)
+      if (ww != 0.0) k[x] /= ww;
+    for (; x < ksize; x++) k[x] = 0;
+    for (x = 0; x < ksize; x++)
+      (*kk)[(size_t)xx * ksize + x] =
+          k[x] < 0 ? (int32_t)(-0.5 + k[x] * (1 << 22)) : (int32_t)(0.5 + k[x] * (1 << 22));
+    (*bounds)[xx * 2 + 0] = xmin;
+    (*bounds)[xx * 2 + 1] = xmax;
+  }
+  return ksize;
+}
+
+// Image.thumbnail preserve_aspect_ratio (PIL/Image.py:2878-2893)
+static int pil_thumbnail_size(int W, int H, int x, int y, int *tw, int *th) {
+  if (x >= W && y >= H) return 1;
+  if (y == 0) return FI_EINVAL;  // ZeroDivisionError in x / y
+  const double aspect = (double)W / (double)H;
+  if ((double)x / (double)y >= aspect) {
+    const double num = y * aspect, f = floor(num), c = ceil(num);
+    const double kf = fabs(aspect - f / y), kc = fabs(aspect - c / y);
+    const double r = (kc < kf) ? c : f;
+    x = r < 1 ? 1 : (int)r;
+  } else {
+    const double num = x / aspect, f = floor(num), c = ceil(num);
+    if (f == 0 && c == 0) {
+      y = 1;
+    } else {
+      const double kf = (f == 0) ? 0 : fabs(aspect - x / f), kc = (c == 0) ? 0 : fabs(aspect - x / c);
+      const double r = (kc < kf) ? c : f;
+      y = r < 1 ? 1 : (int)r;
+    }
+  }
+  *tw = x;
+  *th = y;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// smartcrop.py geometry
+// ---------------------------------------------------------------------------
+int plan_sc(int W, int H, int width, int height, const fi_smartcrop_options &o, ScPlan *p) {
+  *p = ScPlan();
+  p->W = W;
+  p->H = H;
+  auto fail = [&](int code, const char *m) {
+    p->status = code;
+    p->err = m;
+    return code;
+  };
+  if (W <= 0 || H <= 0 || width <= 0 || height <= 0) return fail(FI_EINVAL, "smartcrop: bad dimensions");
+  const double sw = (double)W / width, sh = (double)H / height;
+  const double scale = (sh < sw) ? sh : sw;  // min(a, b)
+  int cw = (int)floor(width * scale), ch = (int)floor(height * scale);
+  double min_scale = o.min_scale;
+  {
+    const double inv = 1 / scale;
+    const double m = (min_scale > inv) ? min_scale : inv;          // max(1/scale, min_scale)
+    min_scale = (m < o.max_scale) ? m : o.max_scale;                // min(max_scale, .)
+  }
+  double pre = 1;
+  int aw = W, ah = H;
+  if (o.prescale) {
+    pre = 1 / scale / min_scale;
+    if (pre < 1) {
+      const int tx = (int)(W * pre), ty = (int)(H * pre);
+      int tw = W, th = H;
+      const int r = pil_thumbnail_size(W, H, tx, ty, &tw, &th);
+      if (r < 0) return fail(FI_EINVAL, "smartcrop: thumbnail size division by zero");
+      if (r == 1) {
+        tw = W;
+        th = H;
+      }
+      if (tw != W || th != H) {
+        p->thumb = true;
+        // Image.resize(reducing_gap=2.0)
+        const int fx = (int)((double)W / tw / 2.0), fy = (int)((double)H / th / 2.0);
+        p->fx = fx ? fx : 1;
+        p->fy = fy ? fy : 1;
+        float bx1 = (float)W, by1 = (float)H;
+        int iw = W, ih = H;
+        if (p->fx > 1 || p->fy > 1) {
+          iw = (W + p->fx - 1) / p->fx;
+          ih = (H + p->fy - 1) / p->fy;
+          bx1 = (float)((double)W / p->fx);
+          by1 = (float)((double)H / p->fy);
+        }
+        p->rw = iw;
+        p->rh = ih;
+        p->need_h = tw != iw || bx1 != (float)iw;
+        p->need_v = th != ih || by1 != (float)ih;
+        p->ksh = pil_coeffs(iw, 0.0f, bx1, tw, &p->hb, &p->hk);
+        p->ksv = pil_coeffs(ih, 0.0f, by1, th, &p->vb, &p->vk);
+        p->ybox_first = p->vb[0];
+        const int ybox_last = p->vb[th * 2 - 2] + p->vb[th * 2 - 1];
+        if (p->need_h) {
+          for (int i = 0; i < th; i++) p->vb[i * 2] -= p->ybox_first;
+          p->hrows = ybox_last - p->ybox_first;
+        } else {
+          p->hrows = 0;
+        }
+      }
+      aw = tw;
+      ah = th;
+      cw = (int)floor(cw * pre);
+      ch = (int)floor(ch * pre);
+    } else {
+      pre = 1;
+    }
+  }
+  if (!p->thumb) {
+    p->rw = W;
+    p->rh = H;
+  }
+  p->prescale = pre;
+  p->aw = aw;
+  p->ah = ah;
+  p->cw = cw;
+  p->ch = ch;
+  // crops() (smartcrop.py:193-229)
+  const int i0 = (int)(o.max_scale * 100), i1 = (int)((min_scale - o.scale_step) * 100);
+  const int di = -(int)(o.scale_step * 100);
+  if (di >= 0 || o.step <= 0) return fail(FI_EINVAL, "smartcrop: bad scale_step/step");
+  for (int i = i0; i > i1; i += di) {
+    const double s = i / 100.0;
+    for (int y = 0; y < ah; y += o.step) {
+      if (!(y + ch * s <= ah)) break;
+      for (int x = 0; x < aw; x += o.step) {
+        if (!(x + cw * s <= aw)) break;
+        CropHost c;
+        c.fx = x;
+        c.fy = y;
+        c.fw = cw * s;
+        c.fh = ch * s;
+        c.x0 = x;
+        c.y0 = y;
+        c.nin_x = std::min(aw - x, (int)ceil(x + c.fw) - x);
+        c.nin_y = std::min(ah - y, (int)ceil(y + c.fh) - y);
+        if (c.nin_x < 0) c.nin_x = 0;
+        if (c.nin_y < 0) c.nin_y = 0;
+        c.rx = (int32_t)floor(c.fx / pre);
+        c.ry = (int32_t)floor(c.fy / pre);
+        c.rw = (int32_t)floor(c.fw / pre);
+        c.rh = (int32_t)floor(c.fh / pre);
+        p->crops.push_back(c);
+      }
+    }
+  }
+  if (p->crops.empty()) return fail(FI_ENOCROP, "smartcrop: no crop windows (smartcrop.py:227-228 ValueError)");
+  return FI_OK;
+}
+
+static double thirds(double x) {
+  x = (fmod(x + 2.0 / 3.0, 2.0) * 0.5 - 0.5) * 16;
+  const double v = 1 - x * x;
+  return (0 > v) ? 0.0 : v;
+}
+
+void sc_importance_table(const fi_smartcrop_params &P, double fw, double fh, int nx, int ny,
+                         std::vector<double> *out) {
+  out->assign((size_t)nx * ny, 0.0);
+  for (int dy = 0; dy < ny; dy++)
+    for (int dx = 0; dx < nx; dx++) {
+      const double xr = dx / fw, yr = dy / fh;
+      const double px = fabs(0.5 - xr) * 2, py = fabs(0.5 - yr) * 2;
+      double ddx = px - 1 + P.edge_radius, ddy = py - 1 + P.edge_radius;
+      if (0 > ddx) ddx = 0;
+      if (0 > ddy) ddy = 0;
+      const double d = (ddx * ddx + ddy * ddy) * P.edge_weight;
+      double s = 1.41 - sqrt(px * px + py * py);
+      if (P.rule_of_thirds) {
+        double m = s + d + 0.5;
+        if (0 > m) m = 0;
+        s += (m * 1.2) * (thirds(px) + thirds(py));
+      }
+      (*out)[(size_t)dy * nx + dx] = s + d;
+    }
+}
+
+}  // namespace fi

@@ -1,0 +1,75 @@
+// fi_plan.h -- host-side planning: ImageMagick geometry and tap tables,
+// Pillow prescale geometry and coefficients, smartcrop crop windows and
+// importance tables.  Pure integer/IEEE-double host code (built with
+// -ffp-contract=off), no GPU calls.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "fi_internal.h"
+
+namespace fi {
+
+enum Filter { kFilterLanczos = 1, kFilterMitchell = 2 };
+
+// Resample geometry of one image, ImageMagick 6 semantics.
+struct ImPlan {
+  int status = FI_OK;
+  std::string err;
+  int W = 0, H = 0, C = 3;
+  int tw = 0, th = 0;       // -thumbnail / -resize target (ParseMetaGeometry)
+  bool resize = false;      // false: ResizeImage returns a clone
+  bool sample = false;      // ThumbnailImage 5x SampleImage pre-step
+  int sw = 0, sh = 0;       // sampled dims (= W, H when !sample)
+  int filter = kFilterLanczos;
+  bool hfirst = false;      // HorizontalFilter first iff x_factor > y_factor
+  double xf = 1, yf = 1;
+  int ex0 = 0, ey0 = 0, ew = 0, eh = 0;  // extent window in the resized image
+  bool gray = false;
+  int rot = 0;
+  int out_w = 0, out_h = 0, out_c = 3;   // after rotate
+};
+int plan_im(const fi_image &img, ImPlan *p);
+
+// One resample axis in the source index domain.
+struct AxisTable {
+  std::vector<int32_t> start, count, woff;
+  std::vector<float> w;
+  int32_t maxtaps = 0, src_lo = 0, src_hi = 0;
+};
+// Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)
+// to `out_size`; taps mapped back to the `in_src` source indices through the
+// SampleImage offsets (identity when !sample) and merged.
+void build_axis(int filter, double factor, int in_sampled, int out_size, int o0, int o1,
+                bool sample, int in_src, AxisTable *t);
+
+// ----------------------------------------------------------------------
+struct CropHost {
+  double fx, fy, fw, fh;
+  int32_t x0, y0, nin_x, nin_y;
+  int32_t rx, ry, rw, rh;
+};
+struct ScPlan {
+  int status = FI_OK;
+  std::string err;
+  int W = 0, H = 0;
+  double prescale = 1;
+  int cw = 0, ch = 0;                   // crop dims in the analysed image
+  bool thumb = false;                   // Pillow thumbnail runs
+  int fx = 1, fy = 1, rw = 0, rh = 0;   // reduce
+  int aw = 0, ah = 0;                   // analysed dims
+  bool need_h = false, need_v = false;
+  int ksh = 0, ksv = 0, ybox_first = 0, hrows = 0;
+  std::vector<int32_t> hb, hk, vb, vk;  // bounds pairs and int32 coeffs
+  std::vector<CropHost> crops;
+};
+int plan_sc(int W, int H, int target_w, int target_h, const fi_smartcrop_options &o, ScPlan *p);
+void sc_importance_table(const fi_smartcrop_params &P, double fw, double fh, int nx, int ny,
+                         std::vector<double> *out);
+// or_pil_coeffs equivalent (Resample.c precompute_coeffs + normalize_coeffs_8bpc)
+int pil_coeffs(int in_size, float in0, float in1, int out_size, std::vector<int32_t> *bounds,
+               std::vector<int32_t> *kk);
+
+}  // namespace fi

@@ -1,0 +1,167 @@
+"""Multi-GPU plumbing: one process per GPU, images sharded across ranks.
+
+flyimg's path has no cross-image reduction: each rank runs
+its own shard end to end on its own GPU; the only exchange is the final gather
+of 32-byte per-image result records to rank 0, done with RCCL over xGMI by
+libflyimg_hip (``fi_rccl_gather_records``).
+
+Control plane (barriers, the RCCL unique id, max-over-ranks timing) needs no
+GPU and must not load a second HIP runtime into the process, so it does not go
+through torch: ``FileComm`` is a single-node rendezvous in a directory shared by
+the ranks a ``torch.distributed.run`` agent starts (they share its PID as
+parent).  Any object with the same five methods works (tests drive the shard
+and gather logic through a torch.distributed gloo wrapper on CPU).
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import time
+
+
+def env_rank_world():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))))
+
+
+class SoloComm:
+    rank, world = 0, 1
+
+    def barrier(self):
+        pass
+
+    def bcast_bytes(self, data: bytes | None) -> bytes:
+        return data
+
+    def allgather_obj(self, obj):
+        return [obj]
+
+    def close(self):
+        pass
+
+
+class FileComm:
+    """Rendezvous through files under a run directory (single node)."""
+
+    def __init__(self, rank: int, world: int, run_id: str | None = None, root: str = "/tmp", timeout: float = 600.0):
+        self.rank, self.world, self.timeout = rank, world, timeout
+        run_id = run_id or f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+        self.dir = os.path.join(root, f"flyimg_rdzv_{run_id}")
+        os.makedirs(self.dir, exist_ok=True)
+        self.gen = 0
+
+    def _path(self, tag, r):
+        return os.path.join(self.dir, f"{tag}.{r}")
+
+    def _put(self, tag, r, payload: bytes):
+        tmp = self._path(tag, r) + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(payload)
+        os.replace(tmp, self._path(tag, r))
+
+    def _get(self, tag, r) -> bytes:
+        p = self._path(tag, r)
+        t0 = time.time()
+        while not os.path.exists(p):
+            if time.time() - t0 > self.timeout:
+                raise TimeoutError(f"rank {self.rank}: waiting for {p}")
+            time.sleep(0.002)
+        with open(p, "rb") as f:
+            return f.read()
+
+    def allgather_obj(self, obj):
+        self.gen += 1
+        tag = f"ag{self.gen}"
+        self._put(tag, self.rank, json.dumps(obj).encode())
+        return [json.loads(self._get(tag, r)) for r in range(self.world)]
+
+    def barrier(self):
+        self.allgather_obj(0)
+
+    def bcast_bytes(self, data: bytes | None) -> bytes:
+        self.gen += 1
+        tag = f"bc{self.gen}"
+        if self.rank == 0:
+            self._put(tag, 0, data)
+        return self._get(tag, 0)
+
+    def close(self):
+        self.barrier()
+        if self.rank == 0:
+            shutil.rmtree(self.dir, ignore_errors=True)
+
+
+def make_comm():
+    rank, world, _ = env_rank_world()
+    return SoloComm() if world == 1 else FileComm(rank, world)
+
+
+def shard_lpt(costs: list[float], world: int) -> list[list[int]]:
+    """Greedy LPT: images (by cost, e.g. algorithmic bytes) to ranks."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    load = [0.0] * world
+    out = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda k: (load[k], k))
+        out[r].append(i)
+        load[r] += costs[i]
+    for s in out:
+        s.sort()
+    return out
+
+
+def shard_contiguous(n: int, world: int) -> list[range]:
+    """Uniform batches: contiguous ranges."""
+    base, extra = divmod(n, world)
+    out, start = [], 0
+    for r in range(world):
+        k = base + (1 if r < extra else 0)
+        out.append(range(start, start + k))
+        start += k
+    return out
+
+
+class RecordGather:
+    """Gather per-image result records to rank 0: RCCL through the C-ABI when a
+    context is given, else through the control-plane comm (CPU tests)."""
+
+    def __init__(self, comm, ctx=None):
+        self.comm, self.ctx, self.backend = comm, ctx, "none"
+        if comm.world == 1:
+            self.backend = "local"
+            return
+        if ctx is not None:
+            import ctypes
+
+            from . import _lib as L
+
+            uid = ctypes.create_string_buffer(128)
+            if comm.rank == 0:
+                L.check(L.lib().fi_rccl_get_unique_id(uid))
+            data = comm.bcast_bytes(uid.raw if comm.rank == 0 else None)
+            L.check(L.lib().fi_rccl_init(ctx.h, comm.rank, comm.world, data))
+            self.backend = "rccl"
+        else:
+            self.backend = "comm"
+
+    def gather(self, records):
+        """records: list of 8-int tuples (fi_record).  Rank 0 gets all ranks'."""
+        if self.backend == "local":
+            return list(records)
+        if self.backend == "rccl":
+            import ctypes
+
+            from . import _lib as L
+
+            n = len(records)
+            send = (L.FiRecord * max(n, 1))()
+            for i, r in enumerate(records):
+                send[i] = L.FiRecord(*r)
+            recv = (L.FiRecord * max(n * self.comm.world, 1))() if self.comm.rank == 0 else None
+            L.check(L.lib().fi_rccl_gather_records(self.ctx.h, send, n, recv))
+            if self.comm.rank != 0:
+                return None
+            return [tuple(getattr(recv[i], f) for f, _ in L.FiRecord._fields_) for i in range(n * self.comm.world)]
+        allr = self.comm.allgather_obj([list(r) for r in records])
+        return [tuple(r) for part in allr for r in part] if self.comm.rank == 0 else None

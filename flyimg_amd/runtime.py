@@ -1,0 +1,175 @@
+"""Host-side runtime over the C-ABI: one ``Context`` per process per GPU.
+
+Thin, allocation-light wrappers: numpy arrays in, numpy arrays out for the
+host path (``fi_process_batch``), raw device pointers for device-resident
+batches (``fi_process_batch_device``, used by bench.py).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass
+class Op:
+    """One image's operator list -- the fields of fi_image a caller sets.
+    Mirrors the convert argv ImageProcessor::generateCommand builds
+    (ImageProcessor.php:66-110)."""
+
+    target_w: int = 0
+    target_h: int = 0
+    flags: int = L.FI_OP_THUMBNAIL
+    gravity: int = L.GRAVITY["Center"]
+    rotate: int = 0
+    smartcrop_w: int = 0
+    smartcrop_h: int = 0
+
+
+def _fill(img: L.FiImage, op: Op):
+    img.target_w, img.target_h = op.target_w, op.target_h
+    img.flags, img.gravity, img.rotate = op.flags, op.gravity, op.rotate
+    img.smartcrop_w, img.smartcrop_h = op.smartcrop_w, op.smartcrop_h
+
+
+def plan(width: int, height: int, op: Op):
+    """fi_plan for one image: (out_w, out_h, out_channels) before smart-crop apply."""
+    img = L.FiImage()
+    img.src_w, img.src_h, img.src_stride, img.src_channels = width, height, width * 3, 3
+    _fill(img, op)
+    L.check(L.lib().fi_plan(ctypes.byref(img), 1))
+    return img.out_w, img.out_h, img.out_channels
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        self._lib = L.lib()
+        h = ctypes.c_void_p()
+        L.check(self._lib.fi_create(ctypes.byref(h), device))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self._lib.fi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- host batches ----------------------------------------------------
+    def process(self, images: list[np.ndarray], ops: list[Op]):
+        """Run a batch of RGB8 HWC numpy images; returns (outputs, fi_image records)."""
+        n = len(images)
+        arr = (L.FiImage * n)()
+        outs = []
+        keep = []
+        for i, (src, op) in enumerate(zip(images, ops)):
+            src = np.ascontiguousarray(src, dtype=np.uint8)
+            keep.append(src)
+            img = arr[i]
+            img.src = src.ctypes.data
+            img.src_h, img.src_w = src.shape[:2]
+            img.src_stride = src.strides[0]
+            img.src_channels = src.shape[2] if src.ndim == 3 else 1
+            _fill(img, op)
+        L.lib().fi_plan(arr, n)  # per-image status decides below
+        for i in range(n):
+            cap = max(arr[i].out_w * arr[i].out_h * max(arr[i].out_channels, 1), 1)
+            buf = np.zeros(cap, np.uint8)
+            outs.append(buf)
+            arr[i].dst = buf.ctypes.data
+            arr[i].dst_capacity = cap
+        rc = self._lib.fi_process_batch(self.h, arr, n)
+        results = []
+        for i in range(n):
+            a = arr[i]
+            if a.status == L.FI_OK:
+                o = outs[i][: a.out_h * a.out_stride].reshape(a.out_h, a.out_w, a.out_channels)
+                results.append(o[:, :, 0] if a.out_channels == 1 else o)
+            else:
+                results.append(None)
+        return results, arr, rc
+
+    # ---- smartcrop (smartcrop.py SmartCrop().crop) ---------------------------
+    def smartcrop_ex(self, rgb: np.ndarray, width: int, height: int, params=None, options=None,
+                     want_images: bool = False):
+        rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+        h, w = rgb.shape[:2]
+        cap = 2 * ((w + 7) // 8 + 1) * ((h + 7) // 8 + 1) + 16
+        crops = (L.FiCropScore * cap)()
+        n, top = ctypes.c_int32(), ctypes.c_int32()
+        awh = (ctypes.c_int32 * 2)()
+        pre = ctypes.c_double()
+        ocap = w * h * 3
+        pbuf = np.zeros(ocap, np.uint8) if want_images else None
+        mbuf = np.zeros(ocap, np.uint8) if want_images else None
+        rc = self._lib.fi_smartcrop_ex(
+            self.h, rgb.ctypes.data, w, h, rgb.strides[0], width, height,
+            ctypes.byref(params) if params is not None else None,
+            ctypes.byref(options) if options is not None else None,
+            crops, cap, ctypes.byref(n), ctypes.byref(top), awh, ctypes.byref(pre),
+            pbuf.ctypes.data if want_images else None, mbuf.ctypes.data if want_images else None, ocap)
+        L.check(rc)
+        out = {"n": n.value, "top_index": top.value, "analyse_size": (awh[0], awh[1]),
+               "prescale": pre.value, "crops": [crops[k] for k in range(n.value)]}
+        if want_images:
+            na = awh[0] * awh[1] * 3
+            out["prescaled"] = pbuf[:na].reshape(awh[1], awh[0], 3)
+            out["maps"] = mbuf[:na].reshape(awh[1], awh[0], 3)
+        return out
+
+    # ---- device memory -------------------------------------------------------
+    def malloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        L.check(self._lib.fi_device_malloc(self.h, ctypes.byref(p), nbytes))
+        return p.value
+
+    def free(self, ptr: int):
+        L.check(self._lib.fi_device_free(self.h, ptr))
+
+    def h2d(self, dptr: int, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        L.check(self._lib.fi_memcpy_h2d(self.h, dptr, arr.ctypes.data, arr.nbytes))
+
+    def d2h(self, dptr: int, nbytes: int) -> np.ndarray:
+        out = np.empty(nbytes, np.uint8)
+        L.check(self._lib.fi_memcpy_d2h(self.h, out.ctypes.data, dptr, nbytes))
+        return out
+
+    def fill_synthetic(self, dptr: int, w: int, h: int, stride: int, seed: int):
+        L.check(self._lib.fi_fill_synthetic(self.h, dptr, w, h, stride, seed & 0xFFFFFFFF))
+
+    def process_device(self, arr, n: int) -> int:
+        """fi_process_batch_device on a prepared FiImage array (device pointers)."""
+        return self._lib.fi_process_batch_device(self.h, arr, n)
+
+    # ---- timing ----------------------------------------------------------------
+    def set_timing(self, on: bool):
+        L.check(self._lib.fi_set_timing(self.h, int(on)))
+
+    def reset_stats(self):
+        L.check(self._lib.fi_reset_stats(self.h))
+
+    def stats(self, name: str):
+        ms, n, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        L.check(self._lib.fi_kernel_stats(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)))
+        return ms.value, n.value, b.value
+
+
+def device_count() -> int:
+    n = ctypes.c_int32()
+    L.check(L.lib().fi_device_count(ctypes.byref(n)))
+    return n.value

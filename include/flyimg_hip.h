@@ -1,0 +1,210 @@
+/*
+ * flyimg_hip.h -- C-ABI of libflyimg_hip.so, the MI355X (gfx950) image hot
+ * path of flyimg.  Plain C: pointers, sizes and PODs only.
+ *
+ * What each entry point replaces in the reference (v1o/flyimg):
+ *
+ *   fi_plan / fi_process_batch / fi_process_batch_device
+ *       replace ImageProcessor::processNewImage -> generateCommand ->
+ *       Processor::execute("convert ...") (src/Core/Processor/
+ *       ImageProcessor.php:49-57, :66-110; Processor.php:44-62): the resize
+ *       operator (-thumbnail/-resize, :264-272) with its geometry
+ *       (generateCropSize :138-148 / generateSimpleSize :154-162),
+ *       -gravity/-extent (c_1), -colorspace Gray (clsp_Gray, :88),
+ *       -rotate (forwarded option, :303-315), and -- when FI_SMARTCROP is set --
+ *       SmartCropProcessor::smartCrop (SmartCropProcessor.php:21-36: the
+ *       python3 smartcrop.py exec plus the "convert -crop" exec).
+ *   fi_smartcrop / fi_smartcrop_ex
+ *       replace SmartCrop().crop(...) of python/smartcrop.py:137-191 (the
+ *       ctypes path of the drop-in smartcrop CLI, smartcrop.py:341-377).
+ *
+ * Error convention (Processor.php:53-59 throws ExecFailedException on a
+ * non-zero exit): every call returns FI_OK (0) or a negative FI_E* code and
+ * fi_last_error() returns the thread-local message of the last failure.
+ * The PHP FFI shim maps a non-zero return to ExecFailedException; the Python
+ * shim maps FI_ENOCROP to ValueError (smartcrop.py:227-228) and the rest to
+ * RuntimeError.
+ *
+ * Ownership: host buffers are caller-owned; device memory, pinned staging and
+ * tap tables are owned by the fi_ctx.  Threading: calls on one fi_ctx are
+ * serialised by an internal mutex.  One fi_ctx per process per GPU (one
+ * process per GPU; torch.distributed-style launch).
+ */
+#ifndef FLYIMG_HIP_H
+#define FLYIMG_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FI_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+#define FI_OK 0
+#define FI_EINVAL (-1)       /* bad argument / geometry                     */
+#define FI_ENOCROP (-2)      /* smartcrop.py crops(): ValueError (:227-228) */
+#define FI_ENOMEM (-3)       /* host or device allocation failed            */
+#define FI_EDEVICE (-4)      /* HIP runtime / kernel error                  */
+#define FI_EUNSUPPORTED (-5) /* operator not implemented on this path       */
+#define FI_ECAPACITY (-6)    /* dst_capacity too small (see fi_plan)        */
+
+/* ---- per-image operator flags (mirror the convert argv) --------------- */
+#define FI_OP_THUMBNAIL (1u << 0)      /* -thumbnail (default, ImageProcessor.php:269)   */
+#define FI_OP_RESIZE (1u << 1)         /* -resize (rz_1)                                  */
+#define FI_GEOM_FILL (1u << 2)         /* '^' geometry flag (generateCropSize :143)       */
+#define FI_GEOM_SHRINK_ONLY (1u << 3)  /* '>' geometry flag (generateSimpleSize :159)     */
+#define FI_OP_EXTENT (1u << 4)         /* -gravity G -extent WxH (c_1, :144-145)          */
+#define FI_OP_GRAY (1u << 5)           /* -colorspace Gray (clsp_Gray, :88)               */
+#define FI_OP_MONOCHROME (1u << 6)     /* -monochrome (mnchr_1, :90-92)                   */
+#define FI_OP_ROTATE (1u << 7)         /* -rotate <deg>, multiples of 90 (r_90, :306)     */
+#define FI_OP_SMARTCROP (1u << 8)      /* compute smartcrop.py's box on the result (smc_1) */
+#define FI_OP_SMARTCROP_APPLY (1u << 9) /* and crop to it (SmartCropProcessor.php:30-34)   */
+
+/* ImageMagick GravityType values used by -gravity (parameters.yml:99). */
+#define FI_GRAVITY_NORTHWEST 1
+#define FI_GRAVITY_NORTH 2
+#define FI_GRAVITY_NORTHEAST 3
+#define FI_GRAVITY_WEST 4
+#define FI_GRAVITY_CENTER 5
+#define FI_GRAVITY_EAST 6
+#define FI_GRAVITY_SOUTHWEST 7
+#define FI_GRAVITY_SOUTH 8
+#define FI_GRAVITY_SOUTHEAST 9
+
+/* One image of a batch.  Caller fills the inputs; the library fills the
+ * "filled by library" fields.  For fi_process_batch the pointers are host
+ * pointers; for fi_process_batch_device they are device pointers. */
+typedef struct fi_image {
+  const uint8_t *src;      /* HWC RGB8 (src_channels 3)                       */
+  int32_t src_w, src_h;    /* pixels                                          */
+  int32_t src_stride;      /* bytes per row                                   */
+  int32_t src_channels;    /* 3                                               */
+  int32_t target_w;        /* geometry W (0 = absent, getDimensions :240-259) */
+  int32_t target_h;        /* geometry H (0 = absent)                         */
+  uint32_t flags;          /* FI_OP_* | FI_GEOM_*                             */
+  int32_t gravity;         /* FI_GRAVITY_*, 0 = Center                        */
+  int32_t rotate;          /* degrees for FI_OP_ROTATE (multiple of 90)       */
+  int32_t smartcrop_w;     /* smartcrop.py --width  (0 = 100, CLI default)    */
+  int32_t smartcrop_h;     /* smartcrop.py --height (0 = 100)                 */
+  uint8_t *dst;            /* output pixels, HWC, out_stride bytes per row    */
+  int64_t dst_capacity;    /* bytes available at dst                          */
+  /* ---- filled by library ---- */
+  int32_t out_w, out_h, out_channels, out_stride;
+  int32_t crop_x, crop_y, crop_w, crop_h; /* smartcrop top_crop (smartcrop.py:184-190 rescaled) */
+  double crop_score;                      /* top_crop["score"]["total"]           */
+  int32_t status;                         /* FI_OK or FI_E* for this image        */
+  int32_t n_candidates;                   /* crops re-scored exactly (diagnostic) */
+} fi_image;
+
+/* SmartCrop.__init__ keyword arguments (python/smartcrop.py:41-77). */
+typedef struct fi_smartcrop_params {
+  double detail_weight;             /* 0.2  */
+  double edge_radius;               /* 0.4  */
+  double edge_weight;               /* -10  */
+  double outside_importance;        /* -0.5 */
+  int32_t rule_of_thirds;           /* 1    */
+  double saturation_bias;           /* 0.2  */
+  double saturation_brightness_max; /* 0.9  */
+  double saturation_brightness_min; /* 0.05 */
+  double saturation_threshold;      /* 0.4  */
+  double saturation_weight;         /* 0.3  */
+  int32_t score_down_sample;        /* 1 (only 1 is supported)  */
+  double skin_bias;                 /* 0.01 */
+  double skin_brightness_max;       /* 1    */
+  double skin_brightness_min;       /* 0.2  */
+  double skin_color[3];             /* 0.78, 0.57, 0.44 */
+  double skin_threshold;            /* 0.8  */
+  double skin_weight;               /* 1.8  */
+} fi_smartcrop_params;
+
+/* SmartCrop.crop() keyword arguments (smartcrop.py:137-147). */
+typedef struct fi_smartcrop_options {
+  int32_t prescale;   /* 1 */
+  double max_scale;   /* 1 */
+  double min_scale;   /* 0.9 */
+  double scale_step;  /* 0.1 */
+  int32_t step;       /* 8 */
+  int32_t exact_all;  /* 1 = score every crop with the reference's sequential sum */
+} fi_smartcrop_options;
+
+/* One entry of result["crops"] (smartcrop.py:184-190, score :300-338). */
+typedef struct fi_crop_score {
+  int32_t x, y, width, height;      /* rescaled ints (crop() :184-190)                  */
+  double fx, fy, fw, fh;            /* analysed-image geometry before rescale           */
+  double detail, saturation, skin, total; /* exact when `exact` != 0                   */
+  int32_t exact;                    /* 1: sequential reference sum; 0: fast-pass value */
+  int32_t pad;
+} fi_crop_score;
+
+typedef struct fi_ctx fi_ctx;
+
+int32_t fi_abi_version(void);
+const char *fi_last_error(void);
+
+/* Devices and contexts. device = HIP ordinal (one process per GPU). */
+int fi_device_count(int32_t *count);
+int fi_create(fi_ctx **out, int32_t device);
+void fi_destroy(fi_ctx *ctx);
+
+/* Geometry only (no pixel work, no GPU): fills out_w/out_h/out_channels/
+ * out_stride for each image; status per image.  Returns FI_OK if all ok. */
+int fi_plan(fi_image *imgs, int32_t n);
+
+/* Host buffers: H2D -> kernels -> D2H.  Synchronous. */
+int fi_process_batch(fi_ctx *ctx, fi_image *imgs, int32_t n);
+/* Device-resident buffers (src/dst are device pointers on ctx's device).
+ * Synchronous; the timed kernels are recorded in fi_kernel_stats. */
+int fi_process_batch_device(fi_ctx *ctx, fi_image *imgs, int32_t n);
+
+/* smartcrop.py SmartCrop().crop(rgb, target_w, target_h) on host RGB8.
+ * out_xywh = top_crop x, y, width, height; *out_score = its total. */
+void fi_smartcrop_default_params(fi_smartcrop_params *p);
+void fi_smartcrop_default_options(fi_smartcrop_options *o);
+int fi_smartcrop(fi_ctx *ctx, const uint8_t *rgb, int32_t w, int32_t h, int32_t stride,
+                 int32_t target_w, int32_t target_h, const fi_smartcrop_params *params,
+                 int32_t out_xywh[4], double *out_score);
+/* Full result: every crop, top index, analysed maps (skin, edge, sat HWC) and
+ * the prescaled image (both analyse_w*analyse_h*3 bytes, may be NULL). */
+int fi_smartcrop_ex(fi_ctx *ctx, const uint8_t *rgb, int32_t w, int32_t h, int32_t stride,
+                    int32_t target_w, int32_t target_h, const fi_smartcrop_params *params,
+                    const fi_smartcrop_options *opts, fi_crop_score *crops, int32_t crops_cap,
+                    int32_t *n_crops, int32_t *top_index, int32_t analyse_wh[2],
+                    double *prescale, uint8_t *prescaled_out, uint8_t *maps_out,
+                    int64_t out_cap);
+
+/* Device memory and synthetic inputs (device-resident batches / benchmarks). */
+int fi_device_malloc(fi_ctx *ctx, void **ptr, uint64_t bytes);
+int fi_device_free(fi_ctx *ctx, void *ptr);
+int fi_memcpy_h2d(fi_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+int fi_memcpy_d2h(fi_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+/* Seeded synthetic RGB8 image (flyimg_amd/synth.py bit for bit). */
+int fi_fill_synthetic(fi_ctx *ctx, uint8_t *dev, int32_t w, int32_t h, int32_t stride,
+                      uint32_t seed);
+
+/* Kernel timing (HIP events on the launch stream).  Names: "resize",
+ * "resize_v", "resize_h", "sc_prescale", "sc_maps", "sc_score", "crop_apply",
+ * "batch".  bytes = algorithmic bytes accounted to that kernel. */
+int fi_set_timing(fi_ctx *ctx, int32_t enable);
+int fi_reset_stats(fi_ctx *ctx);
+int fi_kernel_stats(fi_ctx *ctx, const char *name, double *total_ms, int64_t *launches,
+                    double *bytes);
+
+/* Multi-GPU: the one exchange step is the gather of per-image result
+ * records to rank 0 over RCCL (xGMI).  The 128-byte unique id is created by
+ * rank 0 and distributed out of band. */
+typedef struct fi_record {
+  int32_t image, status, out_w, out_h;
+  int32_t crop_x, crop_y, crop_w, crop_h;
+} fi_record;
+int fi_rccl_get_unique_id(uint8_t id[128]);
+int fi_rccl_init(fi_ctx *ctx, int32_t rank, int32_t world, const uint8_t id[128]);
+/* Every rank sends `count` records (same count on every rank); rank 0
+ * receives world*count records in rank order. */
+int fi_rccl_gather_records(fi_ctx *ctx, const fi_record *send, int32_t count, fi_record *recv);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLYIMG_HIP_H */
