@@ -181,7 +181,9 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "resize stage (k_rs_v_u8 + k_rs_h_final, generic two-pass)",
+                "kernel": ("resize stage: k_rs_v_u8 + k_rs_h_final (generic two-pass)"
+                           if os.environ.get("FI_DISABLE_FUSED") == "1"
+                           else "resize stage: k_rs_fused<K> (fused vertical-first, one launch per batch)"),
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -16,6 +16,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
+#include <cstdlib>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -41,6 +43,9 @@ __global__ void k_sc_score(const ScDesc *, const DevCrop *, const double *, Crop
                            const ScParamsDev);
 __global__ void k_crop_apply(const ApplyDesc *, const int32_t *, int, const DevCrop *, const ScResult *);
 __global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
+// fused vertical-first resample (fi_fused.hip)
+int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
+                 const int32_t *ai, const float *af, int hw_pitch, int max_taps, int max_nbytes);
 }  // namespace fi
 
 using namespace fi;
@@ -101,11 +106,13 @@ struct fi_ctx {
   std::map<std::tuple<int, uint64_t, int, int, int, int, int, int>, AxisTable> axis_cache;
   std::map<std::tuple<int, int, int, int, uint64_t>, ScPlan> sc_cache;
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
+  std::map<const AxisTable *, RingTable> ring_cache;
+  bool fused = true;  // FI_DISABLE_FUSED=1 forces the generic two-pass path
 };
 
 static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
   if (b->cap >= bytes) return FI_OK;
-  if (b->p) hipFree(b->p);
+  if (b->p) (void)hipFree(b->p);
   b->p = nullptr;
   b->cap = 0;
   size_t cap = std::max(bytes + bytes / 4, (size_t)1 << 20);
@@ -118,7 +125,7 @@ static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
 }
 static int ensure_pinned(fi_ctx *c, size_t bytes) {
   if (c->pinned_cap >= bytes) return FI_OK;
-  if (c->pinned) hipHostFree(c->pinned);
+  if (c->pinned) (void)hipHostFree(c->pinned);
   c->pinned = nullptr;
   c->pinned_cap = 0;
   size_t cap = std::max(bytes + bytes / 4, (size_t)1 << 20);
@@ -135,7 +142,7 @@ static hipEvent_t get_event(fi_ctx *c) {
     return e;
   }
   hipEvent_t e;
-  hipEventCreate(&e);
+  (void)hipEventCreate(&e);
   return e;
 }
 struct Timer {
@@ -148,19 +155,19 @@ struct Timer {
     r.bytes = bytes;
     r.a = get_event(c);
     r.b = get_event(c);
-    hipEventRecord(r.a, c->stream);
+    (void)hipEventRecord(r.a, c->stream);
   }
   ~Timer() {
     if (!on) return;
-    hipEventRecord(r.b, c->stream);
+    (void)hipEventRecord(r.b, c->stream);
     c->pending.push_back(r);
   }
 };
 static void collect_timers(fi_ctx *c) {
   for (auto &r : c->pending) {
     float ms = 0;
-    hipEventSynchronize(r.b);
-    hipEventElapsedTime(&ms, r.a, r.b);
+    (void)hipEventSynchronize(r.b);
+    (void)hipEventElapsedTime(&ms, r.a, r.b);
     Stat &s = c->stats[r.name];
     s.ms += ms;
     s.launches += 1;
@@ -251,12 +258,16 @@ struct Exec {
   fi_smartcrop_params params;
 };
 
-static void add_axis(fi_ctx *c, Exec &E, int filter, double factor, int in_sampled, int out_size, int o0, int o1,
-                     bool sample, int in_src, DevAxis *out, std::map<const AxisTable *, DevAxis> &placed) {
+static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, int in_sampled, int out_size,
+                                 int o0, int o1, bool sample, int in_src, DevAxis *out,
+                                 std::map<const AxisTable *, DevAxis> &placed) {
   auto key = std::make_tuple(filter, dbits(factor), in_sampled, out_size, o0, o1, (int)sample, in_src);
   auto it = c->axis_cache.find(key);
   if (it == c->axis_cache.end()) {
-    if (c->axis_cache.size() > 4096) c->axis_cache.clear();
+    if (c->axis_cache.size() > 4096) {
+      c->axis_cache.clear();
+      c->ring_cache.clear();
+    }
     AxisTable t;
     build_axis(filter, factor, in_sampled, out_size, o0, o1, sample, in_src, &t);
     it = c->axis_cache.emplace(key, std::move(t)).first;
@@ -265,7 +276,7 @@ static void add_axis(fi_ctx *c, Exec &E, int filter, double factor, int in_sampl
   auto pit = placed.find(t);
   if (pit != placed.end()) {
     *out = pit->second;
-    return;
+    return t;
   }
   DevAxis d{};
   d.n = (int32_t)t->start.size();
@@ -280,8 +291,38 @@ static void add_axis(fi_ctx *c, Exec &E, int filter, double factor, int in_sampl
   d.maxtaps = t->maxtaps;
   d.src_lo = t->src_lo;
   d.src_hi = t->src_hi;
+  d.touched = t->touched;
   placed[t] = d;
   *out = d;
+  return t;
+}
+
+
+// Column strips of the fused kernel: <= 4096 source bytes (256 lanes x 16 B),
+// <= 512 output columns, horizontal tap table <= 32 KB of LDS.
+static bool fused_strips(const AxisTable &H, int ew, std::vector<FusedTile> *out) {
+  const int nx_max = std::max(1, std::min(512, 8192 / std::max(1, (int)H.maxtaps)));
+  for (int S = std::max(1, (ew + nx_max - 1) / nx_max); S <= ew; S++) {
+    out->clear();
+    bool ok = true;
+    for (int k = 0; k < S && ok; k++) {
+      FusedTile t{};
+      t.x0 = (int)((int64_t)ew * k / S);
+      t.x1 = (int)((int64_t)ew * (k + 1) / S);
+      if (t.x1 <= t.x0) continue;
+      int lo = 1 << 30, hi = 0;
+      for (int x = t.x0; x < t.x1; x++) {
+        lo = std::min(lo, H.start[x]);
+        hi = std::max(hi, H.start[x] + H.count[x]);
+      }
+      t.b0 = (3 * lo) / 16 * 16;
+      t.nbytes = (3 * hi + 15) / 16 * 16 - t.b0;
+      ok = t.nbytes <= 4096;
+      out->push_back(t);
+    }
+    if (ok) return true;
+  }
+  return false;
 }
 
 struct ScLaunchData {
@@ -476,9 +517,14 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
   std::vector<ScItem> sitems;
   std::vector<int> sc_of(n, -1);
   std::map<const AxisTable *, DevAxis> placed;
+  std::map<const RingTable *, std::array<int32_t, 4>> ring_placed;
+  std::vector<const RingTable *> fused_ring;
+  std::vector<const AxisTable *> fused_h;
+  std::vector<std::vector<FusedTile>> fused_strips_of;
+  std::vector<int> fused_img;  // indices into rd
   // per image resized-buffer workspace offsets (for smartcrop-apply)
   std::vector<size_t> res_off(n, 0);
-  double resize_bytes = 0, sc_bytes = 0;
+  double resize_bytes = 0;
   for (int i = 0; i < n; i++) {
     fi_image &im = imgs[i];
     int rc = plan_im(im, &plans[i]);
@@ -525,14 +571,55 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
     } else {
       d.dst = im.dst;
     }
-    int64_t src_bytes;
+    int64_t src_bytes = 0;
     if (!P.resize) {
       d.mode = 0;
       src_bytes = (int64_t)P.ew * P.eh * 3;
     } else {
-      add_axis(c, E, P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &d.v, placed);
-      add_axis(c, E, P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &d.h, placed);
-      if (!P.hfirst) {
+      const AxisTable *vt =
+          add_axis(c, E, P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &d.v, placed);
+      const AxisTable *ht =
+          add_axis(c, E, P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &d.h, placed);
+      const RingTable *ring = nullptr;
+      if (!P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0 &&
+          d.h.maxtaps <= 64) {
+        auto rit = c->ring_cache.find(vt);
+        if (rit == c->ring_cache.end()) {
+          RingTable rt;
+          if (!build_ring(*vt, &rt)) rt.K = 0;
+          rit = c->ring_cache.emplace(vt, std::move(rt)).first;
+        }
+        if (rit->second.K && rit->second.K <= 8) ring = &rit->second;  // K=16 would spill
+      }
+      std::vector<FusedTile> strips;
+      if (ring && !fused_strips(*ht, P.ew, &strips)) ring = nullptr;
+      if (ring) {
+        d.mode = 3;  // fused vertical-first
+        d.fused_k = ring->K;
+        d.ring_n = (int32_t)ring->rows.size();
+        auto pr = ring_placed.find(ring);
+        if (pr == ring_placed.end()) {
+          std::array<int32_t, 4> o;
+          o[0] = (int32_t)E.ai.size();
+          E.ai.insert(E.ai.end(), ring->rows.begin(), ring->rows.end());
+          o[1] = (int32_t)E.af.size();
+          E.af.insert(E.af.end(), ring->ringw.begin(), ring->ringw.end());
+          o[2] = (int32_t)E.ai.size();
+          E.ai.insert(E.ai.end(), ring->ringy.begin(), ring->ringy.end());
+          o[3] = (int32_t)E.ai.size();
+          E.ai.insert(E.ai.end(), ring->flush.begin(), ring->flush.end());
+          pr = ring_placed.emplace(ring, o).first;
+        }
+        d.ring_rows = pr->second[0];
+        d.ring_w = pr->second[1];
+        d.ring_y = pr->second[2];
+        d.ring_flush = pr->second[3];
+        fused_ring.push_back(ring);
+        fused_h.push_back(ht);
+        fused_strips_of.push_back(strips);
+        fused_img.push_back((int)rd.size());
+        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
+      } else if (!P.hfirst) {
         d.mode = 1;
         const int64_t b_lo = (int64_t)3 * d.h.src_lo / 8 * 8;
         const int64_t b_hi = std::min<int64_t>((int64_t)3 * P.W, ((int64_t)3 * d.h.src_hi + 7) / 8 * 8);
@@ -547,8 +634,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
         d.mid_cols = P.ew;
         d.mid_stride = (3 * P.ew + 7) / 8 * 8;
       }
-      d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
-      src_bytes = (int64_t)(d.v.src_hi - d.v.src_lo) * (d.h.src_hi - d.h.src_lo) * 3;
+      if (d.mode != 3) {
+        d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
+        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
+      }
     }
     resize_bytes += (double)src_bytes + (double)need;
     rd_of[i] = (int)rd.size();
@@ -566,7 +655,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       fi_smartcrop_default_options(&it.opt);
       sc_of[i] = (int)sitems.size();
       sitems.push_back(it);
-      sc_bytes += (double)need + 16.0;
+      (void)0;
     }
   }
   // smartcrop planning
@@ -606,8 +695,49 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
     if (sc_of[i] >= 0) SL.descs[sc_of[i]].img = rd[rd_of[i]].dst;
   // ---- build launches
   std::vector<int> m0, m1, m2;
-  for (size_t k = 0; k < rd.size(); k++) (rd[k].mode == 0 ? m0 : rd[k].mode == 1 ? m1 : m2).push_back((int)k);
+  for (size_t k = 0; k < rd.size(); k++) {
+    if (rd[k].mode == 3) continue;
+    (rd[k].mode == 0 ? m0 : rd[k].mode == 1 ? m1 : m2).push_back((int)k);
+  }
+  // fused tiles: (image, column strip, row band); grouped by ring size K
+  struct FusedGroup {
+    std::vector<FusedTile> tiles;
+    int pitch = 0, max_taps = 0, max_nbytes = 0;
+    size_t off = 0;
+  };
+  std::map<int, FusedGroup> fgroups;
+  {
+    const int nf = (int)fused_img.size();
+    for (int q = 0; q < nf; q++) {
+      const ResizeDesc &d = rd[fused_img[q]];
+      const RingTable &R = *fused_ring[q];
+      const AxisTable &H = *fused_h[q];
+      FusedGroup &G = fgroups[d.fused_k];
+      const std::vector<FusedTile> &strips = fused_strips_of[q];
+      // row bands: enough work items to fill the chip (>= ~1024 per batch)
+      const int per_img = (int)strips.size();
+      int B = (1024 + nf * per_img - 1) / (nf * per_img);
+      B = std::max(1, std::min(B, d.eh / 16 > 0 ? d.eh / 16 : 1));
+      for (int b = 0; b < B; b++) {
+        const int y0 = (int)((int64_t)d.eh * b / B), y1 = (int)((int64_t)d.eh * (b + 1) / B);
+        if (y1 <= y0) continue;
+        for (FusedTile t : strips) {
+          t.image = fused_img[q];
+          t.y0 = y0;
+          t.y1 = y1;
+          t.i0 = R.first_i[y0];
+          t.i1 = R.last_i[y1 - 1] + 1;
+          G.tiles.push_back(t);
+          G.pitch = std::max(G.pitch, t.x1 - t.x0);
+          G.max_nbytes = std::max(G.max_nbytes, t.nbytes);
+        }
+      }
+      G.max_taps = std::max(G.max_taps, (int)H.maxtaps);
+    }
+  }
   Blob &B = E.blob;
+  const size_t all_rd_off = B.addv(rd);
+  for (auto &g : fgroups) g.second.off = B.addv(g.second.tiles);
   auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
   auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
   Launch L0 = add_launch(B, rd, m0, eh_tiles);
@@ -677,6 +807,14 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       if (L0.tiles)
         hipLaunchKernelGGL(k_rs_copy, dim3(L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L0),
                            pre_p(L0), L0.n);
+      for (auto &g : fgroups) {
+        const FusedGroup &G = g.second;
+        if (G.tiles.empty()) continue;
+        const int pitch = (G.pitch + 3) & ~3;
+        if (launch_fused(c->stream, g.first, (const ResizeDesc *)(ab + all_rd_off), (const FusedTile *)(ab + G.off),
+                         (int)G.tiles.size(), ai, af, pitch, G.max_taps, G.max_nbytes) != 0)
+          return set_err(FI_EDEVICE, "fused resample launch rejected (K=%d, LDS budget)", g.first);
+      }
       if (L1a.tiles) {
         hipLaunchKernelGGL(k_rs_v_u8, dim3(L1a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L1a),
                            pre_p(L1a), L1a.n, ai, af);
@@ -919,6 +1057,7 @@ int fi_create(fi_ctx **out, int32_t device) {
     return set_err(FI_EDEVICE, "device %d is %s; libflyimg_hip.so is built for gfx950 only", device, prop.gcnArchName);
   fi_ctx *c = new fi_ctx();
   c->device = device;
+  if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return set_err(FI_EDEVICE, "hipStreamCreate failed");
@@ -929,14 +1068,14 @@ int fi_create(fi_ctx **out, int32_t device) {
 
 void fi_destroy(fi_ctx *c) {
   if (!c) return;
-  hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
   for (DevBuf *b : {&c->arena, &c->work, &c->io})
-    if (b->p) hipFree(b->p);
-  if (c->pinned) hipHostFree(c->pinned);
-  for (auto e : c->event_pool) hipEventDestroy(e);
-  hipStreamDestroy(c->stream);
+    if (b->p) (void)hipFree(b->p);
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
   delete c;
 }
 

@@ -27,9 +27,9 @@ struct DevAxis {
   int32_t count;  // arena offset of count[n]
   int32_t woff;   // arena offset of woff[n] (float units in weight area)
   int32_t maxtaps;
-  int32_t src_lo;  // min over start
-  int32_t src_hi;  // max over start+count (exclusive)
-  int32_t pad;
+  int32_t src_lo;   // min over start
+  int32_t src_hi;   // max over start+count (exclusive)
+  int32_t touched;  // source indices with a non-zero merged weight
 };
 
 // Per-image descriptor of the resample path (generic two-pass kernels and
@@ -51,11 +51,14 @@ struct ResizeDesc {
   uint8_t *dst;
   int64_t dst_stride;
   int32_t out_w, out_h, out_c;  // post-rotate dims
-  int32_t fused_k;              // ring slots for the fused kernel (0 = not fused)
-  int32_t vring;                // arena offset of per-source-row slot weights (fused)
-  int32_t vring_rows;           // number of source rows in ring table
-  int32_t vring_r0;             // first source row
-  int32_t pad2;
+  // fused vertical-first kernel: list of touched source rows and, per list
+  // row, the weight of each of the K ring slots and the output row owning it
+  int32_t fused_k;     // ring slots (0 = not fused)
+  int32_t ring_n;      // touched source rows
+  int32_t ring_rows;   // ai offset: source row index [ring_n]
+  int32_t ring_w;      // af offset: slot weights [ring_n][K]
+  int32_t ring_y;      // ai offset: slot owner output row or -1 [ring_n][K]
+  int32_t ring_flush;  // ai offset: output rows [lo, hi) completing at list row [ring_n][2]
 };
 
 // Fused-kernel work item: one (image, column strip, row band).
@@ -64,7 +67,7 @@ struct FusedTile {
   int32_t x0, x1;      // output columns [x0, x1) of the extent window
   int32_t y0, y1;      // output rows    [y0, y1)
   int32_t b0, nbytes;  // source byte range (16-B aligned start, length) of the strip
-  int32_t r0, r1;      // source rows streamed
+  int32_t i0, i1;      // range of the image's touched-row list streamed
 };
 
 // smartcrop crop window in the analysed image (smartcrop.py crops()).

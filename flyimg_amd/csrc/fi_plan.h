@@ -37,8 +37,21 @@ int plan_im(const fi_image &img, ImPlan *p);
 struct AxisTable {
   std::vector<int32_t> start, count, woff;
   std::vector<float> w;
-  int32_t maxtaps = 0, src_lo = 0, src_hi = 0;
+  int32_t maxtaps = 0, src_lo = 0, src_hi = 0, touched = 0;
 };
+// Ring table of the fused vertical-first kernel (fi_fused.hip): the list of
+// touched source rows, and per list row the weight for each of the K ring
+// slots (slot = output row % K) plus the output rows that complete there.
+struct RingTable {
+  int K = 0;
+  std::vector<int32_t> rows, ringy, flush;
+  std::vector<float> ringw;
+  std::vector<int32_t> first_i, last_i;  // per output row, list-row span
+};
+// false when the fused kernel cannot take this axis (more than 16 output rows
+// active on one source row, or a non-monotone tap layout).
+bool build_ring(const AxisTable &v, RingTable *rt);
+
 // Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)
 // to `out_size`; taps mapped back to the `in_src` source indices through the
 // SampleImage offsets (identity when !sample) and merged.

@@ -29,6 +29,25 @@ def ctx():
     c.close()
 
 
+@pytest.fixture(scope="module", params=["fused", "generic"])
+def rctx(request):
+    """Resample path under test: the fused vertical-first kernel (default) or
+    the generic two-pass kernels (FI_DISABLE_FUSED=1 at context creation)."""
+    import os
+
+    old = os.environ.get("FI_DISABLE_FUSED")
+    os.environ["FI_DISABLE_FUSED"] = "1" if request.param == "generic" else "0"
+    try:
+        c = Context(0)
+    finally:
+        if old is None:
+            os.environ.pop("FI_DISABLE_FUSED", None)
+        else:
+            os.environ["FI_DISABLE_FUSED"] = old
+    yield c
+    c.close()
+
+
 def _opts(exact_all):
     o = L.FiSmartcropOptions()
     L.lib().fi_smartcrop_default_options(o)
@@ -148,7 +167,8 @@ def _oracle_flags(flags):
 
 
 @pytest.mark.parametrize("case", RESIZE_CASES, ids=[c[0] for c in RESIZE_CASES])
-def test_resize_within_one_lsb_of_oracle(ctx, case):
+def test_resize_within_one_lsb_of_oracle(rctx, case):
+    ctx = rctx
     name, W, H, tw, th, flags, rot = case
     src = synth_rgb(W, H, 1000 + W + H)
     grav = L.GRAVITY["North"] if name == "north_gravity" else L.GRAVITY["Center"]
@@ -158,7 +178,8 @@ def test_resize_within_one_lsb_of_oracle(ctx, case):
     _cmp(outs[0], ref, name)
 
 
-def test_mixed_batch_one_call(ctx):
+def test_mixed_batch_one_call(rctx):
+    ctx = rctx
     imgs, ops, refs = [], [], []
     for k, case in enumerate(RESIZE_CASES):
         name, W, H, tw, th, flags, rot = case
@@ -177,7 +198,8 @@ def test_mixed_batch_one_call(ctx):
     (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray,smc_1"),
     (3840, 2160, "w_512,h_512,c_1,smc_1"),
 ])
-def test_full_size_pipeline_smartcrop_box_bit_exact(ctx, W, H, opts):
+def test_full_size_pipeline_smartcrop_box_bit_exact(rctx, W, H, opts):
+    ctx = rctx
     """BASELINE sizes: the crop box computed on the GPU-resized pixels equals
     the oracle's smartcrop on those same pixels; apply == crop of the box."""
     from flyimg_amd.processor import ImageProcessor, OptionsBag
