@@ -319,6 +319,17 @@ bool build_ring(const AxisTable &v, RingTable *rt) {
       f[1] = y + 1;
     }
   }
+  // padding rows (fi_fused.hip kPad): zero weights, no flush, last source row
+  const int kPad = 16;  // >= 2 * kDepth of fi_fused.hip
+  for (int q = 0; q < kPad; q++) {
+    rt->rows.push_back(rt->rows.back());
+    for (int k = 0; k < K; k++) {
+      rt->ringw.push_back(0.0f);
+      rt->ringy.push_back(-1);
+    }
+    rt->flush.push_back(0);
+    rt->flush.push_back(0);
+  }
   return true;
 }
 
