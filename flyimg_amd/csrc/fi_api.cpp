@@ -107,6 +107,7 @@ struct fi_ctx {
   std::map<std::tuple<int, int, int, int, uint64_t>, ScPlan> sc_cache;
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
   std::map<const AxisTable *, RingTable> ring_cache;
+  std::map<const AxisTable *, std::vector<StripTab>> strip_cache;
   bool fused = true;  // FI_DISABLE_FUSED=1 forces the generic two-pass path
 };
 
@@ -267,6 +268,7 @@ static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, 
     if (c->axis_cache.size() > 4096) {
       c->axis_cache.clear();
       c->ring_cache.clear();
+      c->strip_cache.clear();
     }
     AxisTable t;
     build_axis(filter, factor, in_sampled, out_size, o0, o1, sample, in_src, &t);
@@ -298,27 +300,48 @@ static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, 
 }
 
 
-// Column strips of the fused kernel: <= 4096 source bytes (256 lanes x 16 B),
-// <= 512 output columns, horizontal tap table <= 32 KB of LDS.
-static bool fused_strips(const AxisTable &H, int ew, std::vector<FusedTile> *out) {
-  const int nx_max = std::max(1, std::min(512, 8192 / std::max(1, (int)H.maxtaps)));
+// Column strips of the fused kernel (fi_fused.hip): <= kFusedStripBytes
+// source bytes (256 streaming lanes x 8 B), <= 768 output columns, horizontal
+// tap table <= 32 KB of LDS.  Every column's window is padded (zero weights)
+// to the strip's longest, so the epilogue loop has a uniform trip count.
+struct StripTab {
+  FusedTile t;
+  std::vector<int32_t> starts;  // [nx]
+  std::vector<float> wT;        // [htaps][nx]
+};
+static constexpr int kFusedStripBytes = 2048;
+static bool fused_strips(const AxisTable &H, int ew, std::vector<StripTab> *out) {
+  const int nx_max = std::max(1, std::min(768, 8192 / std::max(1, (int)H.maxtaps)));
   for (int S = std::max(1, (ew + nx_max - 1) / nx_max); S <= ew; S++) {
     out->clear();
     bool ok = true;
     for (int k = 0; k < S && ok; k++) {
-      FusedTile t{};
+      StripTab st;
+      FusedTile &t = st.t;
+      t = FusedTile{};
       t.x0 = (int)((int64_t)ew * k / S);
       t.x1 = (int)((int64_t)ew * (k + 1) / S);
       if (t.x1 <= t.x0) continue;
-      int lo = 1 << 30, hi = 0;
+      int lo = 1 << 30, hi = 0, T = 0;
       for (int x = t.x0; x < t.x1; x++) {
         lo = std::min(lo, H.start[x]);
         hi = std::max(hi, H.start[x] + H.count[x]);
+        T = std::max(T, H.count[x]);
       }
       t.b0 = (3 * lo) / 16 * 16;
       t.nbytes = (3 * hi + 15) / 16 * 16 - t.b0;
-      ok = t.nbytes <= 4096;
-      out->push_back(t);
+      t.htaps = T;
+      ok = t.nbytes <= kFusedStripBytes;
+      const int nx = t.x1 - t.x0;
+      st.starts.resize(nx);
+      st.wT.assign((size_t)T * nx, 0.0f);
+      for (int x = t.x0; x < t.x1; x++) {
+        const int s0 = H.start[x], c = H.count[x];
+        const int sp = std::max(lo, std::min(s0, hi - T));
+        st.starts[x - t.x0] = sp;
+        for (int j = 0; j < c; j++) st.wT[(size_t)(s0 - sp + j) * nx + (x - t.x0)] = H.w[H.woff[x] + j];
+      }
+      out->push_back(std::move(st));
     }
     if (ok) return true;
   }
@@ -520,7 +543,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
   std::map<const RingTable *, std::array<int32_t, 4>> ring_placed;
   std::vector<const RingTable *> fused_ring;
   std::vector<const AxisTable *> fused_h;
-  std::vector<std::vector<FusedTile>> fused_strips_of;
+  std::vector<const std::vector<StripTab> *> fused_strips_of;
+  std::map<const StripTab *, std::pair<int32_t, int32_t>> strip_placed;
   std::vector<int> fused_img;  // indices into rd
   // per image resized-buffer workspace offsets (for smartcrop-apply)
   std::vector<size_t> res_off(n, 0);
@@ -591,8 +615,19 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
         }
         if (rit->second.K && rit->second.K <= 8) ring = &rit->second;  // K=16 would spill
       }
-      std::vector<FusedTile> strips;
-      if (ring && !fused_strips(*ht, P.ew, &strips)) ring = nullptr;
+      const std::vector<StripTab> *strips = nullptr;
+      if (ring) {
+        auto sit = c->strip_cache.find(ht);
+        if (sit == c->strip_cache.end()) {
+          std::vector<StripTab> st;
+          if (!fused_strips(*ht, P.ew, &st)) st.clear();
+          sit = c->strip_cache.emplace(ht, std::move(st)).first;
+        }
+        if (sit->second.empty())
+          ring = nullptr;
+        else
+          strips = &sit->second;
+      }
       if (ring) {
         d.mode = 3;  // fused vertical-first
         d.fused_k = ring->K;
@@ -713,7 +748,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       const RingTable &R = *fused_ring[q];
       const AxisTable &H = *fused_h[q];
       FusedGroup &G = fgroups[d.fused_k];
-      const std::vector<FusedTile> &strips = fused_strips_of[q];
+      const std::vector<StripTab> &strips = *fused_strips_of[q];
       // row bands: enough work items to fill the chip (>= ~1024 per batch)
       const int per_img = (int)strips.size();
       int B = (1024 + nf * per_img - 1) / (nf * per_img);
@@ -721,7 +756,18 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       for (int b = 0; b < B; b++) {
         const int y0 = (int)((int64_t)d.eh * b / B), y1 = (int)((int64_t)d.eh * (b + 1) / B);
         if (y1 <= y0) continue;
-        for (FusedTile t : strips) {
+        for (const StripTab &st : strips) {
+          auto sp = strip_placed.find(&st);
+          if (sp == strip_placed.end()) {
+            const int32_t so = (int32_t)E.ai.size();
+            E.ai.insert(E.ai.end(), st.starts.begin(), st.starts.end());
+            const int32_t wo = (int32_t)E.af.size();
+            E.af.insert(E.af.end(), st.wT.begin(), st.wT.end());
+            sp = strip_placed.emplace(&st, std::make_pair(so, wo)).first;
+          }
+          FusedTile t = st.t;
+          t.hstart = sp->second.first;
+          t.hw = sp->second.second;
           t.image = fused_img[q];
           t.y0 = y0;
           t.y1 = y1;
@@ -730,9 +776,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
           G.tiles.push_back(t);
           G.pitch = std::max(G.pitch, t.x1 - t.x0);
           G.max_nbytes = std::max(G.max_nbytes, t.nbytes);
+          G.max_taps = std::max(G.max_taps, t.htaps);
         }
       }
-      G.max_taps = std::max(G.max_taps, (int)H.maxtaps);
+      (void)H;
     }
   }
   Blob &B = E.blob;

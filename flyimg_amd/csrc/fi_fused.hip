@@ -4,7 +4,7 @@
 // 512-thread workgroup per item, two wave roles:
 //
 //   streaming waves 0-3: every touched source row of the strip is read once
-//     (16 B/lane global_load_dwordx4, kDepth rows in flight per lane) into a
+//     (8 B/lane global_load_dwordx2, kDepth rows in flight per lane) into a
 //     K-slot ring of fp32 accumulators (slot = output row % K, weights are
 //     wave-uniform SGPRs).  When an output row's last tap has arrived its
 //     slot is rounded to Q16 (ClampToQuantum) and written to an LDS row
@@ -31,6 +31,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
 typedef __attribute__((address_space(1))) uint8_t g_u8;
 __device__ __forceinline__ u32x4 gload16(const uint8_t *p) { return *(g_u32x4 *)(p); }
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const u32x2 g_u32x2;
+__device__ __forceinline__ u32x2 gload8(const uint8_t *p) { return *(g_u32x2 *)(p); }
 
 // ClampToQuantum (Q16, non-HDRI) without branches: med3 clamp, +0.5,
 // truncate.  Equal to "v<=0 ? 0 : v>=65535 ? 65535 : (int)(v+0.5f)" for every
@@ -83,12 +86,24 @@ __device__ __forceinline__ void unpack16(const u32x4 v, float *f) {
   }
 }
 
-constexpr int kDepth = 8;  // source rows in flight per streaming lane (host pads 2*kDepth rows)
-constexpr int kStreamThreads = 256;
-constexpr int kThreads = 512;
+__device__ __forceinline__ void unpack8(const u32x2 v, float *f) {
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint32_t w = q ? v.y : v.x;
+    f[4 * q + 0] = (float)(w & 255u);
+    f[4 * q + 1] = (float)((w >> 8) & 255u);
+    f[4 * q + 2] = (float)((w >> 16) & 255u);
+    f[4 * q + 3] = (float)(w >> 24);
+  }
+}
+
+constexpr int kDepth = 8;           // source rows in flight per streaming lane (host pads 16 rows)
+constexpr int kLaneBytes = 8;       // source bytes per streaming lane (dwordx2)
+constexpr int kStreamThreads = 256; // streaming waves 0-3 -> strips of <= 2048 bytes
+constexpr int kThreads = 512;       // + epilogue waves 4-7
 
 template <int K>
-__global__ __launch_bounds__(kThreads, 2) void k_rs_fused(const ResizeDesc *__restrict__ descs,
+__global__ __launch_bounds__(kThreads, 4) void k_rs_fused(const ResizeDesc *__restrict__ descs,
                                                           const FusedTile *__restrict__ tiles,
                                                           const int32_t *__restrict__ ai,
                                                           const float *__restrict__ af, int lds_hw_pitch) {
@@ -97,61 +112,62 @@ __global__ __launch_bounds__(kThreads, 2) void k_rs_fused(const ResizeDesc *__re
   const ResizeDesc &D = descs[T.image];
   const int tid = threadIdx.x;
   const int nx = T.x1 - T.x0;
-  const int maxT = D.h.maxtaps;
+  const int HT = T.htaps;
   const int NBp = (T.nbytes + 63) & ~63;
-  float *hw = lds;                          // [maxT][lds_hw_pitch]
-  float *vrow = lds + maxT * lds_hw_pitch;  // [2][NBp]
-  const int32_t *hstart = ai + D.h.start, *hcount = ai + D.h.count, *hwoff = ai + D.h.woff;
-  // horizontal tap table of this strip -> LDS, transposed (conflict-free reads)
-  for (int i = tid; i < nx * maxT; i += kThreads) {
-    const int x = i % nx, j = i / nx;
-    const int gx = T.x0 + x;
-    hw[j * lds_hw_pitch + x] = j < hcount[gx] ? af[hwoff[gx] + j] : 0.0f;
+  float *hw = lds;                         // [HT][lds_hw_pitch]
+  int *hs = (int *)(lds + HT * lds_hw_pitch);  // [lds_hw_pitch] window start (LDS row offset)
+  float *vrow = lds + (HT + 1) * lds_hw_pitch;  // [2][NBp]
+  // strip's horizontal table -> LDS (already transposed and padded by the host)
+  for (int i = tid; i < nx * HT; i += kThreads) {
+    const int j = i / nx, x = i - j * nx;
+    hw[j * lds_hw_pitch + x] = af[T.hw + i];
   }
+  for (int x = tid; x < nx; x += kThreads) hs[x] = 3 * ai[T.hstart + x] - T.b0;
   __syncthreads();
 
   if (tid < kStreamThreads) {
     // ------------------------------------------------------------ streaming
-    const bool vlane = tid * 16 < T.nbytes;
+    const bool vlane = tid * kLaneBytes < T.nbytes;
     const float *ring_w = af + D.ring_w;       // [n + pad][K]
     const int32_t *rows = ai + D.ring_rows;    // source row per list index
     const int32_t *flush = ai + D.ring_flush;  // [n + pad][2] output rows completing at list row
     // lanes past the strip load lane 0's bytes: every load is unconditional
-    const uint8_t *src = D.src + T.b0 + (vlane ? (int64_t)tid * 16 : 0);
+    const uint8_t *src = D.src + T.b0 + (vlane ? (int64_t)tid * kLaneBytes : 0);
     const int64_t sstride = D.src_stride;
-    float acc[K][16];
+    float acc[K][kLaneBytes];
 #pragma unroll
     for (int k = 0; k < K; k++)
 #pragma unroll
-      for (int e = 0; e < 16; e++) acc[k][e] = 0.0f;
+      for (int e = 0; e < kLaneBytes; e++) acc[k][e] = 0.0f;
     // The ring list is padded on the host with zero-weight rows so the
     // unrolled body runs unconditionally (a guarded body makes the number of
     // outstanding loads path dependent -> vmcnt(0) at the loop head).  Issue
     // order of the prologue must match the loop's (pf[0] oldest).
-    u32x4 pf[kDepth];
+    u32x2 pf[kDepth];
 #pragma unroll
     for (int d = 0; d < kDepth; d++) {
-      pf[d] = gload16(src + (int64_t)rows[T.i0 + d] * sstride);
+      pf[d] = gload8(src + (int64_t)rows[T.i0 + d] * sstride);
       __builtin_amdgcn_sched_barrier(0);
     }
+    float wc[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) wc[k] = ring_w[T.i0 * K + k];
     for (int ib = T.i0; ib < T.i1; ib += kDepth) {
 #pragma unroll
       for (int d = 0; d < kDepth; d++) {
         const int i = ib + d;
-        float f[16];
-        unpack16(pf[d], f);
-        pf[d] = gload16(src + (int64_t)rows[i + kDepth] * sstride);
-        float w[K];
+        float f[kLaneBytes];
+        unpack8(pf[d], f);
+        pf[d] = gload8(src + (int64_t)rows[i + kDepth] * sstride);
+        float wn[K];  // next row's slot weights (scalar loads one row ahead)
 #pragma unroll
-        for (int k = 0; k < K; k++) w[k] = ring_w[i * K + k];
-        // slots of rows outside the band accumulate too; never written out
+        for (int k = 0; k < K; k++) wn[k] = ring_w[(i + 1) * K + k];
+        // every slot, straight line (zero weights cost less than branches);
+        // slots of rows outside the band accumulate too and are never written
 #pragma unroll
-        for (int k = 0; k < K; k++) {
-          if (w[k] != 0.0f) {
+        for (int k = 0; k < K; k++)
 #pragma unroll
-            for (int e = 0; e < 16; e++) acc[k][e] = fmaf(w[k], f[e], acc[k][e]);
-          }
-        }
+          for (int e = 0; e < kLaneBytes; e++) acc[k][e] = fmaf(wc[k], f[e], acc[k][e]);
         const int ylo = flush[2 * i], yhi = flush[2 * i + 1];
         for (int y = ylo; y < yhi; y++) {
           const int ks = y % K;
@@ -161,9 +177,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_rs_fused(const ResizeDesc *__re
           for (int k = 0; k < K; k++) {
             if (k == ks) {
               if (inband && vlane) {
-                float4 *o = reinterpret_cast<float4 *>(buf + tid * 16);
+                float4 *o = reinterpret_cast<float4 *>(buf + tid * kLaneBytes);
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
+                for (int q = 0; q < kLaneBytes / 4; q++) {
                   float4 v;
                   v.x = clamp_q16_bf(acc[k][4 * q + 0] * 257.0f);
                   v.y = clamp_q16_bf(acc[k][4 * q + 1] * 257.0f);
@@ -173,50 +189,32 @@ __global__ __launch_bounds__(kThreads, 2) void k_rs_fused(const ResizeDesc *__re
                 }
               }
 #pragma unroll
-              for (int e = 0; e < 16; e++) acc[k][e] = 0.0f;
+              for (int e = 0; e < kLaneBytes; e++) acc[k][e] = 0.0f;
             }
           }
           if (inband) __syncthreads();  // row y ready in buf[y & 1]
         }
+#pragma unroll
+        for (int k = 0; k < K; k++) wc[k] = wn[k];
       }
     }
   } else {
     // ------------------------------------------------------------- epilogue
     const int h = tid - kStreamThreads;
-    int hb0 = 0, hn0 = 0, hb1 = 0, hn1 = 0;
-    if (h < nx) {
-      hb0 = 3 * hstart[T.x0 + h] - T.b0;
-      hn0 = hcount[T.x0 + h];
-    }
-    if (h + 256 < nx) {
-      hb1 = 3 * hstart[T.x0 + h + 256] - T.b0;
-      hn1 = hcount[T.x0 + h + 256];
-    }
     for (int y = T.y0; y < T.y1; y++) {
       __syncthreads();
       const float *buf = vrow + (y & 1) * NBp;
-      if (h < nx) {
+      for (int x = h; x < nx; x += kThreads - kStreamThreads) {
+        const float *p = buf + hs[x];
         float r = 0.f, g = 0.f, b = 0.f;
-        const float *p = buf + hb0;
-        for (int j = 0; j < hn0; j++) {
-          const float w = hw[j * lds_hw_pitch + h];
+#pragma unroll 4
+        for (int j = 0; j < HT; j++) {
+          const float w = hw[j * lds_hw_pitch + x];
           r = fmaf(w, p[3 * j + 0], r);
           g = fmaf(w, p[3 * j + 1], g);
           b = fmaf(w, p[3 * j + 2], b);
         }
-        store_pixel_f(D, T.x0 + h, y, (uint32_t)clamp_q16_bf(r), (uint32_t)clamp_q16_bf(g),
-                      (uint32_t)clamp_q16_bf(b));
-      }
-      if (h + 256 < nx) {
-        float r = 0.f, g = 0.f, b = 0.f;
-        const float *p = buf + hb1;
-        for (int j = 0; j < hn1; j++) {
-          const float w = hw[j * lds_hw_pitch + h + 256];
-          r = fmaf(w, p[3 * j + 0], r);
-          g = fmaf(w, p[3 * j + 1], g);
-          b = fmaf(w, p[3 * j + 2], b);
-        }
-        store_pixel_f(D, T.x0 + h + 256, y, (uint32_t)clamp_q16_bf(r), (uint32_t)clamp_q16_bf(g),
+        store_pixel_f(D, T.x0 + x, y, (uint32_t)clamp_q16_bf(r), (uint32_t)clamp_q16_bf(g),
                       (uint32_t)clamp_q16_bf(b));
       }
     }
@@ -226,7 +224,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_rs_fused(const ResizeDesc *__re
 int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
                  const int32_t *ai, const float *af, int hw_pitch, int max_taps, int max_nbytes) {
   const int NBp = (max_nbytes + 63) & ~63;
-  const size_t lds = (size_t)max_taps * hw_pitch * 4 + (size_t)2 * NBp * 4;
+  const size_t lds = (size_t)(max_taps + 1) * hw_pitch * 4 + (size_t)2 * NBp * 4;
   if (lds > 160 * 1024) return -1;
   switch (K) {
     case 4:

@@ -68,6 +68,9 @@ struct FusedTile {
   int32_t y0, y1;      // output rows    [y0, y1)
   int32_t b0, nbytes;  // source byte range (16-B aligned start, length) of the strip
   int32_t i0, i1;      // range of the image's touched-row list streamed
+  int32_t htaps;       // horizontal taps of every column of the strip (zero padded)
+  int32_t hstart;      // ai offset: first source column of each column's window [nx]
+  int32_t hw;          // af offset: weights, transposed [htaps][nx]
 };
 
 // smartcrop crop window in the analysed image (smartcrop.py crops()).
