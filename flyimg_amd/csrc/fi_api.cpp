@@ -89,6 +89,11 @@ struct TimedRange {
   double bytes;
 };
 
+struct StripTab {
+  FusedTile t;
+  std::vector<int32_t> starts;  // [nx]
+  std::vector<float> wT;        // [htaps][nx]
+};
 struct fi_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -304,11 +309,6 @@ static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, 
 // source bytes (256 streaming lanes x 8 B), <= 768 output columns, horizontal
 // tap table <= 32 KB of LDS.  Every column's window is padded (zero weights)
 // to the strip's longest, so the epilogue loop has a uniform trip count.
-struct StripTab {
-  FusedTile t;
-  std::vector<int32_t> starts;  // [nx]
-  std::vector<float> wT;        // [htaps][nx]
-};
 static constexpr int kFusedStripBytes = 2048;
 static bool fused_strips(const AxisTable &H, int ew, std::vector<StripTab> *out) {
   const int nx_max = std::max(1, std::min(768, 8192 / std::max(1, (int)H.maxtaps)));
