@@ -20,6 +20,8 @@
 // once.  See DESIGN.md "Fused resample kernel".
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "fi_internal.h"
 
@@ -44,8 +46,14 @@ __device__ __forceinline__ float clamp_q16_bf(float v) {
 __device__ __forceinline__ uint8_t q16_to_u8f(uint32_t q) {  // ScaleQuantumToChar
   return (uint8_t)(((q + 128u) - ((q + 128u) >> 8)) >> 8);
 }
-__device__ __forceinline__ void store_pixel_f(const ResizeDesc &D, int x, int y, uint32_t r, uint32_t g,
-                                              uint32_t b) {
+// Epilogue constants of one image, held in registers (a reference into the
+// descriptor array would be re-read after every store: the stores may alias).
+struct Epi {
+  uint8_t *dst;
+  int64_t stride;
+  int ew, eh, rot, gray;
+};
+__device__ __forceinline__ void store_pixel_f(const Epi &D, int x, int y, uint32_t r, uint32_t g, uint32_t b) {
   int dx = x, dy = y;
   if (D.rot == 90) {
     dx = D.eh - 1 - y;
@@ -57,7 +65,7 @@ __device__ __forceinline__ void store_pixel_f(const ResizeDesc &D, int x, int y,
     dx = y;
     dy = D.ew - 1 - x;
   }
-  g_u8 *o = (g_u8 *)(D.dst + (int64_t)dy * D.dst_stride);
+  g_u8 *o = (g_u8 *)(D.dst + (int64_t)dy * D.stride);
   if (D.gray) {  // -colorspace Gray: Rec709Luma on gamma-encoded Q16
     const double gv = 0.212656 * (double)r + 0.715158 * (double)g + 0.072186 * (double)b;
     uint32_t q;
@@ -97,12 +105,16 @@ __device__ __forceinline__ void unpack8(const u32x2 v, float *f) {
   }
 }
 
-constexpr int kDepth = 8;           // source rows in flight per streaming lane (host pads 16 rows)
+// source rows in flight per streaming lane is the template parameter DEPTH
+// (host pads every ring list with 32 zero-weight rows >= 2 * DEPTH)
 constexpr int kLaneBytes = 8;       // source bytes per streaming lane (dwordx2)
 constexpr int kStreamThreads = 256; // streaming waves 0-3 -> strips of <= 2048 bytes
 constexpr int kThreads = 512;       // + epilogue waves 4-7
 
-template <int K>
+// MODE: 0 = production; 1 = ablation without epilogue work (barriers only);
+// 2 = ablation without the vertical FMAs (loads + flushes only).  The
+// ablations produce wrong pixels and exist for profiling (FI_FUSED_VARIANT).
+template <int K, int DEPTH, int MODE>
 __global__ __launch_bounds__(kThreads, 4) void k_rs_fused(const ResizeDesc *__restrict__ descs,
                                                           const FusedTile *__restrict__ tiles,
                                                           const int32_t *__restrict__ ai,
@@ -143,33 +155,44 @@ __global__ __launch_bounds__(kThreads, 4) void k_rs_fused(const ResizeDesc *__re
     // unrolled body runs unconditionally (a guarded body makes the number of
     // outstanding loads path dependent -> vmcnt(0) at the loop head).  Issue
     // order of the prologue must match the loop's (pf[0] oldest).
-    u32x2 pf[kDepth];
+    u32x2 pf[DEPTH];
 #pragma unroll
-    for (int d = 0; d < kDepth; d++) {
+    for (int d = 0; d < DEPTH; d++) {
       pf[d] = gload8(src + (int64_t)rows[T.i0 + d] * sstride);
       __builtin_amdgcn_sched_barrier(0);
     }
+    // Per-row metadata (the row to prefetch next, the K slot weights, the
+    // output rows completing) is loaded ONE ROW AHEAD: scalar loads can only
+    // be waited with lgkmcnt(0), so a value loaded and used in the same row
+    // exposes the scalar-cache/L2 latency on every row.
     float wc[K];
 #pragma unroll
     for (int k = 0; k < K; k++) wc[k] = ring_w[T.i0 * K + k];
-    for (int ib = T.i0; ib < T.i1; ib += kDepth) {
+    int rnext = rows[T.i0 + DEPTH];
+    int f0 = flush[2 * T.i0], f1 = flush[2 * T.i0 + 1];
+    for (int ib = T.i0; ib < T.i1; ib += DEPTH) {
 #pragma unroll
-      for (int d = 0; d < kDepth; d++) {
+      for (int d = 0; d < DEPTH; d++) {
         const int i = ib + d;
-        float f[kLaneBytes];
-        unpack8(pf[d], f);
-        pf[d] = gload8(src + (int64_t)rows[i + kDepth] * sstride);
-        float wn[K];  // next row's slot weights (scalar loads one row ahead)
+        // metadata of row i + 1
+        float wn[K];
 #pragma unroll
         for (int k = 0; k < K; k++) wn[k] = ring_w[(i + 1) * K + k];
-        // every slot, straight line (zero weights cost less than branches);
-        // slots of rows outside the band accumulate too and are never written
+        const int rn = rows[i + 1 + DEPTH];
+        const int g0 = flush[2 * (i + 1)], g1 = flush[2 * (i + 1) + 1];
+        float f[kLaneBytes];
+        unpack8(pf[d], f);
+        pf[d] = gload8(src + (int64_t)rnext * sstride);
+        if (MODE != 2) {
 #pragma unroll
-        for (int k = 0; k < K; k++)
+          for (int k = 0; k < K; k++)
 #pragma unroll
-          for (int e = 0; e < kLaneBytes; e++) acc[k][e] = fmaf(wc[k], f[e], acc[k][e]);
-        const int ylo = flush[2 * i], yhi = flush[2 * i + 1];
-        for (int y = ylo; y < yhi; y++) {
+            for (int e = 0; e < kLaneBytes; e++) acc[k][e] = fmaf(wc[k], f[e], acc[k][e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < kLaneBytes; e++) acc[0][e] += f[e];
+        }
+        for (int y = f0; y < f1; y++) {
           const int ks = y % K;
           const bool inband = y >= T.y0 && y < T.y1;
           float *buf = vrow + (y & 1) * NBp;
@@ -196,13 +219,24 @@ __global__ __launch_bounds__(kThreads, 4) void k_rs_fused(const ResizeDesc *__re
         }
 #pragma unroll
         for (int k = 0; k < K; k++) wc[k] = wn[k];
+        rnext = rn;
+        f0 = g0;
+        f1 = g1;
       }
     }
   } else {
     // ------------------------------------------------------------- epilogue
     const int h = tid - kStreamThreads;
+    Epi E;
+    E.dst = D.dst;
+    E.stride = D.dst_stride;
+    E.ew = D.ew;
+    E.eh = D.eh;
+    E.rot = D.rot;
+    E.gray = D.gray;
     for (int y = T.y0; y < T.y1; y++) {
       __syncthreads();
+      if (MODE == 1) continue;
       const float *buf = vrow + (y & 1) * NBp;
       for (int x = h; x < nx; x += kThreads - kStreamThreads) {
         const float *p = buf + hs[x];
@@ -214,7 +248,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_rs_fused(const ResizeDesc *__re
           g = fmaf(w, p[3 * j + 1], g);
           b = fmaf(w, p[3 * j + 2], b);
         }
-        store_pixel_f(D, T.x0 + x, y, (uint32_t)clamp_q16_bf(r), (uint32_t)clamp_q16_bf(g),
+        store_pixel_f(E, T.x0 + x, y, (uint32_t)clamp_q16_bf(r), (uint32_t)clamp_q16_bf(g),
                       (uint32_t)clamp_q16_bf(b));
       }
     }
@@ -226,16 +260,24 @@ int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile 
   const int NBp = (max_nbytes + 63) & ~63;
   const size_t lds = (size_t)(max_taps + 1) * hw_pitch * 4 + (size_t)2 * NBp * 4;
   if (lds > 160 * 1024) return -1;
-  switch (K) {
-    case 4:
-      hipLaunchKernelGGL(k_rs_fused<4>, dim3(ntiles), dim3(kThreads), lds, s, descs, tiles, ai, af, hw_pitch);
-      break;
-    case 8:
-      hipLaunchKernelGGL(k_rs_fused<8>, dim3(ntiles), dim3(kThreads), lds, s, descs, tiles, ai, af, hw_pitch);
-      break;
-    default:
-      return -2;
+  static const char *variant = getenv("FI_FUSED_VARIANT");  // profiling ablations only
+  const int v = !variant ? 0 : !strcmp(variant, "d16") ? 1 : !strcmp(variant, "noepi") ? 2
+              : !strcmp(variant, "noflops") ? 3 : 0;
+#define FI_LAUNCH(KK, DD, MM) \
+  hipLaunchKernelGGL((k_rs_fused<KK, DD, MM>), dim3(ntiles), dim3(kThreads), lds, s, descs, tiles, ai, af, hw_pitch)
+  if (K == 4) {
+    FI_LAUNCH(4, 8, 0);
+  } else if (K == 8) {
+    switch (v) {
+      case 1: FI_LAUNCH(8, 16, 0); break;
+      case 2: FI_LAUNCH(8, 8, 1); break;
+      case 3: FI_LAUNCH(8, 8, 2); break;
+      default: FI_LAUNCH(8, 8, 0); break;
+    }
+  } else {
+    return -2;
   }
+#undef FI_LAUNCH
   return 0;
 }
 

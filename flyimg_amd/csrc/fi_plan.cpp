@@ -320,7 +320,7 @@ bool build_ring(const AxisTable &v, RingTable *rt) {
     }
   }
   // padding rows (fi_fused.hip kPad): zero weights, no flush, last source row
-  const int kPad = 16;  // >= 2 * kDepth of fi_fused.hip
+  const int kPad = 32;  // >= 2 * DEPTH of fi_fused.hip
   for (int q = 0; q < kPad; q++) {
     rt->rows.push_back(rt->rows.back());
     for (int k = 0; k < K; k++) {
