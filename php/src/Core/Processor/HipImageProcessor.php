@@ -1,0 +1,152 @@
+<?php
+
+namespace Core\Processor;
+
+use Core\Entity\Image\OutputImage;
+use Core\Exception\ExecFailedException;
+
+/**
+ * Drop-in for ImageProcessor (src/Core/Processor/ImageProcessor.php) that runs
+ * the resample step -- and smc_1, when set -- on an MI355X through
+ * libflyimg_hip.so over PHP FFI instead of exec'ing `convert`
+ * (ImageProcessor.php:49-57, Processor.php:44-62).
+ *
+ * Geometry and option semantics are the parent's: the same OptionsBag keys,
+ * the same calculateSize() decision (:115-130) and updateTargetDimensions()
+ * clamp (:277-295); they are translated to one fi_image descriptor instead of
+ * a command line.  Decode/encode stay on the host (djpeg -> PPM -> GPU ->
+ * cjpeg, as ImageProcessor.php:204-209 pipes TGA into MozJPEG).
+ * Errors raise ExecFailedException, as Processor::execute does.
+ */
+class HipImageProcessor extends ImageProcessor
+{
+    private const FI_OP_THUMBNAIL = 1 << 0;
+    private const FI_OP_RESIZE = 1 << 1;
+    private const FI_GEOM_FILL = 1 << 2;
+    private const FI_GEOM_SHRINK_ONLY = 1 << 3;
+    private const FI_OP_EXTENT = 1 << 4;
+    private const FI_OP_GRAY = 1 << 5;
+    private const FI_OP_MONOCHROME = 1 << 6;
+    private const FI_OP_ROTATE = 1 << 7;
+    private const FI_OP_SMARTCROP = 1 << 8;
+    private const FI_OP_SMARTCROP_APPLY = 1 << 9;
+    private const GRAVITY = ['NorthWest' => 1, 'North' => 2, 'NorthEast' => 3, 'West' => 4, 'Center' => 5,
+        'East' => 6, 'SouthWest' => 7, 'South' => 8, 'SouthEast' => 9];
+
+    /** @var \FFI|null one library handle and one fi_ctx per PHP-FPM worker */
+    private static $ffi = null;
+    private static $ctx = null;
+
+    private static function lib(): \FFI
+    {
+        if (self::$ffi === null) {
+            $dir = getenv('FLYIMG_HIP_DIR') ?: '/opt/flyimg-hip';
+            self::$ffi = \FFI::cdef(file_get_contents($dir . '/php/flyimg_hip_ffi.h'),
+                $dir . '/flyimg_amd/libflyimg_hip.so');
+            $ctx = self::$ffi->new('fi_ctx*');
+            self::check(self::$ffi->fi_create(\FFI::addr($ctx), (int)(getenv('FLYIMG_HIP_DEVICE') ?: 0)));
+            self::$ctx = $ctx;
+        }
+        return self::$ffi;
+    }
+
+    private static function check(int $rc): void
+    {
+        if ($rc !== 0) {
+            throw new ExecFailedException("Command failed.\nThe exit code: " . $rc .
+                "\nThe last line of output: " . self::$ffi->fi_last_error());
+        }
+    }
+
+    public function processNewImage(OutputImage $outputImage): OutputImage
+    {
+        $this->sourceImageInfo = $outputImage->getInputImage()->sourceImageInfo();
+        $this->options = $outputImage->getInputImage()->optionsBag();
+        $ffi = self::lib();
+        [$w, $h, $rgb] = $this->decodeRgb($this->getSourceImagePath($outputImage));
+
+        $img = $ffi->new('fi_image');
+        $src = $ffi->new("uint8_t[" . strlen($rgb) . "]", false);
+        \FFI::memcpy($src, $rgb, strlen($rgb));
+        $img->src = $src;
+        $img->src_w = $w;
+        $img->src_h = $h;
+        $img->src_stride = 3 * $w;
+        $img->src_channels = 3;
+        $this->describe($img, $outputImage);
+        self::check($ffi->fi_plan(\FFI::addr($img), 1));
+        $cap = $img->out_h * $img->out_stride;
+        $dst = $ffi->new("uint8_t[$cap]", false);
+        $img->dst = $dst;
+        $img->dst_capacity = $cap;
+        self::check($ffi->fi_process_batch(self::$ctx, \FFI::addr($img), 1));
+        self::check($img->status);
+        $this->encode($outputImage, \FFI::string($dst, $img->out_h * $img->out_stride),
+            $img->out_w, $img->out_h, $img->out_channels);
+        \FFI::free($src);
+        \FFI::free($dst);
+        return $outputImage;
+    }
+
+    /** The fi_image equivalent of generateCommand()'s argv (:66-110). */
+    private function describe($img, OutputImage $outputImage): void
+    {
+        $flags = empty($this->options->getOption('resize')) ? self::FI_OP_THUMBNAIL : self::FI_OP_RESIZE;
+        $this->updateTargetDimensions();
+        $tw = (int)$this->options->getOption('width');
+        $th = (int)$this->options->getOption('height');
+        if ($tw && $th && !empty($this->options->getOption('crop'))) {        // generateCropSize :138-148
+            $flags |= self::FI_GEOM_FILL | self::FI_OP_EXTENT;
+        } elseif ($tw || $th) {                                                 // generateSimpleSize :154-162
+            if (!empty($this->options->getOption('preserve-natural-size'))) {
+                $flags |= self::FI_GEOM_SHRINK_ONLY;
+            }
+        }
+        if (strcasecmp((string)$outputImage->extractKey('colorspace'), 'Gray') === 0) {
+            $flags |= self::FI_OP_GRAY;
+        }
+        if (!empty($outputImage->extractKey('monochrome'))) {
+            $flags |= self::FI_OP_MONOCHROME;                                   // FI_EUNSUPPORTED today
+        }
+        $rotate = (int)$this->options->getOption('rotate');
+        if ($rotate % 360 !== 0) {
+            $flags |= self::FI_OP_ROTATE;
+        }
+        if (!empty($outputImage->extractKey('smart-crop'))) {                   // ImageHandler.php:125-133
+            $flags |= self::FI_OP_SMARTCROP | self::FI_OP_SMARTCROP_APPLY;
+        }
+        $img->target_w = $tw;
+        $img->target_h = $th;
+        $img->flags = $flags;
+        $img->gravity = self::GRAVITY[$this->options->getOption('gravity')] ?? 5;
+        $img->rotate = $rotate;
+        $img->smartcrop_w = 100;                                                // smartcrop.py CLI defaults
+        $img->smartcrop_h = 100;
+    }
+
+    /** Host decode to packed RGB8 (libjpeg-turbo's djpeg, PPM output). */
+    private function decodeRgb(string $path): array
+    {
+        $ppm = shell_exec('/opt/mozjpeg/bin/djpeg -pnm ' . escapeshellarg($path));
+        if (!is_string($ppm) || !preg_match('/^P6\s+(\d+)\s+(\d+)\s+255\s/', $ppm, $m)) {
+            throw new ExecFailedException("Command failed.\nThe exit code: decode\nThe last line of output: " . $path);
+        }
+        return [(int)$m[1], (int)$m[2], substr($ppm, strlen($m[0]))];
+    }
+
+    /** Host encode with MozJPEG (ImageProcessor.php:204-209 pipes TGA; PPM is equivalent). */
+    private function encode(OutputImage $outputImage, string $pixels, int $w, int $h, int $c): void
+    {
+        $header = ($c === 1 ? "P5\n" : "P6\n") . "$w $h\n255\n";
+        $cmd = escapeshellarg(self::MOZJPEG_COMMAND) . ' -quality ' .
+            escapeshellarg($outputImage->extractKey('quality')) . ' -outfile ' .
+            escapeshellarg($outputImage->getOutputImagePath());
+        $p = proc_open($cmd, [0 => ['pipe', 'r'], 1 => ['pipe', 'w'], 2 => ['pipe', 'w']], $pipes);
+        fwrite($pipes[0], $header . $pixels);
+        fclose($pipes[0]);
+        $err = stream_get_contents($pipes[2]);
+        if (proc_close($p) !== 0) {
+            throw new ExecFailedException("Command failed.\nThe exit code: encode\nThe last line of output: " . $err);
+        }
+    }
+}

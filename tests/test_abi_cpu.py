@@ -92,3 +92,42 @@ def test_unsupported_ops_fail_loudly():
     op = Op(100, 0, L.FI_OP_THUMBNAIL | L.FI_OP_MONOCHROME)
     with pytest.raises(L.FiError):
         plan(400, 300, op)
+
+
+def _norm_decls(text):
+    """Function prototypes and fi_image fields of a C header, whitespace-normalised."""
+    import re
+
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    protos = {}
+    for m in re.finditer(r"([A-Za-z_][A-Za-z0-9_ \*]*?\b(fi_[a-z0-9_]+)\s*\([^;{]*\))\s*;", text):
+        protos[m.group(2)] = re.sub(r"\s+", " ", m.group(1)).replace("( ", "(").strip()
+    body = re.search(r"typedef struct fi_image \{(.*?)\} fi_image;", text, flags=re.S).group(1)
+    fields = []
+    for decl in body.split(";"):
+        decl = re.sub(r"\s+", " ", decl).strip()
+        if not decl:
+            continue
+        m = re.match(r"(.*?)\s*(\**)([A-Za-z_][A-Za-z0-9_]*)((?:\s*,\s*\**[A-Za-z_][A-Za-z0-9_]*)*)$", decl)
+        base = m.group(1)
+        names = [m.group(2) + m.group(3)] + [n.strip() for n in m.group(4).split(",") if n.strip()]
+        fields += [(base.strip(), n) for n in names]
+    return protos, fields
+
+
+def test_php_ffi_cdef_matches_header():
+    """php/flyimg_hip_ffi.h (FFI::cdef subset, INTEGRATION.md) declares the
+    same prototypes and the same fi_image layout as include/flyimg_hip.h."""
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "include", "flyimg_hip.h")) as f:
+        hp, hf = _norm_decls(f.read())
+    with open(os.path.join(root, "php", "flyimg_hip_ffi.h")) as f:
+        text = f.read()
+    assert not any(l.lstrip().startswith("#") for l in text.splitlines())  # FFI::cdef: no preprocessor
+    pp, pf = _norm_decls(text)
+    assert pp and set(pp) <= set(hp)
+    for name, proto in pp.items():
+        assert proto == hp[name], (proto, hp[name])
+    assert pf == hf
