@@ -147,7 +147,8 @@ def main():
     comm.barrier()
     ctx.set_timing(False)
     el = t1 - t0
-    stats = {k: ctx.stats(k) for k in ("batch", "resize", "sc_prescale", "sc_maps", "sc_score", "crop_apply")}
+    stats = {k: ctx.stats(k) for k in ("batch", "resize", "sc_prep", "sc_score", "crop_apply",
+                                      "host_plan", "host_launch", "host_after_sync", "host_total")}
     allv = comm.allgather_obj({"elapsed": el, "stats": stats,
                                "ncand": sum(arr[i].n_candidates for i in range(nimg)),
                                "bad": sum(1 for i in range(nimg) if arr[i].status != 0)})

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <cstdlib>
 #include <cmath>
@@ -39,9 +40,13 @@ __global__ void k_sc_reduce(const ScDesc *, const int32_t *, int);
 __global__ void k_sc_hpass(const ScDesc *, const int32_t *, int, const int32_t *);
 __global__ void k_sc_vpass(const ScDesc *, const int32_t *, int, const int32_t *);
 __global__ void k_sc_maps(const ScDesc *, const int32_t *, int, const ScParamsDev);
-__global__ void k_sc_score(const ScDesc *, const DevCrop *, const double *, CropScore *, ScResult *,
-                           const ScParamsDev);
-__global__ void k_crop_apply(const ApplyDesc *, const int32_t *, int, const DevCrop *, const ScResult *);
+// per-image smartcrop kernels (fi_smartcrop.hip)
+int launch_sc_h(hipStream_t s, bool mfma, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai);
+int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
+                const ScParamsDev &P);
+int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, int max_px, const DevCrop *crops,
+                    const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P);
+int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
 __global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
 // fused vertical-first resample (fi_fused.hip)
 int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
@@ -113,7 +118,9 @@ struct fi_ctx {
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
   std::map<const AxisTable *, RingTable> ring_cache;
   std::map<const AxisTable *, std::vector<StripTab>> strip_cache;
-  bool fused = true;  // FI_DISABLE_FUSED=1 forces the generic two-pass path
+  bool fused = true;    // FI_DISABLE_FUSED=1 forces the generic two-pass resample
+  bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
+  bool sc_mfma = true;  // FI_DISABLE_SC_MFMA=1: VALU horizontal pass (k_sc_hrows) instead of k_sc_hmfma
 };
 
 static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
@@ -350,19 +357,26 @@ static bool fused_strips(const AxisTable &H, int ew, std::vector<StripTab> *out)
 
 struct ScLaunchData {
   std::vector<ScDesc> descs;
-  std::vector<DevCrop> crops;
-  int ncrop_total = 0;
-  // per image: where its crops live, for result decoding
+  std::vector<DevCrop> crops;  // one list per distinct plan, shared by its images
+  int nscores = 0;             // per-image CropScore slots
   std::vector<const ScPlan *> plans;
 };
 
 // Plan the smartcrop stage of `items` into E (descriptors, crops, tables,
-// workspace).  Returns FI_OK or per-item status in status[].
+// workspace).  Per-item status in status[].  Images sharing a plan (same
+// geometry) share its tables and crop list; `want_pre` keeps the prescaled
+// image in the workspace (fi_smartcrop_ex).
 static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items, ScLaunchData *L,
-                           std::vector<int> *status, std::vector<std::string> *errs) {
+                           std::vector<int> *status, std::vector<std::string> *errs, bool want_pre) {
   const uint64_t ph = params_hash(E.params);
-  std::map<std::pair<const std::vector<double> *, int>, int32_t> imp_placed;
-  std::map<const ScPlan *, std::tuple<int32_t, int32_t, int32_t, int32_t>> tab_placed;
+  // the fast pass's error bound assumes non-negative per-pixel terms
+  const bool fast_ok = E.params.skin_bias >= 0 && E.params.saturation_bias >= 0;
+  struct Placed {
+    int32_t hb = 0, hk = 0, hkT = 0, vb = 0, vk = 0, crop0 = 0, ncrops = 0;
+    int32_t hmB = 0, hmC = 0, hmS0 = 0;
+  };
+  std::map<const ScPlan *, Placed> placed;
+  std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_placed;
   for (size_t k = 0; k < items.size(); k++) {
     const ScItem &it = items[k];
     const fi_smartcrop_options &o = it.opt;
@@ -378,15 +392,103 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     }
     const ScPlan &P = pit->second;
     L->plans.push_back(&P);
+    ScDesc d{};
+    d.result = it.result;
+    if (P.status == FI_OK && (int)P.crops.size() > kScoreMaxCrops) {
+      (*status)[k] = FI_EUNSUPPORTED;
+      (*errs)[k] = "smartcrop: " + std::to_string(P.crops.size()) + " crop windows (max " +
+                   std::to_string(kScoreMaxCrops) + ")";
+      L->descs.push_back(d);
+      continue;
+    }
     if (P.status != FI_OK) {
       (*status)[k] = P.status;
       (*errs)[k] = P.err;
-      L->descs.push_back(ScDesc{});
-      L->descs.back().ncrops = 0;
-      L->descs.back().result = it.result;
+      L->descs.push_back(d);
       continue;
     }
-    ScDesc d{};
+    auto pp = placed.find(&P);
+    if (pp == placed.end()) {
+      Placed q;
+      if (P.thumb) {
+        q.hb = (int32_t)E.ai.size();
+        E.ai.insert(E.ai.end(), P.hb.begin(), P.hb.end());
+        q.hk = (int32_t)E.ai.size();
+        E.ai.insert(E.ai.end(), P.hk.begin(), P.hk.end());
+        q.hkT = (int32_t)E.ai.size();
+        E.ai.insert(E.ai.end(), P.hkT.begin(), P.hkT.end());
+        q.vb = (int32_t)E.ai.size();
+        E.ai.insert(E.ai.end(), P.vb.begin(), P.vb.end());
+        q.vk = (int32_t)E.ai.size();
+        E.ai.insert(E.ai.end(), P.vk.begin(), P.vk.end());
+        if (P.hm_ok) {
+          while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
+          q.hmB = (int32_t)E.ai.size();
+          E.ai.insert(E.ai.end(), P.hmB.begin(), P.hmB.end());
+          q.hmC = (int32_t)E.ai.size();
+          E.ai.insert(E.ai.end(), P.hmC.begin(), P.hmC.end());
+          q.hmS0 = (int32_t)E.ai.size();
+          E.ai.insert(E.ai.end(), P.hmS0.begin(), P.hmS0.end());
+        }
+      }
+      // crops + importance tables (one table per distinct window size)
+      std::map<std::pair<uint64_t, uint64_t>, std::pair<int, int>> sizes;
+      for (const CropHost &ch : P.crops) {
+        auto &e = sizes[{dbits(ch.fw), dbits(ch.fh)}];
+        e.first = std::max(e.first, ch.nin_x);
+        e.second = std::max(e.second, ch.nin_y);
+      }
+      std::map<std::pair<uint64_t, uint64_t>, std::tuple<int32_t, int32_t, double>> tab_of;
+      for (auto &sz : sizes) {
+        double fw, fh;
+        memcpy(&fw, &sz.first.first, 8);
+        memcpy(&fh, &sz.first.second, 8);
+        const int nx = std::max(sz.second.first, 1), ny = std::max(sz.second.second, 1);
+        auto ikey = std::make_tuple(sz.first.first, sz.first.second, nx, ny, ph);
+        auto iit = c->imp_cache.find(ikey);
+        if (iit == c->imp_cache.end()) {
+          if (c->imp_cache.size() > 1024) c->imp_cache.clear();
+          std::vector<double> t;
+          sc_importance_table(E.params, fw, fh, nx, ny, &t);
+          iit = c->imp_cache.emplace(ikey, std::move(t)).first;
+        }
+        auto pk = std::make_pair(&iit->second, nx);
+        auto ip = imp_placed.find(pk);
+        if (ip == imp_placed.end()) {
+          double imax = 0;
+          for (double v : iit->second) imax = std::max(imax, std::fabs(v));
+          const int32_t off = (int32_t)E.ad.size();
+          E.ad.insert(E.ad.end(), iit->second.begin(), iit->second.end());
+          ip = imp_placed.emplace(pk, std::make_pair(off, imax)).first;
+        }
+        tab_of[sz.first] = std::make_tuple(ip->second.first, nx, ip->second.second);
+      }
+      q.crop0 = (int32_t)L->crops.size();
+      q.ncrops = (int32_t)P.crops.size();
+      for (const CropHost &ch : P.crops) {
+        DevCrop dc{};
+        dc.fx = ch.fx;
+        dc.fy = ch.fy;
+        dc.fw = ch.fw;
+        dc.fh = ch.fh;
+        dc.x0 = ch.x0;
+        dc.y0 = ch.y0;
+        dc.nin_x = ch.nin_x;
+        dc.nin_y = ch.nin_y;
+        const auto &t = tab_of[{dbits(ch.fw), dbits(ch.fh)}];
+        dc.table = std::get<0>(t);
+        dc.table_w = std::get<1>(t);
+        dc.imax = std::get<2>(t);
+        dc.rx = ch.rx;
+        dc.ry = ch.ry;
+        dc.rw = ch.rw;
+        dc.rh = ch.rh;
+        L->crops.push_back(dc);
+      }
+      pp = placed.emplace(&P, q).first;
+    }
+    const Placed &q = pp->second;
+    const bool prep = c->sc_prep && P.prep_ok;
     d.img = it.img;
     d.stride = it.stride;
     d.W = it.W;
@@ -404,91 +506,36 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.hrows = P.hrows;
     d.ksh = P.ksh;
     d.ksv = P.ksv;
+    d.hb = q.hb;
+    d.hk = q.hk;
+    d.hkT = q.hkT;
+    d.vb = q.vb;
+    d.vk = q.vk;
+    d.prep = prep ? 1 : 0;
+    d.hm = prep && P.hm_ok && c->sc_mfma ? 1 : 0;
+    d.hm_rows = P.hm_rows;
+    d.hm_ks = P.hm_ks;
+    d.hm_pitch = P.hm_pitch;
+    d.hm_nb = P.hm_nb;
+    d.hmB = q.hmB;
+    d.hmC = q.hmC;
+    d.hmS0 = q.hmS0;
     d.prescale = P.prescale;
-    d.result = it.result;
-    d.exact_all = o.exact_all;
-    if (P.thumb) {
-      auto tp = tab_placed.find(&P);
-      if (tp == tab_placed.end()) {
-        int32_t hb = (int32_t)E.ai.size();
-        E.ai.insert(E.ai.end(), P.hb.begin(), P.hb.end());
-        int32_t hk = (int32_t)E.ai.size();
-        E.ai.insert(E.ai.end(), P.hk.begin(), P.hk.end());
-        int32_t vb = (int32_t)E.ai.size();
-        E.ai.insert(E.ai.end(), P.vb.begin(), P.vb.end());
-        int32_t vk = (int32_t)E.ai.size();
-        E.ai.insert(E.ai.end(), P.vk.begin(), P.vk.end());
-        tp = tab_placed.emplace(&P, std::make_tuple(hb, hk, vb, vk)).first;
-      }
-      d.hb = std::get<0>(tp->second);
-      d.hk = std::get<1>(tp->second);
-      d.vb = std::get<2>(tp->second);
-      d.vk = std::get<3>(tp->second);
-      // workspace (offsets; converted to pointers after allocation)
-      d.red = (P.fx > 1 || P.fy > 1) ? (uint8_t *)(uintptr_t)(E.work.take((size_t)P.rw * P.rh * 3) + 1) : nullptr;
-      d.hbuf = P.need_h ? (uint8_t *)(uintptr_t)(E.work.take((size_t)P.aw * std::max(P.hrows, 1) * 3) + 1) : nullptr;
-      d.pre = (uint8_t *)(uintptr_t)(E.work.take((size_t)P.aw * P.ah * 3) + 1);
-    }
-    d.maps = (uint32_t *)(uintptr_t)(E.work.take((size_t)P.aw * P.ah * 4) + 1);
-    d.crop0 = L->ncrop_total;
-    d.ncrops = (int32_t)P.crops.size();
-    // crops + importance tables (one table per distinct window size)
-    std::map<std::pair<uint64_t, uint64_t>, std::pair<int, int>> sizes;
-    for (const CropHost &ch : P.crops) {
-      auto &e = sizes[{dbits(ch.fw), dbits(ch.fh)}];
-      e.first = std::max(e.first, ch.nin_x);
-      e.second = std::max(e.second, ch.nin_y);
-    }
-    std::map<std::pair<uint64_t, uint64_t>, std::pair<int32_t, int32_t>> tab_of;
-    for (auto &s : sizes) {
-      double fw, fh;
-      memcpy(&fw, &s.first.first, 8);
-      memcpy(&fh, &s.first.second, 8);
-      const int nx = std::max(s.second.first, 1), ny = std::max(s.second.second, 1);
-      auto ikey = std::make_tuple(s.first.first, s.first.second, nx, ny, ph);
-      auto iit = c->imp_cache.find(ikey);
-      if (iit == c->imp_cache.end()) {
-        if (c->imp_cache.size() > 1024) c->imp_cache.clear();
-        std::vector<double> t;
-        sc_importance_table(E.params, fw, fh, nx, ny, &t);
-        iit = c->imp_cache.emplace(ikey, std::move(t)).first;
-      }
-      auto pk = std::make_pair(&iit->second, nx);
-      auto ip = imp_placed.find(pk);
-      int32_t off;
-      if (ip == imp_placed.end()) {
-        off = (int32_t)E.ad.size();
-        E.ad.insert(E.ad.end(), iit->second.begin(), iit->second.end());
-        imp_placed[pk] = off;
-      } else {
-        off = ip->second;
-      }
-      tab_of[s.first] = {off, nx};
-    }
-    for (const CropHost &ch : P.crops) {
-      DevCrop dc{};
-      dc.fx = ch.fx;
-      dc.fy = ch.fy;
-      dc.fw = ch.fw;
-      dc.fh = ch.fh;
-      dc.x0 = ch.x0;
-      dc.y0 = ch.y0;
-      dc.nin_x = ch.nin_x;
-      dc.nin_y = ch.nin_y;
-      auto t = tab_of[{dbits(ch.fw), dbits(ch.fh)}];
-      dc.table = t.first;
-      dc.table_w = t.second;
-      dc.rx = ch.rx;
-      dc.ry = ch.ry;
-      dc.rw = ch.rw;
-      dc.rh = ch.rh;
-      L->crops.push_back(dc);
-    }
-    L->ncrop_total += d.ncrops;
+    d.exact_all = o.exact_all || !fast_ok;
+    // workspace (offsets; converted to pointers after allocation)
+    auto take = [&](size_t n) { return (uint8_t *)(uintptr_t)(E.work.take(n) + 1); };
+    if (P.fx > 1 || P.fy > 1) d.red = take((size_t)P.rw * P.rh * 3);
+    if (P.thumb && P.need_h)  // generic kernels: pitch aw*3; k_sc_hrows: pitch apitch
+      d.hbuf = take((size_t)(prep ? (P.aw * 3 + 15) / 16 * 16 : P.aw * 3) * std::max(P.hrows, 1));
+    if (P.thumb && (!prep || want_pre)) d.pre = take((size_t)P.aw * P.ah * 3);
+    d.maps = (uint32_t *)take((size_t)P.aw * P.ah * 4);
+    d.crop0 = q.crop0;
+    d.ncrops = q.ncrops;
+    d.score0 = L->nscores;
+    L->nscores += q.ncrops;
     L->descs.push_back(d);
   }
 }
-
 template <class D>
 static void fix_ptr(D *&p, uint8_t *base) {
   if (p) p = reinterpret_cast<D *>(base + ((uintptr_t)p - 1));
@@ -519,16 +566,112 @@ static Launch add_launch(Blob &blob, const std::vector<Desc> &all, const std::ve
   return L;
 }
 
-// Enqueue smartcrop kernels for a planned batch.
-struct ScRun {
-  Launch red, hp, vp, maps;
-  size_t desc_all = 0, crops_off = 0;
-  size_t results_off = 0, scores_off = 0;  // workspace
-  int n = 0;
+// Launch lists of a planned smartcrop stage: the per-image kernels where the
+// plan fits them (k_sc_prep, k_sc_score2), the generic per-row kernels
+// otherwise.
+struct ScLaunches {
+  Launch red, hp, vp, maps;        // generic (fi_kernels.hip)
+  size_t prep_off = 0, hv_off = 0, hm_off = 0;  // k_sc_vmaps / k_sc_hrows / k_sc_hmfma
+  int nprep = 0, nhv = 0, nhm = 0, h_chunks = 0, h_lds = 0, hm_chunks = 0, hm_lds = 0, v_chunks = 0, v_lds = 0;
+  size_t sl_off = 0, sg_off = 0;   // k_sc_score2 with maps in LDS / global
+  int nsl = 0, nsg = 0, sl_px = 0;
+  size_t crops_off = 0;
 };
+static void add_sc_launches(Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus, ScLaunches *X) {
+  std::vector<int> sred, shp, svp, smaps;
+  std::vector<ScDesc> prep, hv, hm, sl, sg;
+  for (size_t k = 0; k < SL.descs.size(); k++) {
+    if (sstatus[k] != FI_OK) continue;
+    const ScDesc &d = SL.descs[k];
+    const ScPlan &P = *SL.plans[k];
+    if (d.red) sred.push_back((int)k);
+    if (d.prep) {
+      prep.push_back(d);
+      if (d.hm) {
+        hm.push_back(d);
+        X->hm_chunks = std::max(X->hm_chunks, P.hm_chunks);
+        X->hm_lds = std::max(X->hm_lds, P.hm_lds);
+      } else if (d.need_h) {
+        hv.push_back(d);
+        X->h_chunks = std::max(X->h_chunks, P.h_chunks);
+        X->h_lds = std::max(X->h_lds, P.h_lds);
+      }
+      X->v_chunks = std::max(X->v_chunks, P.v_chunks);
+      X->v_lds = std::max(X->v_lds, P.v_lds);
+    } else {
+      if (d.hbuf) shp.push_back((int)k);
+      if (d.pre) svp.push_back((int)k);
+      smaps.push_back((int)k);
+    }
+    if ((int64_t)d.aw * d.ah * 4 <= kScoreLdsMaps) {
+      sl.push_back(d);
+      X->sl_px = std::max(X->sl_px, d.aw * d.ah);
+    } else {
+      sg.push_back(d);
+    }
+  }
+  X->red = add_launch(B, SL.descs, sred, [](const ScDesc &d) { return d.rh; });
+  X->hp = add_launch(B, SL.descs, shp, [](const ScDesc &d) { return d.hrows; });
+  X->vp = add_launch(B, SL.descs, svp, [](const ScDesc &d) { return d.ah; });
+  X->maps = add_launch(B, SL.descs, smaps, [](const ScDesc &d) { return d.ah; });
+  X->prep_off = B.addv(prep);
+  X->nprep = (int)prep.size();
+  X->hv_off = B.addv(hv);
+  X->nhv = (int)hv.size();
+  X->hm_off = B.addv(hm);
+  X->nhm = (int)hm.size();
+  X->sl_off = B.addv(sl);
+  X->nsl = (int)sl.size();
+  X->sg_off = B.addv(sg);
+  X->nsg = (int)sg.size();
+  X->crops_off = B.addv(SL.crops);
+}
+static int enqueue_sc(fi_ctx *c, uint8_t *ab, const ScLaunches &X, const int32_t *ai, const double *ad,
+                      CropScore *scores, ScResult *results, const ScParamsDev &PD) {
+  auto desc = [&](const Launch &L) { return (const ScDesc *)(ab + L.desc_off); };
+  auto pre = [&](const Launch &L) { return (const int32_t *)(ab + L.prefix_off); };
+  {
+    Timer t(c, "sc_prep", 0);
+    if (X.red.tiles)
+      hipLaunchKernelGGL(k_sc_reduce, dim3(X.red.tiles), dim3(256), 0, c->stream, desc(X.red), pre(X.red), X.red.n);
+    if (launch_sc_h(c->stream, true, (const ScDesc *)(ab + X.hm_off), X.nhm, X.hm_chunks, X.hm_lds, ai) != 0 ||
+        launch_sc_h(c->stream, false, (const ScDesc *)(ab + X.hv_off), X.nhv, X.h_chunks, X.h_lds, ai) != 0 ||
+        launch_sc_v(c->stream, (const ScDesc *)(ab + X.prep_off), X.nprep, X.v_chunks, X.v_lds, ai, PD) != 0)
+      return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d)", X.hm_lds, X.h_lds, X.v_lds);
+    if (X.hp.tiles)
+      hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, c->stream, desc(X.hp), pre(X.hp), X.hp.n, ai);
+    if (X.vp.tiles)
+      hipLaunchKernelGGL(k_sc_vpass, dim3(X.vp.tiles), dim3(256), 0, c->stream, desc(X.vp), pre(X.vp), X.vp.n, ai);
+    if (X.maps.tiles)
+      hipLaunchKernelGGL(k_sc_maps, dim3(X.maps.tiles), dim3(256), 0, c->stream, desc(X.maps), pre(X.maps),
+                         X.maps.n, PD);
+  }
+  {
+    Timer t(c, "sc_score", 0);
+    const DevCrop *crops = (const DevCrop *)(ab + X.crops_off);
+    if (launch_sc_score(c->stream, true, (const ScDesc *)(ab + X.sl_off), X.nsl, X.sl_px, crops, ad, scores,
+                        results, PD) != 0)
+      return set_err(FI_EDEVICE, "k_sc_score2 launch rejected (%d px)", X.sl_px);
+    (void)launch_sc_score(c->stream, false, (const ScDesc *)(ab + X.sg_off), X.nsg, 0, crops, ad, scores, results,
+                          PD);
+  }
+  HIP_TRY(hipGetLastError());
+  return FI_OK;
+}
+
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static void host_stat(fi_ctx *c, const char *name, double ms) {
+  if (!c->timing) return;
+  Stat &s = c->stats[name];
+  s.ms += ms;
+  s.launches += 1;
+}
 
 static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) {
   (void)device_ptrs_ok;
+  const double t_start = now_ms();
   Exec E;
   E.c = c;
   fi_smartcrop_default_params(&E.params);
@@ -704,9 +847,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       const ResizeDesc &d = rd[rd_of[i]];
       it.img = d.dst;  // may still be a workspace offset (+1 tagged); fixed below
     }
-  plan_smartcrop(c, E, sitems, &SL, &sstatus, &serrs);
+  plan_smartcrop(c, E, sitems, &SL, &sstatus, &serrs, false);
   const size_t results_off = E.work.take(sizeof(ScResult) * std::max<size_t>(sitems.size(), 1));
-  const size_t scores_off = E.work.take(sizeof(CropScore) * std::max(SL.ncrop_total, 1));
+  const size_t scores_off = E.work.take(sizeof(CropScore) * std::max(SL.nscores, 1));
   const size_t outwh_off = E.work.take(sizeof(int32_t) * 2 * std::max(n, 1));
   int rc = ensure(c, &c->work, E.work.size + 256);
   if (rc) return rc;
@@ -791,23 +934,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
   Launch L1a = add_launch(B, rd, m1, eh_tiles);
   Launch L2a = add_launch(B, rd, m2, mid_tiles);
   Launch L2b = add_launch(B, rd, m2, eh_tiles);
-  std::vector<int> sall, sred, shp, svp;
-  for (size_t k = 0; k < SL.descs.size(); k++) {
-    if (sstatus[k] != FI_OK) continue;
-    const ScDesc &d = SL.descs[k];
-    sall.push_back((int)k);
-    if (d.red) sred.push_back((int)k);
-    if (d.hbuf) shp.push_back((int)k);
-    if (d.pre) svp.push_back((int)k);
-  }
-  Launch Sred = add_launch(B, SL.descs, sred, [](const ScDesc &d) { return d.rh; });
-  Launch Shp = add_launch(B, SL.descs, shp, [](const ScDesc &d) { return d.hrows; });
-  Launch Svp = add_launch(B, SL.descs, svp, [](const ScDesc &d) { return d.ah; });
-  Launch Smaps = add_launch(B, SL.descs, sall, [](const ScDesc &d) { return d.ah; });
-  std::vector<ScDesc> score_descs;
-  for (int k : sall) score_descs.push_back(SL.descs[k]);
-  const size_t score_desc_off = B.addv(score_descs);
-  const size_t crops_off = B.addv(SL.crops);
+  ScLaunches SX;
+  add_sc_launches(B, SL, sstatus, &SX);
+  const bool any_sc = SX.nsl + SX.nsg > 0;
   std::vector<ApplyDesc> apply;
   std::vector<int> apply_img;
   for (int i = 0; i < n; i++) {
@@ -828,9 +957,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
     apply.push_back(a);
     apply_img.push_back(i);
   }
-  std::vector<int> all_apply(apply.size());
-  for (size_t k = 0; k < apply.size(); k++) all_apply[k] = (int)k;
-  Launch Lap = add_launch(B, apply, all_apply, [](const ApplyDesc &a) { return a.H; });
+  const size_t apply_off = B.addv(apply);
   const size_t ai_off = B.addv(E.ai), af_off = B.addv(E.af), ad_off = B.addv(E.ad);
   // ---- upload
   rc = ensure(c, &c->arena, B.b.size() + 256);
@@ -839,6 +966,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
   if (rc) return rc;
   memcpy(c->pinned, B.b.data(), B.b.size());
   HIP_TRY(hipMemcpyAsync(c->arena.p, c->pinned, B.b.size(), hipMemcpyHostToDevice, c->stream));
+  const double t_planned = now_ms();
+  host_stat(c, "host_plan", t_planned - t_start);
+  if (c->timing) c->stats["host_plan"].bytes += (double)B.b.size();
   uint8_t *ab = (uint8_t *)c->arena.p;
   const int32_t *ai = (const int32_t *)(ab + ai_off);
   const float *af = (const float *)(ab + af_off);
@@ -876,34 +1006,13 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       }
     }
     HIP_TRY(hipGetLastError());
-    if (!score_descs.empty()) {
-      {
-        Timer t(c, "sc_prescale", 0);
-        if (Sred.tiles)
-          hipLaunchKernelGGL(k_sc_reduce, dim3(Sred.tiles), dim3(256), 0, c->stream, (const ScDesc *)desc_p(Sred),
-                             pre_p(Sred), Sred.n);
-        if (Shp.tiles)
-          hipLaunchKernelGGL(k_sc_hpass, dim3(Shp.tiles), dim3(256), 0, c->stream, (const ScDesc *)desc_p(Shp),
-                             pre_p(Shp), Shp.n, ai);
-        if (Svp.tiles)
-          hipLaunchKernelGGL(k_sc_vpass, dim3(Svp.tiles), dim3(256), 0, c->stream, (const ScDesc *)desc_p(Svp),
-                             pre_p(Svp), Svp.n, ai);
-      }
-      {
-        Timer t(c, "sc_maps", 0);
-        hipLaunchKernelGGL(k_sc_maps, dim3(Smaps.tiles), dim3(256), 0, c->stream, (const ScDesc *)desc_p(Smaps),
-                           pre_p(Smaps), Smaps.n, PD);
-      }
-      {
-        Timer t(c, "sc_score", 0);
-        hipLaunchKernelGGL(k_sc_score, dim3((unsigned)score_descs.size()), dim3(256), 0, c->stream,
-                           (const ScDesc *)(ab + score_desc_off), (const DevCrop *)(ab + crops_off), ad,
-                           (CropScore *)(wb + scores_off), (ScResult *)(wb + results_off), PD);
-      }
-      if (Lap.tiles) {
+    if (any_sc) {
+      rc = enqueue_sc(c, ab, SX, ai, ad, (CropScore *)(wb + scores_off), (ScResult *)(wb + results_off), PD);
+      if (rc) return rc;
+      if (!apply.empty()) {
         Timer t(c, "crop_apply", 0);
-        hipLaunchKernelGGL(k_crop_apply, dim3(Lap.tiles), dim3(256), 0, c->stream, (const ApplyDesc *)desc_p(Lap),
-                           pre_p(Lap), Lap.n, (const DevCrop *)(ab + crops_off), (const ScResult *)(wb + results_off));
+        (void)launch_crop_apply(c->stream, (const ApplyDesc *)(ab + apply_off), (int)apply.size(),
+                                (const DevCrop *)(ab + SX.crops_off), (const ScResult *)(wb + results_off));
       }
       HIP_TRY(hipGetLastError());
     }
@@ -916,8 +1025,11 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
                            c->stream));
   if (!apply.empty())
     HIP_TRY(hipMemcpyAsync(outwh.data(), wb + outwh_off, sizeof(int32_t) * 2 * n, hipMemcpyDeviceToHost, c->stream));
+  const double t_launched = now_ms();
+  host_stat(c, "host_launch", t_launched - t_planned);
   HIP_TRY(hipStreamSynchronize(c->stream));
   collect_timers(c);
+  const double t_done = now_ms();
   int first_bad = FI_OK;
   std::string first_err;
   for (int i = 0; i < n; i++) {
@@ -955,6 +1067,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       first_err = "image " + std::to_string(i) + ": " + errs[i];
     }
   }
+  host_stat(c, "host_total", now_ms() - t_start);
+  host_stat(c, "host_after_sync", now_ms() - t_done);
   if (first_bad != FI_OK) return set_err(first_bad, "%s", first_err.c_str());
   return FI_OK;
 }
@@ -982,12 +1096,11 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   ScLaunchData SL;
   std::vector<int> st(1, FI_OK);
   std::vector<std::string> errs(1);
-  plan_smartcrop(c, E, items, &SL, &st, &errs);
+  plan_smartcrop(c, E, items, &SL, &st, &errs, prescaled != nullptr);
   if (st[0] != FI_OK) return set_err(st[0], "%s", errs[0].c_str());
-  if (SL.descs[0].ncrops > 2048) return set_err(FI_EUNSUPPORTED, "smartcrop: %d crop windows (max 2048)", SL.descs[0].ncrops);
   *plan_out = *SL.plans[0];
   const size_t results_off = E.work.take(sizeof(ScResult));
-  const size_t scores_off = E.work.take(sizeof(CropScore) * std::max(SL.ncrop_total, 1));
+  const size_t scores_off = E.work.take(sizeof(CropScore) * std::max(SL.nscores, 1));
   int rc = ensure(c, &c->work, E.work.size + 256);
   if (rc) return rc;
   uint8_t *wb = (uint8_t *)c->work.p;
@@ -997,13 +1110,8 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   fix_ptr(d.pre, wb);
   fix_ptr(d.maps, wb);
   Blob &B = E.blob;
-  std::vector<int> all{0};
-  Launch Sred = add_launch(B, SL.descs, d.red ? all : std::vector<int>{}, [](const ScDesc &x) { return x.rh; });
-  Launch Shp = add_launch(B, SL.descs, d.hbuf ? all : std::vector<int>{}, [](const ScDesc &x) { return x.hrows; });
-  Launch Svp = add_launch(B, SL.descs, d.pre ? all : std::vector<int>{}, [](const ScDesc &x) { return x.ah; });
-  Launch Smaps = add_launch(B, SL.descs, all, [](const ScDesc &x) { return x.ah; });
-  const size_t score_desc_off = B.addv(SL.descs);
-  const size_t crops_off = B.addv(SL.crops);
+  ScLaunches SX;
+  add_sc_launches(B, SL, st, &SX);
   const size_t ai_off = B.addv(E.ai), ad_off = B.addv(E.ad);
   rc = ensure(c, &c->arena, B.b.size() + 256);
   if (rc) return rc;
@@ -1012,35 +1120,11 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   memcpy(c->pinned, B.b.data(), B.b.size());
   HIP_TRY(hipMemcpyAsync(c->arena.p, c->pinned, B.b.size(), hipMemcpyHostToDevice, c->stream));
   uint8_t *ab = (uint8_t *)c->arena.p;
-  const int32_t *ai = (const int32_t *)(ab + ai_off);
-  const double *ad = (const double *)(ab + ad_off);
-  const ScParamsDev PD = to_dev(params);
-  {
-    Timer t(c, "sc_prescale", 0);
-    if (Sred.tiles)
-      hipLaunchKernelGGL(k_sc_reduce, dim3(Sred.tiles), dim3(256), 0, c->stream, (const ScDesc *)(ab + Sred.desc_off),
-                         (const int32_t *)(ab + Sred.prefix_off), Sred.n);
-    if (Shp.tiles)
-      hipLaunchKernelGGL(k_sc_hpass, dim3(Shp.tiles), dim3(256), 0, c->stream, (const ScDesc *)(ab + Shp.desc_off),
-                         (const int32_t *)(ab + Shp.prefix_off), Shp.n, ai);
-    if (Svp.tiles)
-      hipLaunchKernelGGL(k_sc_vpass, dim3(Svp.tiles), dim3(256), 0, c->stream, (const ScDesc *)(ab + Svp.desc_off),
-                         (const int32_t *)(ab + Svp.prefix_off), Svp.n, ai);
-  }
-  {
-    Timer t(c, "sc_maps", 0);
-    hipLaunchKernelGGL(k_sc_maps, dim3(Smaps.tiles), dim3(256), 0, c->stream, (const ScDesc *)(ab + Smaps.desc_off),
-                       (const int32_t *)(ab + Smaps.prefix_off), Smaps.n, PD);
-  }
-  {
-    Timer t(c, "sc_score", 0);
-    hipLaunchKernelGGL(k_sc_score, dim3(1), dim3(256), 0, c->stream, (const ScDesc *)(ab + score_desc_off),
-                       (const DevCrop *)(ab + crops_off), ad, (CropScore *)(wb + scores_off),
-                       (ScResult *)(wb + results_off), PD);
-  }
-  HIP_TRY(hipGetLastError());
-  scores->resize(SL.ncrop_total);
-  HIP_TRY(hipMemcpyAsync(scores->data(), wb + scores_off, sizeof(CropScore) * SL.ncrop_total, hipMemcpyDeviceToHost,
+  rc = enqueue_sc(c, ab, SX, (const int32_t *)(ab + ai_off), (const double *)(ab + ad_off),
+                  (CropScore *)(wb + scores_off), (ScResult *)(wb + results_off), to_dev(params));
+  if (rc) return rc;
+  scores->resize(SL.nscores);
+  HIP_TRY(hipMemcpyAsync(scores->data(), wb + scores_off, sizeof(CropScore) * SL.nscores, hipMemcpyDeviceToHost,
                          c->stream));
   HIP_TRY(hipMemcpyAsync(result, wb + results_off, sizeof(ScResult), hipMemcpyDeviceToHost, c->stream));
   const size_t na = (size_t)d.aw * d.ah;
@@ -1105,6 +1189,8 @@ int fi_create(fi_ctx **out, int32_t device) {
   fi_ctx *c = new fi_ctx();
   c->device = device;
   if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
+  if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');
+  if (const char *e = getenv("FI_DISABLE_SC_MFMA")) c->sc_mfma = !(e[0] == '1');
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return set_err(FI_EDEVICE, "hipStreamCreate failed");

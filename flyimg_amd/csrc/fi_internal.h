@@ -10,6 +10,7 @@
 //     path, resized images feeding smartcrop, prescale scratch, packed maps,
 //     per-crop score slots.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/flyimg_hip.h"
@@ -81,6 +82,7 @@ struct DevCrop {
   int32_t table;          // arena offset (double units) of importance table
   int32_t table_w;        // row pitch of the table
   int32_t rx, ry, rw, rh; // rescaled ints (crop() :184-190)
+  double imax;            // max |importance| over the table (fast-pass error bound)
 };
 
 struct ScDesc {
@@ -94,16 +96,50 @@ struct ScDesc {
   int32_t ybox_first, hrows;
   int32_t hb, hk, ksh; // arena offsets: H bounds (pairs), H coeffs (int32), ksize
   int32_t vb, vk, ksv;
+  int32_t hkT;         // H coeffs transposed [ksh][aw] (k_sc_prep: lanes read consecutive x)
+  int32_t prep;        // 1: k_sc_hrows/k_sc_vmaps path (hbuf pitch apitch), 0: generic kernels
+  int32_t hm;          // 1: horizontal pass by k_sc_hmfma (tables below), 0: k_sc_hrows
+  int32_t hm_rows, hm_ks, hm_pitch, hm_nb;
+  int32_t hmB, hmC, hmS0;  // arena offsets (int32 units; hmB 16-B aligned)
   uint8_t *red;        // reduce scratch rw*rh*3
   uint8_t *hbuf;       // H-pass scratch aw*hrows*3
   uint8_t *pre;        // prescaled image aw*ah*3
   uint32_t *maps;      // packed skin | edge<<8 | sat<<16
-  int32_t crop0, ncrops;  // into the batch crop array
+  int32_t crop0, ncrops;  // into the batch crop array (shared by images of one plan)
+  int32_t score0;         // into the batch CropScore array (per image)
   double prescale;
   double T[3];         // unused on host; device scratch
   int32_t result;      // index into result array
   int32_t exact_all;
 };
+
+// k_sc_hrows / k_sc_vmaps (fi_smartcrop.hip): kPrepRows rows per workgroup;
+// apitch = 16-B rounded aw*3 (hbuf and LDS row pitch), spitch = 16-B rounded
+// source width*3.  LDS per workgroup <= kPrepMaxLds (host-checked).
+constexpr int kPrepRows = 16;
+constexpr int kPrepMaxLds = 64 * 1024;
+// k_sc_score2: maps resident in LDS when aw*ah*4 <= this; crops per image.
+constexpr int kScoreLdsMaps = 112 * 1024;
+constexpr int kScoreMaxCrops = 1024;
+
+// v_mfma_i32_16x16x64_i8 operand map (pinned by tools/mfma_probe.hip): lane l
+// holds A[l & 15][k] and B[k][l & 15] for its 16 fragment bytes j, with
+// k = mfma_i8_k(l, j); D[4 (l >> 4) + i][l & 15], i = 0..3.
+#ifndef FI_MFMA_I8_MAP
+#define FI_MFMA_I8_MAP 1
+#endif
+__host__ __device__ inline int mfma_i8_k(int l, int j) {
+#if FI_MFMA_I8_MAP == 1
+  return 16 * (l >> 4) + j;
+#else
+  return j < 8 ? 8 * (l >> 4) + j : 32 + 8 * (l >> 4) + (j - 8);
+#endif
+}
+// k_sc_hmfma (fi_smartcrop.hip): Pillow's horizontal pass as exact integer
+// MFMA.  Per 16-column output block b: source window [s0(b), s0(b) + 64 KS),
+// coefficient limbs L0 + 256 L1 + 65536 L2 (signed i8) in fragment order;
+// s0(b) is 8-B aligned (two 8-byte fragment reads), ks <= 2.
+constexpr int kHmMaxLds = 64 * 1024;
 
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "fi_internal.h"
+#include "fi_sc_device.h"
 
 namespace fi {
 
@@ -258,10 +259,6 @@ __global__ __launch_bounds__(256) void k_sc_reduce(const ScDesc *__restrict__ de
   }
 }
 
-__device__ __forceinline__ uint8_t pil_clip8(int32_t v) {
-  v >>= 22;
-  return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
-}
 
 // Horizontal pass over rows [ybox_first, ybox_first + hrows) of the (reduced) image.
 __global__ __launch_bounds__(256) void k_sc_hpass(const ScDesc *__restrict__ descs,
@@ -352,14 +349,6 @@ __global__ __launch_bounds__(256) void k_sc_vpass(const ScDesc *__restrict__ des
 // ---------------------------------------------------------------------------
 // smartcrop maps (analyse(), smartcrop.py:94-101)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t sc_luma(uint32_t r, uint32_t g, uint32_t b) {
-  // Pillow ImagingConvertMatrix: float sum in order, +0.5 in double, CLIPF
-  float v = 0.2126f * (float)r + 0.7152f * (float)g;
-  v = v + 0.0722f * (float)b;
-  v = v + 0.0f;
-  v = (float)((double)v + 0.5);
-  return v <= 0.0f ? 0u : v >= 255.0f ? 255u : (uint32_t)v;
-}
 
 __device__ __forceinline__ uint32_t pre_luma(const ScDesc &D, const uint8_t *pre, int64_t stride, int C,
                                              int x, int y) {
@@ -393,265 +382,8 @@ __global__ __launch_bounds__(256) void k_sc_maps(const ScDesc *__restrict__ desc
                     (int)pre_luma(D, img, stride, C, x + 1, y) + 1;
       E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
     }
-    const double rd_ = (double)r, gd_ = (double)g, bd_ = (double)b;
-    // detect_skin (smartcrop.py:250-274)
-    uint32_t S = 0;
-    {
-      double rd = -P.skin_color[0], gd = -P.skin_color[1], bd = -P.skin_color[2];
-      const double mag = sqrt(rd_ * rd_ + gd_ * gd_ + bd_ * bd_);
-      if (!(fabs(mag) < 1e-6)) {
-        rd = rd_ / mag - P.skin_color[0];
-        gd = gd_ / mag - P.skin_color[1];
-        bd = bd_ / mag - P.skin_color[2];
-      }
-      const double skin = 1 - sqrt(rd * rd + gd * gd + bd * bd);
-      if ((skin > P.skin_threshold) && ((double)L >= P.skin_brightness_min * 255) &&
-          ((double)L <= P.skin_brightness_max * 255))
-        S = (uint32_t)(uint8_t)(int)((skin - P.skin_threshold) * (255 / (1 - P.skin_threshold)));
-    }
-    // saturation() + detect_saturation (smartcrop.py:16-27, 234-248)
-    uint32_t T = 0;
-    {
-      const double mx = fmax(fmax(rd_, gd_), bd_), mn = fmin(fmin(rd_, gd_), bd_);
-      double s = (mx + mn) / 255, d = (mx - mn) / 255;
-      if (mx == mn) {
-        d = 0;
-        s = 1;
-      }
-      if (s > 1) s = 2 - d;
-      const double sat = d / s;
-      const double thr = P.saturation_threshold;
-      if ((sat > thr) && ((double)L >= P.saturation_brightness_min * 255) &&
-          ((double)L <= P.saturation_brightness_max * 255))
-        T = (uint32_t)(uint8_t)(int)((sat - thr) * (255 / (1 - thr)));
-    }
-    D.maps[(int64_t)y * W + x] = S | (E << 8) | (T << 16);
+    D.maps[(int64_t)y * W + x] = sc_skin_sat(r, g, b, L, P) | (E << 8);
   }
-}
-
-// ---------------------------------------------------------------------------
-// smartcrop scoring (score() smartcrop.py:300-338 for every crop + argmax
-// analyse() :116-133).
-//
-// Fast pass: per crop, inside-window sums of importance x term by one wave
-// (importance from a per-geometry f64 table); the outside part from the
-// image totals (summed-area identity: outside = total - inside) times
-// outside_importance.  Each fast total carries a rigorous bound on its
-// distance to the reference's left-to-right f64 sum.  Crops whose bound
-// interval reaches the best lower bound are re-scored exactly: one lane per
-// crop, every pixel in the reference's row-major order, same IEEE operations.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-constexpr int kMaxCrops = 2048;  // per image; LDS holds totals + bounds
-
-__global__ __launch_bounds__(256) void k_sc_score(const ScDesc *__restrict__ descs,
-                                                  const DevCrop *__restrict__ crops,
-                                                  const double *__restrict__ ad, CropScore *scores,
-                                                  ScResult *results, const ScParamsDev P) {
-  const ScDesc &D = descs[blockIdx.x];
-  __shared__ double lut[256];
-  __shared__ double part[4][3];
-  __shared__ double T[3];
-  __shared__ double s_tot[kMaxCrops];
-  __shared__ double s_bnd[kMaxCrops];
-  __shared__ int32_t cand[kMaxCrops];
-  __shared__ int32_t ncand_s;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (D.ncrops > kMaxCrops) {
-    if (tid == 0) {
-      results[D.result].top = -1;
-      results[D.result].n_candidates = D.ncrops;
-      results[D.result].total = 0;
-    }
-    return;
-  }
-  lut[tid] = (double)tid / 255.0;  // Python int / 255 (correctly rounded)
-  __syncthreads();
-  const int W = D.aw, H = D.ah, npx = W * H;
-  const uint32_t *maps = D.maps;
-  const double sb = P.skin_bias, tb = P.saturation_bias, oi = P.outside_importance;
-
-  // image totals of the three per-pixel terms (outside part of every crop)
-  {
-    double t0 = 0, t1 = 0, t2 = 0;
-    for (int p = tid; p < npx; p += 256) {
-      const uint32_t m = maps[p];
-      const double d = lut[(m >> 8) & 255];
-      t0 += d;
-      t1 += lut[m & 255] * (d + sb);
-      t2 += lut[(m >> 16) & 255] * (d + tb);
-    }
-    t0 = wave_sum(t0);
-    t1 = wave_sum(t1);
-    t2 = wave_sum(t2);
-    if (lane == 0) {
-      part[wave][0] = t0;
-      part[wave][1] = t1;
-      part[wave][2] = t2;
-    }
-    __syncthreads();
-    if (tid < 3) T[tid] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
-    __syncthreads();
-  }
-  const double u = 1.1102230246251565e-16;  // 2^-53
-  const double nn = (double)npx + 1.0;
-  const double gam = nn * u / (1.0 - nn * u);
-  const double aoi = fabs(oi);
-  const double wd = P.detail_weight, ws = P.skin_weight, wt = P.saturation_weight;
-
-  for (int c = wave; c < D.ncrops; c += 4) {
-    const DevCrop cr = crops[D.crop0 + c];
-    const double *tab = ad + cr.table;
-    double sd = 0, ss = 0, st = 0, ad_ = 0, as_ = 0, at_ = 0, id = 0, is = 0, it = 0;
-    for (int dy = 0; dy < cr.nin_y; dy++) {
-      const uint32_t *mrow = maps + (int64_t)(cr.y0 + dy) * W + cr.x0;
-      const double *trow = tab + (int64_t)dy * cr.table_w;
-      for (int dx = lane; dx < cr.nin_x; dx += 64) {
-        const uint32_t m = mrow[dx];
-        const double imp = trow[dx];
-        const double d = lut[(m >> 8) & 255];
-        const double a1 = lut[m & 255] * (d + sb);
-        const double a2 = lut[(m >> 16) & 255] * (d + tb);
-        const double ai_ = fabs(imp);
-        sd = fma(imp, d, sd);
-        ss = fma(imp, a1, ss);
-        st = fma(imp, a2, st);
-        ad_ = fma(ai_, d, ad_);
-        as_ = fma(ai_, a1, as_);
-        at_ = fma(ai_, a2, at_);
-        id += d;
-        is += a1;
-        it += a2;
-      }
-    }
-    sd = wave_sum(sd);
-    ss = wave_sum(ss);
-    st = wave_sum(st);
-    ad_ = wave_sum(ad_);
-    as_ = wave_sum(as_);
-    at_ = wave_sum(at_);
-    id = wave_sum(id);
-    is = wave_sum(is);
-    it = wave_sum(it);
-    if (lane == 0) {
-      const double Fd = sd + oi * (T[0] - id), Fs = ss + oi * (T[1] - is), Ft = st + oi * (T[2] - it);
-      // |python_sum - F| <= 5 gamma(n+1) (sum |imp| a)   ("bound-and-verify")
-      const double Ed = 5.0 * gam * (ad_ + aoi * T[0]) * 1.0000001;
-      const double Es = 5.0 * gam * (as_ + aoi * T[1]) * 1.0000001;
-      const double Et = 5.0 * gam * (at_ + aoi * T[2]) * 1.0000001;
-      const double area = cr.fw * cr.fh;
-      const double tot = (Fd * wd + Fs * ws + Ft * wt) / area;
-      const double mag = fabs(wd) * (fabs(Fd) + Ed) + fabs(ws) * (fabs(Fs) + Es) + fabs(wt) * (fabs(Ft) + Et);
-      const double B = ((fabs(wd) * Ed + fabs(ws) * Es + fabs(wt) * Et) * (1.0 + 16.0 * u) + 16.0 * u * mag) /
-                       area * 1.01;
-      s_tot[c] = tot;
-      s_bnd[c] = B;
-      CropScore &o = scores[D.crop0 + c];
-      o.detail = Fd;
-      o.saturation = Ft;
-      o.skin = Fs;
-      o.total = tot;
-      o.bound = B;
-      o.exact = 0;
-    }
-  }
-  __syncthreads();
-  // candidate set: every crop whose interval reaches the best lower bound
-  if (tid == 0) {
-    double best_lo = -1.0e308;
-    for (int c = 0; c < D.ncrops; c++) best_lo = fmax(best_lo, s_tot[c] - s_bnd[c]);
-    int k = 0;
-    for (int c = 0; c < D.ncrops; c++)
-      if (D.exact_all || s_tot[c] + s_bnd[c] >= best_lo) cand[k++] = c;
-    ncand_s = k;
-  }
-  __syncthreads();
-  const int ncand = ncand_s;
-  const bool need_exact = D.exact_all || ncand > 1;
-  if (need_exact) {
-    // exact re-score: one lane per candidate, the reference's row-major order
-    for (int k = tid; k < ncand; k += 256) {
-      const int c = cand[k];
-      const DevCrop cr = crops[D.crop0 + c];
-      const double *tab = ad + cr.table;
-      double skin = 0, detail = 0, sat = 0;
-      for (int y = 0; y < H; y++) {
-        const bool yin = y >= cr.y0 && y < cr.y0 + cr.nin_y;
-        const uint32_t *mrow = maps + (int64_t)y * W;
-        const int64_t trow = (int64_t)(y - cr.y0) * cr.table_w - cr.x0;
-        for (int x = 0; x < W; x++) {
-          const bool in = yin && x >= cr.x0 && x < cr.x0 + cr.nin_x;
-          const double tv = tab[in ? trow + x : 0];
-          const double imp = in ? tv : oi;
-          const uint32_t m = mrow[x];
-          const double det = lut[(m >> 8) & 255];
-          skin = skin + lut[m & 255] * (det + sb) * imp;
-          detail = detail + det * imp;
-          sat = sat + lut[(m >> 16) & 255] * (det + tb) * imp;
-        }
-      }
-      const double tot = (detail * wd + skin * ws + sat * wt) / (cr.fw * cr.fh);
-      s_tot[c] = tot;
-      CropScore &o = scores[D.crop0 + c];
-      o.detail = detail;
-      o.saturation = sat;
-      o.skin = skin;
-      o.total = tot;
-      o.bound = 0;
-      o.exact = 1;
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    int top = cand[0];
-    double best = s_tot[top];
-    if (need_exact) {
-      best = -9223372036854775807.0;  // -sys.maxsize; strict > keeps the first max
-      for (int k = 0; k < ncand; k++) {
-        const double v = s_tot[cand[k]];
-        if (v > best) {
-          best = v;
-          top = cand[k];
-        }
-      }
-    }
-    results[D.result].top = top;
-    results[D.result].n_candidates = ncand;
-    results[D.result].total = best;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// convert <out> -crop WxH+X+Y (SmartCropProcessor.php:30-34), W = w + x,
-// H = h + y as smartcrop.py prints them (:372-377); CropImage clips to the
-// image.  src is the resized image; per-image box from ScResult + crops.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_crop_apply(const ApplyDesc *__restrict__ descs,
-                                                    const int32_t *__restrict__ prefix, int nimg,
-                                                    const DevCrop *__restrict__ crops,
-                                                    const ScResult *__restrict__ results) {
-  const int t = blockIdx.x;
-  const int i = find_image(prefix, nimg, t);
-  const ApplyDesc &A = descs[i];
-  const int y = t - prefix[i];
-  const ScResult r = results[A.result];
-  if (r.top < 0) return;
-  const DevCrop c = crops[A.crop0 + r.top];
-  const int gw = c.rw + c.rx, gh = c.rh + c.ry;
-  const int ow = min(gw, A.W - c.rx), oh = min(gh, A.H - c.ry);
-  if (y == 0 && threadIdx.x == 0) {
-    A.out_wh[0] = ow;
-    A.out_wh[1] = oh;
-  }
-  if (y >= oh) return;
-  const uint8_t *s = A.src + (int64_t)(c.ry + y) * A.src_stride + (int64_t)c.rx * A.C;
-  uint8_t *d = A.dst + (int64_t)y * ow * A.C;
-  for (int k = threadIdx.x; k < ow * A.C; k += 256) d[k] = s[k];
 }
 
 // ---------------------------------------------------------------------------

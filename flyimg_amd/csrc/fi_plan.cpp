@@ -519,7 +519,111 @@ int plan_sc(int W, int H, int width, int height, const fi_smartcrop_options &o, 
     }
   }
   if (p->crops.empty()) return fail(FI_ENOCROP, "smartcrop: no crop windows (smartcrop.py:227-228 ValueError)");
+  plan_sc_prep(p);
   return FI_OK;
+}
+
+// k_sc_hrows / k_sc_vmaps launch geometry (fi_smartcrop.hip): row chunks and
+// the LDS each needs (transposed H coefficients + staged source rows; staged
+// H-stage rows + prescaled rows of an output chunk with its one-row halo).
+// Exact-integer MFMA form of Pillow's horizontal pass (k_sc_hmfma): for each
+// block of 16 output columns, the banded coefficient matrix over a window of
+// 64 * ks source columns, split into three signed-byte limbs
+// (k = L0 + 256 L1 + 65536 L2), laid out in the MFMA B-fragment order.
+static void plan_sc_hmfma(ScPlan *p, int sw) {
+  p->hm_ok = false;
+  const int aw = p->aw, nb = (aw + 15) / 16;
+  int ks = 1, maxend = sw;
+  std::vector<int32_t> s0(nb);
+  for (int b = 0; b < nb; b++) {
+    int lo = 1 << 30, hi = 0;
+    for (int x = 16 * b; x < std::min(aw, 16 * b + 16); x++) {
+      lo = std::min(lo, p->hb[2 * x]);
+      hi = std::max(hi, p->hb[2 * x] + p->hb[2 * x + 1]);
+    }
+    s0[b] = lo / 8 * 8;  // fragment reads are two 8-byte LDS reads: 8-B aligned
+    ks = std::max(ks, (hi - s0[b] + 63) / 64);
+  }
+  for (int b = 0; b < nb; b++) maxend = std::max(maxend, s0[b] + 64 * ks);
+  const int pitch = (maxend + 15) / 16 * 16;
+  int rows = 32;
+  while (rows >= 16 && (int64_t)3 * rows * pitch > kHmMaxLds) rows -= 16;
+  if (rows < 16 || ks > 2) return;
+  p->hm_ks = ks;
+  p->hm_pitch = pitch;
+  p->hm_rows = rows;
+  p->hm_nb = nb;
+  p->hm_lds = 3 * rows * pitch;
+  p->hm_chunks = (p->hrows + rows - 1) / rows;
+  p->hmS0 = s0;
+  p->hmC.assign(aw, 0);
+  for (int x = 0; x < aw; x++) {
+    int64_t sum = 0;
+    for (int j = 0; j < p->hb[2 * x + 1]; j++) sum += p->hk[(size_t)x * p->ksh + j];
+    p->hmC[x] = (int32_t)((1 << 21) + 128 * sum);
+  }
+  p->hmB.assign((size_t)nb * ks * 3 * 256, 0);
+  for (int b = 0; b < nb; b++)
+    for (int t = 0; t < ks; t++)
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int x = 16 * b + (l & 15), s = s0[b] + 64 * t + mfma_i8_k(l, j);
+          int32_t k = 0;
+          if (x < aw) {
+            const int xmin = p->hb[2 * x], cnt = p->hb[2 * x + 1];
+            if (s >= xmin && s < xmin + cnt) k = p->hk[(size_t)x * p->ksh + (s - xmin)];
+          }
+          const int32_t l0 = ((k + 128) & 255) - 128;
+          const int32_t k1 = (k - l0) / 256;
+          const int32_t l1 = ((k1 + 128) & 255) - 128;
+          const int32_t l2 = (k1 - l1) / 256;
+          const int32_t limb[3] = {l0, l1, l2};
+          for (int q = 0; q < 3; q++) {
+            uint8_t *frag = reinterpret_cast<uint8_t *>(&p->hmB[((size_t)(b * ks + t) * 3 + q) * 256]);
+            frag[l * 16 + j] = (uint8_t)(int8_t)limb[q];
+          }
+        }
+  p->hm_ok = true;
+}
+
+void plan_sc_prep(ScPlan *p) {
+  p->prep_ok = false;
+  p->hkT.clear();
+  const bool reduced = p->fx > 1 || p->fy > 1;
+  const int sw = reduced ? p->rw : p->W;
+  const int64_t apitch = (p->aw * 3 + 15) / 16 * 16, spitch = (sw * 3 + 15) / 16 * 16;
+  p->h_chunks = 0;
+  p->h_lds = 0;
+  if (p->thumb && p->need_h) {
+    p->hkT.assign((size_t)p->ksh * p->aw, 0);
+    for (int x = 0; x < p->aw; x++)
+      for (int j = 0; j < p->ksh; j++) p->hkT[(size_t)j * p->aw + x] = p->hk[(size_t)x * p->ksh + j];
+    p->h_chunks = (p->hrows + kPrepRows - 1) / kPrepRows;
+    const int64_t lds = ((int64_t)p->ksh * p->aw * 4 + 15) / 16 * 16 + kPrepRows * spitch;
+    if (lds > kPrepMaxLds) return;
+    p->h_lds = (int)lds;
+    plan_sc_hmfma(p, sw);
+  }
+  p->v_chunks = (p->ah + kPrepRows - 1) / kPrepRows;
+  int64_t vmax = 0;
+  const bool need_v = p->thumb && p->need_v;
+  for (int c = 0; c < p->v_chunks; c++) {
+    const int y0 = c * kPrepRows, y1 = std::min(y0 + kPrepRows, p->ah);
+    const int pa = std::max(0, y0 - 1), pb = std::min(p->ah, y1 + 1);
+    int lo = pa, hi = pb;
+    if (need_v) {
+      lo = p->vb[2 * pa];
+      hi = 0;
+      for (int y = pa; y < pb; y++) {
+        if (p->vb[2 * y] < lo) return;  // kernel stages from the first row's window start
+        hi = std::max(hi, p->vb[2 * y] + p->vb[2 * y + 1]);
+      }
+    }
+    vmax = std::max(vmax, (int64_t)(hi - lo) * apitch + (int64_t)(pb - pa) * apitch);
+  }
+  if (vmax > kPrepMaxLds) return;
+  p->v_lds = (int)vmax;
+  p->prep_ok = true;
 }
 
 static double thirds(double x) {

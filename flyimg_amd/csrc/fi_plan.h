@@ -76,8 +76,18 @@ struct ScPlan {
   bool need_h = false, need_v = false;
   int ksh = 0, ksv = 0, ybox_first = 0, hrows = 0;
   std::vector<int32_t> hb, hk, vb, vk;  // bounds pairs and int32 coeffs
+  std::vector<int32_t> hkT;             // hk transposed [ksh][aw]
+  bool prep_ok = false;                 // k_sc_hrows/k_sc_vmaps fit LDS (else generic kernels)
+  int h_chunks = 0, h_lds = 0, v_chunks = 0, v_lds = 0;
+  // k_sc_hmfma: exact-integer MFMA horizontal pass (fi_internal.h mfma_i8_k)
+  bool hm_ok = false;
+  int hm_ks = 0, hm_pitch = 0, hm_rows = 0, hm_nb = 0, hm_lds = 0, hm_chunks = 0;
+  std::vector<int32_t> hmB;   // [nb][ks][3 limbs] fragments of 64 lanes x 16 B (256 int32)
+  std::vector<int32_t> hmC;   // [aw] 2^21 + 128 * sum_j k[x][j]  (pixels enter as p - 128)
+  std::vector<int32_t> hmS0;  // [nb] first source column of the block's window (multiple of 16)
   std::vector<CropHost> crops;
 };
+void plan_sc_prep(ScPlan *p);
 int plan_sc(int W, int H, int target_w, int target_h, const fi_smartcrop_options &o, ScPlan *p);
 void sc_importance_table(const fi_smartcrop_params &P, double fw, double fh, int nx, int ny,
                          std::vector<double> *out);

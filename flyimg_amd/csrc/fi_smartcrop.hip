@@ -1,0 +1,558 @@
+// fi_smartcrop.hip -- smartcrop.py's saliency stage, one workgroup per image.
+//
+//   k_sc_hrows    Pillow thumbnail, horizontal pass (22-bit fixed-point
+//                 Lanczos, Resample.c) -> u8 rows in HBM; per (image, row chunk).
+//   k_sc_vmaps    vertical pass + the analyse() maps (luma, Laplacian edge,
+//                 skin, saturation; smartcrop.py:94-101, 231-274) per (image,
+//                 output-row chunk), rows staged in LDS; writes the packed
+//                 maps (skin | edge << 8 | sat << 16).
+//   k_sc_score2   every crop's score (smartcrop.py:300-338) + the argmax
+//                 (:116-133), maps resident in LDS: fast f64 pass with a
+//                 rigorous error bound, exact sequential re-score of the
+//                 crops whose interval reaches the best lower bound.
+//   k_crop_apply2 convert -crop of the winning box (SmartCropProcessor.php:30-34).
+//
+// The generic per-row kernels in fi_kernels.hip remain for geometries whose
+// staging does not fit LDS (ScPlan::prep_ok == 0).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fi_internal.h"
+#include "fi_sc_device.h"
+
+namespace fi {
+
+constexpr int kPrepThreads = 256;
+
+// ---- k_sc_hrows: Pillow's horizontal pass, one workgroup per (image, chunk
+// of kPrepRows H-stage rows).  Source rows and the transposed coefficient
+// table are staged in LDS; output rows go to D.hbuf with pitch apitch.
+__global__ __launch_bounds__(kPrepThreads) void k_sc_hrows(const ScDesc *__restrict__ descs,
+                                                           const int32_t *__restrict__ ai) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const ScDesc &D = descs[blockIdx.x];
+  const int r0 = blockIdx.y * kPrepRows;
+  if (r0 >= D.hrows) return;
+  const int r1 = min(r0 + kPrepRows, D.hrows);
+  const int tid = threadIdx.x;
+  const bool reduced = D.fx > 1 || D.fy > 1;
+  const uint8_t *src = reduced ? D.red : D.img;
+  const int64_t sstride = reduced ? (int64_t)D.rw * 3 : D.stride;
+  const int sC = reduced ? 3 : D.C;
+  const int sW = reduced ? D.rw : D.W;
+  const int aw = D.aw, ksh = D.ksh;
+  const int apitch = (aw * 3 + 15) & ~15;
+  const int spitch = (sW * 3 + 15) & ~15;
+  int32_t *kT = reinterpret_cast<int32_t *>(lds8);  // [ksh][aw]
+  uint8_t *stg = lds8 + (((size_t)ksh * aw * 4 + 15) & ~(size_t)15);  // [kPrepRows][spitch]
+  const int32_t *hb = ai + D.hb, *hkT = ai + D.hkT;
+  for (int k = tid; k < ksh * aw; k += kPrepThreads) kT[k] = hkT[k];
+  const int rowbytes = sW * sC, yoff = D.ybox_first;
+  if ((((uintptr_t)src | (uintptr_t)sstride) & 3) == 0) {
+    const int nd = (rowbytes + 3) >> 2;  // rows are padded to 16 B in the staging buffer
+    for (int it = tid; it < (r1 - r0) * nd; it += kPrepThreads) {
+      const int rr = it / nd, k = it - rr * nd;
+      const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride;
+      uint32_t v;
+      if (4 * k + 4 <= rowbytes) {
+        v = reinterpret_cast<const uint32_t *>(s)[k];
+      } else {  // row tail
+        v = 0;
+        for (int b = 0; 4 * k + b < rowbytes; b++) v |= (uint32_t)s[4 * k + b] << (8 * b);
+      }
+      reinterpret_cast<uint32_t *>(stg + rr * spitch)[k] = v;
+    }
+  } else {
+    for (int it = tid; it < (r1 - r0) * rowbytes; it += kPrepThreads) {
+      const int rr = it / rowbytes, k = it - rr * rowbytes;
+      stg[rr * spitch + k] = src[(int64_t)(r0 + rr + yoff) * sstride + k];
+    }
+  }
+  __syncthreads();
+  for (int it = tid; it < (r1 - r0) * aw; it += kPrepThreads) {
+    const int rr = it / aw, x = it - rr * aw;
+    const uint8_t *srow = stg + rr * spitch;
+    const int xmin = hb[2 * x], cnt = hb[2 * x + 1];
+    int32_t s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+    if (sC == 3) {
+      const uint8_t *q = srow + 3 * xmin;
+      for (int j = 0; j < cnt; j++) {
+        const int32_t k = kT[j * aw + x];
+        s0 += (int32_t)q[3 * j] * k;
+        s1 += (int32_t)q[3 * j + 1] * k;
+        s2 += (int32_t)q[3 * j + 2] * k;
+      }
+    } else {  // gray input pasted into RGB (smartcrop.py:357-365): R = G = B
+      const uint8_t *q = srow + xmin;
+      for (int j = 0; j < cnt; j++) s0 += (int32_t)q[j] * kT[j * aw + x];
+      s1 = s2 = s0;
+    }
+    uint8_t *o = D.hbuf + (int64_t)(r0 + rr) * apitch + 3 * x;
+    o[0] = pil_clip8(s0);
+    o[1] = pil_clip8(s1);
+    o[2] = pil_clip8(s2);
+  }
+}
+
+// ---- k_sc_hmfma: the same horizontal pass as exact integer MFMA.  One
+// workgroup per (image, chunk of hm_rows H-stage rows).  Source rows are
+// staged as three planar channels of (p - 128) in signed bytes; each wave
+// takes 16-column output blocks: D = A(16 rows x 64 cols of one channel)
+// x B(64 cols x 16 outputs) with v_mfma_i32_16x16x64_i8 per coefficient limb,
+// then sum = D0 + 256 D1 + 65536 D2 + 2^21 + 128 sum(k) is Pillow's int32
+// accumulator bit for bit (Resample.c ImagingResampleHorizontal_8bpc).
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(kPrepThreads) void k_sc_hmfma(const ScDesc *__restrict__ descs,
+                                                           const int32_t *__restrict__ ai) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const ScDesc &D = descs[blockIdx.x];
+  const int R = D.hm_rows, P = D.hm_pitch, KS = D.hm_ks, nb = D.hm_nb;
+  const int r0 = blockIdx.y * R;
+  if (r0 >= D.hrows) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool reduced = D.fx > 1 || D.fy > 1;
+  const uint8_t *src = reduced ? D.red : D.img;
+  const int64_t sstride = reduced ? (int64_t)D.rw * 3 : D.stride;
+  const int sC = reduced ? 3 : D.C;
+  const int sW = reduced ? D.rw : D.W;
+  const int aw = D.aw, hrows = D.hrows, yoff = D.ybox_first;
+  const int apitch = (aw * 3 + 15) & ~15;
+  const int nch = sC == 3 ? 3 : 1;
+  // ---- stage rows [r0, r0 + R) as planes [c][row][P] of (p - 128); zero pad
+  const int ng = P >> 2;  // 4-pixel groups per plane row
+  const bool a4 = (((uintptr_t)src | (uintptr_t)sstride) & 3) == 0;
+  for (int it = tid; it < R * ng; it += kPrepThreads) {
+    const int rr = it / ng, g = it - rr * ng;
+    uint32_t w0 = 0, w1 = 0, w2 = 0;
+    if (r0 + rr < hrows && 4 * g < sW) {
+      const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride;
+      if (sC == 3) {
+        uint8_t b[12];
+        if (a4 && 4 * g + 4 <= sW) {
+          const uint32_t *q = reinterpret_cast<const uint32_t *>(s + 12 * g);
+          const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            b[k] = (uint8_t)(d0 >> (8 * k));
+            b[4 + k] = (uint8_t)(d1 >> (8 * k));
+            b[8 + k] = (uint8_t)(d2 >> (8 * k));
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 12; k++) b[k] = (4 * g + k / 3 < sW) ? s[12 * g + k] : (uint8_t)128;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          w0 |= (uint32_t)(b[3 * i] ^ 0x80) << (8 * i);
+          w1 |= (uint32_t)(b[3 * i + 1] ^ 0x80) << (8 * i);
+          w2 |= (uint32_t)(b[3 * i + 2] ^ 0x80) << (8 * i);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) w0 |= (uint32_t)((4 * g + i < sW ? s[4 * g + i] : (uint8_t)128) ^ 0x80) << (8 * i);
+      }
+    }
+    reinterpret_cast<uint32_t *>(lds8 + (0 * R + rr) * P)[g] = w0;
+    if (nch == 3) {
+      reinterpret_cast<uint32_t *>(lds8 + (1 * R + rr) * P)[g] = w1;
+      reinterpret_cast<uint32_t *>(lds8 + (2 * R + rr) * P)[g] = w2;
+    }
+  }
+  __syncthreads();
+  const int32_t *hmS0 = ai + D.hmS0, *hmC = ai + D.hmC;
+  const i32x4 *hmB = reinterpret_cast<const i32x4 *>(ai + D.hmB);
+  const int k0 = mfma_i8_k(lane, 0), k8 = mfma_i8_k(lane, 8);
+  for (int b = wave; b < nb; b += kPrepThreads / 64) {
+    const int s0 = hmS0[b];
+    i32x4 Bf[2][3];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+      for (int q = 0; q < 3; q++) Bf[t][q] = t < KS ? hmB[((b * KS + t) * 3 + q) * 64 + lane] : i32x4{0, 0, 0, 0};
+    const int x = 16 * b + (lane & 15);
+    const int32_t cx = x < aw ? hmC[x] : 0;
+    for (int c = 0; c < nch; c++) {
+      for (int rb = 0; rb < R; rb += 16) {
+        i32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+          if (t < KS) {
+            const uint8_t *base = lds8 + (c * R + rb + (lane & 15)) * P + s0 + 64 * t;
+            const i32x2 lo = *reinterpret_cast<const i32x2 *>(base + k0);
+            const i32x2 hi = *reinterpret_cast<const i32x2 *>(base + k8);
+            const i32x4 a = {lo.x, lo.y, hi.x, hi.y};
+            acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, Bf[t][0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, Bf[t][1], acc1, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, Bf[t][2], acc2, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int row = r0 + rb + 4 * (lane >> 4) + i;
+          if (x < aw && row < hrows) {
+            // modular int32: the limbs' partial products may wrap, the sum fits
+            const uint32_t v = (uint32_t)acc0[i] + ((uint32_t)acc1[i] << 8) + ((uint32_t)acc2[i] << 16) + (uint32_t)cx;
+            const uint8_t o = pil_clip8((int32_t)v);
+            uint8_t *dst = D.hbuf + (int64_t)row * apitch + 3 * x;
+            if (nch == 3) {
+              dst[c] = o;
+            } else {
+              dst[0] = dst[1] = dst[2] = o;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---- k_sc_vmaps: Pillow's vertical pass + analyse() maps, one workgroup per
+// (image, chunk of kPrepRows output rows).  The H-stage rows the chunk and its
+// one-row halo need are staged in LDS (from hbuf, or from the source when no
+// horizontal pass runs), the prescaled rows [y0-1, y1+1) are computed into
+// LDS, then the maps of [y0, y1) are written.
+__global__ __launch_bounds__(kPrepThreads) void k_sc_vmaps(const ScDesc *__restrict__ descs,
+                                                           const int32_t *__restrict__ ai, const ScParamsDev P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const ScDesc &D = descs[blockIdx.x];
+  const int aw = D.aw, ah = D.ah;
+  const int y0 = blockIdx.y * kPrepRows;
+  if (y0 >= ah) return;
+  const int y1 = min(y0 + kPrepRows, ah);
+  const int pa = max(0, y0 - 1), pb = min(ah, y1 + 1);
+  const int tid = threadIdx.x;
+  const int apitch = (aw * 3 + 15) & ~15;
+  const int32_t *vb = ai + D.vb, *vk = ai + D.vk;
+  const bool need_v = D.need_v;
+  int lo = pa, hi = pb;
+  if (need_v) {
+    lo = vb[2 * pa];
+    hi = 0;
+    for (int y = pa; y < pb; y++) hi = max(hi, vb[2 * y] + vb[2 * y + 1]);
+  }
+  uint8_t *rows = lds8;                        // [hi - lo][apitch] H-stage rows
+  uint8_t *prer = lds8 + (hi - lo) * apitch;   // [pb - pa][apitch] prescaled rows
+  if (D.need_h) {
+    const int nq = apitch >> 4;
+    for (int it = tid; it < (hi - lo) * nq; it += kPrepThreads) {
+      const int rr = it / nq, k = it - rr * nq;
+      reinterpret_cast<uint4 *>(rows + rr * apitch)[k] =
+          reinterpret_cast<const uint4 *>(D.hbuf + (int64_t)(lo + rr) * apitch)[k];
+    }
+  } else {
+    const bool reduced = D.fx > 1 || D.fy > 1;
+    const uint8_t *src = reduced ? D.red : D.img;
+    const int64_t sstride = reduced ? (int64_t)D.rw * 3 : D.stride;
+    const int sC = reduced ? 3 : D.C;
+    for (int it = tid; it < (hi - lo) * aw; it += kPrepThreads) {
+      const int rr = it / aw, x = it - rr * aw;
+      const uint8_t *s = src + (int64_t)(lo + rr) * sstride + x * sC;
+      uint8_t *o = rows + rr * apitch + 3 * x;
+      o[0] = s[0];
+      o[1] = s[sC == 3 ? 1 : 0];
+      o[2] = s[sC == 3 ? 2 : 0];
+    }
+  }
+  __syncthreads();
+  for (int it = tid; it < (pb - pa) * aw; it += kPrepThreads) {
+    const int yr = it / aw, x = it - yr * aw, y = pa + yr;
+    uint8_t *q = prer + yr * apitch + 3 * x;
+    if (need_v) {
+      const int ymin = vb[2 * y], cnt = vb[2 * y + 1];
+      const int32_t *k = vk + y * D.ksv;
+      const uint8_t *p = rows + (ymin - lo) * apitch + 3 * x;
+      int32_t s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+      for (int j = 0; j < cnt; j++) {
+        const int32_t kj = k[j];
+        s0 += (int32_t)p[j * apitch] * kj;
+        s1 += (int32_t)p[j * apitch + 1] * kj;
+        s2 += (int32_t)p[j * apitch + 2] * kj;
+      }
+      q[0] = pil_clip8(s0);
+      q[1] = pil_clip8(s1);
+      q[2] = pil_clip8(s2);
+    } else {
+      const uint8_t *p = rows + (y - lo) * apitch + 3 * x;
+      q[0] = p[0];
+      q[1] = p[1];
+      q[2] = p[2];
+    }
+  }
+  __syncthreads();
+  for (int it = tid; it < (y1 - y0) * aw; it += kPrepThreads) {
+    const int yr = it / aw, x = it - yr * aw, y = y0 + yr;
+    const uint8_t *row = prer + (y - pa) * apitch;
+    const uint32_t r = row[3 * x], g = row[3 * x + 1], b = row[3 * x + 2];
+    if (D.pre) {
+      uint8_t *o = D.pre + ((int64_t)y * aw + x) * 3;
+      o[0] = (uint8_t)r;
+      o[1] = (uint8_t)g;
+      o[2] = (uint8_t)b;
+    }
+    const uint32_t L = sc_luma(r, g, b);
+    // detect_edge: ImagingFilter3x3 interior, border copies L
+    uint32_t E = L;
+    if (aw >= 3 && ah >= 3 && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
+      const uint8_t *up = row - apitch, *dn = row + apitch;
+      const int v = 4 * (int)L - (int)sc_luma(up[3 * x], up[3 * x + 1], up[3 * x + 2]) -
+                    (int)sc_luma(dn[3 * x], dn[3 * x + 1], dn[3 * x + 2]) -
+                    (int)sc_luma(row[3 * x - 3], row[3 * x - 2], row[3 * x - 1]) -
+                    (int)sc_luma(row[3 * x + 3], row[3 * x + 4], row[3 * x + 5]) + 1;
+      E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
+    }
+    D.maps[(int64_t)y * aw + x] = sc_skin_sat(r, g, b, L, P) | (E << 8);
+  }
+}
+
+// ---------------------------------------------------------------------------
+constexpr int kScoreThreads = 512;
+constexpr int kScoreWaves = kScoreThreads / 64;
+
+template <bool LDS_MAPS>
+__global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__restrict__ descs,
+                                                             const DevCrop *__restrict__ crops,
+                                                             const double *__restrict__ ad,
+                                                             CropScore *__restrict__ scores,
+                                                             ScResult *__restrict__ results, const ScParamsDev P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smaps[];
+  __shared__ double lut[256];
+  __shared__ double part[kScoreWaves][3];
+  __shared__ double T[3];
+  __shared__ double s_tot[kScoreMaxCrops];
+  __shared__ double s_bnd[kScoreMaxCrops];
+  __shared__ int32_t cand[kScoreMaxCrops];
+  __shared__ int32_t ncand_s;
+  const ScDesc &D = descs[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ncrops = D.ncrops;
+  const int W = D.aw, H = D.ah, npx = W * H;
+  const uint32_t *maps = D.maps;
+  if (LDS_MAPS) {
+    const uint4 *g = reinterpret_cast<const uint4 *>(D.maps);
+    for (int k = tid; k < (npx >> 2); k += kScoreThreads) reinterpret_cast<uint4 *>(smaps)[k] = g[k];
+    for (int k = (npx & ~3) + tid; k < npx; k += kScoreThreads) smaps[k] = D.maps[k];
+    maps = smaps;
+  }
+  if (tid < 256) lut[tid] = (double)tid / 255.0;  // Python int / 255 (correctly rounded)
+  __syncthreads();
+  const double sb = P.skin_bias, tb = P.saturation_bias, oi = P.outside_importance;
+  // image totals of the three per-pixel terms (the outside part of every crop)
+  {
+    double t0 = 0, t1 = 0, t2 = 0;
+    for (int p = tid; p < npx; p += kScoreThreads) {
+      const uint32_t m = maps[p];
+      const double d = lut[(m >> 8) & 255];
+      t0 += d;
+      t1 += lut[m & 255] * (d + sb);
+      t2 += lut[(m >> 16) & 255] * (d + tb);
+    }
+    t0 = wave_sum(t0);
+    t1 = wave_sum(t1);
+    t2 = wave_sum(t2);
+    if (lane == 0) {
+      part[wave][0] = t0;
+      part[wave][1] = t1;
+      part[wave][2] = t2;
+    }
+    __syncthreads();
+    if (tid < 3) {
+      double s = 0;
+      for (int w = 0; w < kScoreWaves; w++) s += part[w][tid];
+      T[tid] = s;
+    }
+    __syncthreads();
+  }
+  const double u = 1.1102230246251565e-16;  // 2^-53
+  const double nn = (double)npx + 1.0;
+  const double gam = nn * u / (1.0 - nn * u);
+  const double aoi = fabs(oi);
+  const double wd = P.detail_weight, ws = P.skin_weight, wt = P.saturation_weight;
+
+  // ---- fast pass: one wave per crop, lanes across the window's columns
+  for (int c = wave; c < ncrops; c += kScoreWaves) {
+    const DevCrop cr = crops[D.crop0 + c];
+    const double *tab = ad + cr.table;
+    double sd = 0, ss = 0, st = 0, id = 0, is = 0, it = 0;
+    for (int dx0 = 0; dx0 < cr.nin_x; dx0 += 64) {
+      const int dx = dx0 + lane;
+      const bool act = dx < cr.nin_x;
+      const int dxc = act ? dx : 0;
+      const uint32_t *mcol = maps + (int64_t)cr.y0 * W + cr.x0 + dxc;
+      const double *tcol = tab + dxc;
+#pragma unroll 4
+      for (int dy = 0; dy < cr.nin_y; dy++) {
+        const uint32_t m = act ? mcol[dy * W] : 0u;  // m = 0: every term is 0
+        const double imp = tcol[(int64_t)dy * cr.table_w];
+        const double d = lut[(m >> 8) & 255];
+        const double a1 = lut[m & 255] * (d + sb);
+        const double a2 = lut[(m >> 16) & 255] * (d + tb);
+        sd = fma(imp, d, sd);
+        ss = fma(imp, a1, ss);
+        st = fma(imp, a2, st);
+        id += d;
+        is += a1;
+        it += a2;
+      }
+    }
+    sd = wave_sum(sd);
+    ss = wave_sum(ss);
+    st = wave_sum(st);
+    id = wave_sum(id);
+    is = wave_sum(is);
+    it = wave_sum(it);
+    if (lane == 0) {
+      const double Fd = sd + oi * (T[0] - id), Fs = ss + oi * (T[1] - is), Ft = st + oi * (T[2] - it);
+      // |python_sum - F| <= 5 gamma(n+1) (sum |imp a|); with a >= 0 (biases >= 0, host-checked)
+      // sum |imp a| <= imax * inside(a) + |oi| * total(a)   ("bound-and-verify")
+      const double Ed = 5.0 * gam * (cr.imax * id + aoi * T[0]) * 1.0000001;
+      const double Es = 5.0 * gam * (cr.imax * is + aoi * T[1]) * 1.0000001;
+      const double Et = 5.0 * gam * (cr.imax * it + aoi * T[2]) * 1.0000001;
+      const double area = cr.fw * cr.fh;
+      const double tot = (Fd * wd + Fs * ws + Ft * wt) / area;
+      const double mag = fabs(wd) * (fabs(Fd) + Ed) + fabs(ws) * (fabs(Fs) + Es) + fabs(wt) * (fabs(Ft) + Et);
+      const double B = ((fabs(wd) * Ed + fabs(ws) * Es + fabs(wt) * Et) * (1.0 + 16.0 * u) + 16.0 * u * mag) /
+                       area * 1.01;
+      s_tot[c] = tot;
+      s_bnd[c] = B;
+      CropScore &o = scores[D.score0 + c];
+      o.detail = Fd;
+      o.saturation = Ft;
+      o.skin = Fs;
+      o.total = tot;
+      o.bound = B;
+      o.exact = 0;
+    }
+  }
+  __syncthreads();
+  // candidates: every crop whose interval reaches the best lower bound
+  if (tid == 0) {
+    double best_lo = -1.0e308;
+    for (int c = 0; c < ncrops; c++) best_lo = fmax(best_lo, s_tot[c] - s_bnd[c]);
+    int k = 0;
+    for (int c = 0; c < ncrops; c++)
+      if (D.exact_all || s_tot[c] + s_bnd[c] >= best_lo) cand[k++] = c;
+    ncand_s = k;
+  }
+  __syncthreads();
+  const int ncand = ncand_s;
+  const bool need_exact = D.exact_all || ncand > 1;
+  if (need_exact) {
+    // exact re-score: one lane per candidate, the reference's row-major order
+    for (int k = tid; k < ncand; k += kScoreThreads) {
+      const int c = cand[k];
+      const DevCrop cr = crops[D.crop0 + c];
+      const double *tab = ad + cr.table;
+      double skin = 0, detail = 0, sat = 0;
+      for (int y = 0; y < H; y++) {
+        const bool yin = y >= cr.y0 && y < cr.y0 + cr.nin_y;
+        const uint32_t *mrow = maps + (int64_t)y * W;
+        const int64_t trow = (int64_t)(y - cr.y0) * cr.table_w - cr.x0;
+#pragma unroll 4
+        for (int x = 0; x < W; x++) {
+          const bool in = yin && x >= cr.x0 && x < cr.x0 + cr.nin_x;
+          const double tv = tab[in ? trow + x : 0];
+          const double imp = in ? tv : oi;
+          const uint32_t m = mrow[x];
+          const double det = lut[(m >> 8) & 255];
+          skin = skin + lut[m & 255] * (det + sb) * imp;
+          detail = detail + det * imp;
+          sat = sat + lut[(m >> 16) & 255] * (det + tb) * imp;
+        }
+      }
+      const double tot = (detail * wd + skin * ws + sat * wt) / (cr.fw * cr.fh);
+      s_tot[c] = tot;
+      CropScore &o = scores[D.score0 + c];
+      o.detail = detail;
+      o.saturation = sat;
+      o.skin = skin;
+      o.total = tot;
+      o.bound = 0;
+      o.exact = 1;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int top = cand[0];
+    double best = s_tot[top];
+    if (need_exact) {
+      best = -9223372036854775807.0;  // -sys.maxsize; strict > keeps the first max
+      for (int k = 0; k < ncand; k++) {
+        const double v = s_tot[cand[k]];
+        if (v > best) {
+          best = v;
+          top = cand[k];
+        }
+      }
+    }
+    results[D.result].top = top;
+    results[D.result].n_candidates = ncand;
+    results[D.result].total = best;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// convert <out> -crop WxH+X+Y with W = w + x, H = h + y as smartcrop.py prints
+// them (:372-377); CropImage clips to the image.  kApplyBands workgroups per
+// image, rows interleaved.
+constexpr int kApplyBands = 8;
+__global__ __launch_bounds__(256) void k_crop_apply2(const ApplyDesc *__restrict__ descs,
+                                                     const DevCrop *__restrict__ crops,
+                                                     const ScResult *__restrict__ results) {
+  const ApplyDesc &A = descs[blockIdx.x / kApplyBands];
+  const int band = blockIdx.x % kApplyBands;
+  const ScResult r = results[A.result];
+  if (r.top < 0) return;
+  const DevCrop c = crops[A.crop0 + r.top];
+  const int gw = c.rw + c.rx, gh = c.rh + c.ry;
+  const int ow = min(gw, A.W - c.rx), oh = min(gh, A.H - c.ry);
+  if (band == 0 && threadIdx.x == 0) {
+    A.out_wh[0] = ow;
+    A.out_wh[1] = oh;
+  }
+  const int rowb = ow * A.C;
+  for (int y = band; y < oh; y += kApplyBands) {
+    const uint8_t *__restrict__ s = A.src + (int64_t)(c.ry + y) * A.src_stride + (int64_t)c.rx * A.C;
+    uint8_t *__restrict__ d = A.dst + (int64_t)y * rowb;
+    for (int k = threadIdx.x; k < rowb; k += 256) d[k] = s[k];
+  }
+}
+
+int launch_sc_h(hipStream_t s, bool mfma, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai) {
+  if (n <= 0 || chunks <= 0) return 0;
+  if (lds > (mfma ? kHmMaxLds : kPrepMaxLds)) return -1;
+  if (mfma)
+    hipLaunchKernelGGL(k_sc_hmfma, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai);
+  else
+    hipLaunchKernelGGL(k_sc_hrows, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai);
+  return 0;
+}
+int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
+                const ScParamsDev &P) {
+  if (n <= 0) return 0;
+  if (lds > kPrepMaxLds) return -1;
+  hipLaunchKernelGGL(k_sc_vmaps, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai, P);
+  return 0;
+}
+int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, int max_px, const DevCrop *crops,
+                    const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P) {
+  if (n <= 0) return 0;
+  if (lds_maps) {
+    const size_t lds = (size_t)max_px * 4;
+    if (lds > (size_t)kScoreLdsMaps) return -1;
+    hipLaunchKernelGGL((k_sc_score2<true>), dim3(n), dim3(kScoreThreads), lds, s, descs, crops, ad, scores, results,
+                       P);
+  } else {
+    hipLaunchKernelGGL((k_sc_score2<false>), dim3(n), dim3(kScoreThreads), 0, s, descs, crops, ad, scores, results,
+                       P);
+  }
+  return 0;
+}
+int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_crop_apply2, dim3(n * kApplyBands), dim3(256), 0, s, descs, crops, results);
+  return 0;
+}
+
+}  // namespace fi

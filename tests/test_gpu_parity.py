@@ -29,21 +29,42 @@ def ctx():
     c.close()
 
 
-@pytest.fixture(scope="module", params=["fused", "generic"])
-def rctx(request):
-    """Resample path under test: the fused vertical-first kernel (default) or
-    the generic two-pass kernels (FI_DISABLE_FUSED=1 at context creation)."""
+def _context_with(env):
     import os
 
-    old = os.environ.get("FI_DISABLE_FUSED")
-    os.environ["FI_DISABLE_FUSED"] = "1" if request.param == "generic" else "0"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
-        c = Context(0)
+        return Context(0)
     finally:
-        if old is None:
-            os.environ.pop("FI_DISABLE_FUSED", None)
-        else:
-            os.environ["FI_DISABLE_FUSED"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+PATHS = {
+    # default kernels: fused resample; MFMA horizontal prescale, k_sc_vmaps, k_sc_score2
+    "fused": {"FI_DISABLE_FUSED": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0"},
+    # generic kernels: two-pass resample, per-row prescale/maps kernels
+    "generic": {"FI_DISABLE_FUSED": "1", "FI_DISABLE_SC_PREP": "1", "FI_DISABLE_SC_MFMA": "1"},
+    # per-image prescale with the VALU horizontal pass (k_sc_hrows)
+    "valu_h": {"FI_DISABLE_FUSED": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "1"},
+}
+
+
+@pytest.fixture(scope="module", params=["fused", "generic"])
+def rctx(request):
+    """Kernel path under test (environment read at context creation)."""
+    c = _context_with(PATHS[request.param])
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module", params=sorted(PATHS))
+def sctx(request):
+    c = _context_with(PATHS[request.param])
     yield c
     c.close()
 
@@ -78,7 +99,8 @@ def test_synthetic_generator_matches_numpy(ctx):
 
 
 @pytest.mark.parametrize("case", SC["cases"], ids=[c["name"] for c in SC["cases"]])
-def test_smartcrop_exact_all_bit_exact(ctx, case):
+def test_smartcrop_exact_all_bit_exact(sctx, case):
+    ctx = sctx
     arr = G.case_input(case)
     r = ctx.smartcrop_ex(arr, 100, 100, options=_opts(True), want_images=True)
     assert G.sha(r["prescaled"]) == case["prescaled_sha256"]
@@ -90,7 +112,8 @@ def test_smartcrop_exact_all_bit_exact(ctx, case):
 
 
 @pytest.mark.parametrize("case", SC["cases"], ids=[c["name"] for c in SC["cases"]])
-def test_smartcrop_fast_path_top_crop(ctx, case):
+def test_smartcrop_fast_path_top_crop(sctx, case):
+    ctx = sctx
     """Default (bound-and-verify) path: same top crop and exact top score."""
     arr = G.case_input(case)
     r = ctx.smartcrop_ex(arr, 100, 100, options=_opts(False))
@@ -104,7 +127,8 @@ def test_smartcrop_fast_path_top_crop(ctx, case):
         assert abs(t.total - float.fromhex(g[7])) <= 1e-9 * max(1.0, abs(t.total))
 
 
-def test_smartcrop_reference_fixture(ctx):
+def test_smartcrop_reference_fixture(sctx):
+    ctx = sctx
     """SmartCropProcessorTest.php:16-24: smart_crop.jpg -> 674x674+0+0."""
     g = SC["fixture"]
     arr = G.fixture_input()
