@@ -37,6 +37,15 @@ WORKLOADS = {
 }
 
 
+KERNEL_OF_PATH = {
+    "path_mfma": "k_rs_mfma (exact-integer MFMA, vertical first)",
+    "path_fused": "k_rs_fused (VALU, vertical first)",
+    "path_generic_v": "k_rs_v_u8 + k_rs_h_final (two-pass)",
+    "path_generic_h": "k_rs_h_u8 + k_rs_v_final (two-pass)",
+    "path_copy": "k_rs_copy",
+}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -149,6 +158,8 @@ def main():
     el = t1 - t0
     stats = {k: ctx.stats(k) for k in ("batch", "resize", "sc_prep", "sc_score", "crop_apply",
                                       "host_plan", "host_launch", "host_after_sync", "host_total")}
+    # images per resample kernel over the timed steps (counts kept by the library)
+    paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in KERNEL_OF_PATH}
     allv = comm.allgather_obj({"elapsed": el, "stats": stats,
                                "ncand": sum(arr[i].n_candidates for i in range(nimg)),
                                "bad": sum(1 for i in range(nimg) if arr[i].status != 0)})
@@ -182,9 +193,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("resize stage: k_rs_v_u8 + k_rs_h_final (generic two-pass)"
-                           if os.environ.get("FI_DISABLE_FUSED") == "1"
-                           else "resize stage: k_rs_fused<K> (fused vertical-first, one launch per batch)"),
+                "kernel": "resize stage: " + " + ".join(
+                    f"{KERNEL_OF_PATH[p]} ({n} images)" for p, n in paths.items() if n) ,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

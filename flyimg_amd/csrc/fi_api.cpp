@@ -49,6 +49,10 @@ int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, in
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
 __global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
 // fused vertical-first resample (fi_fused.hip)
+// exact-integer MFMA resample (fi_mfma.hip)
+size_t mfma_lds_bytes(int nblocks);
+int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const MTile *tiles, int ntiles,
+                const int32_t *ai, size_t lds);
 int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
                  const int32_t *ai, const float *af, int hw_pitch, int max_taps, int max_nbytes);
 }  // namespace fi
@@ -118,7 +122,10 @@ struct fi_ctx {
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
   std::map<const AxisTable *, RingTable> ring_cache;
   std::map<const AxisTable *, std::vector<StripTab>> strip_cache;
+  std::map<const AxisTable *, MfmaV> mv_cache;  // ok iff nyb > 0
+  std::map<const AxisTable *, MfmaH> mh_cache;  // ok iff !strips.empty()
   bool fused = true;    // FI_DISABLE_FUSED=1 forces the generic two-pass resample
+  bool mfma_rs = false;  // FI_ENABLE_MFMA_RS=1: k_rs_mfma instead of the VALU fused kernel
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
   bool sc_mfma = true;  // FI_DISABLE_SC_MFMA=1: VALU horizontal pass (k_sc_hrows) instead of k_sc_hmfma
 };
@@ -281,6 +288,8 @@ static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, 
       c->axis_cache.clear();
       c->ring_cache.clear();
       c->strip_cache.clear();
+      c->mv_cache.clear();
+      c->mh_cache.clear();
     }
     AxisTable t;
     build_axis(filter, factor, in_sampled, out_size, o0, o1, sample, in_src, &t);
@@ -689,6 +698,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
   std::vector<const std::vector<StripTab> *> fused_strips_of;
   std::map<const StripTab *, std::pair<int32_t, int32_t>> strip_placed;
   std::vector<int> fused_img;  // indices into rd
+  std::vector<int> mfma_img;   // indices into rd (mode 4)
+  std::vector<const MfmaV *> mfma_v;
+  std::vector<const MfmaH *> mfma_h;
   // per image resized-buffer workspace offsets (for smartcrop-apply)
   std::vector<size_t> res_off(n, 0);
   double resize_bytes = 0;
@@ -747,8 +759,28 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
           add_axis(c, E, P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &d.v, placed);
       const AxisTable *ht =
           add_axis(c, E, P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &d.h, placed);
+      const MfmaV *mv = nullptr;
+      const MfmaH *mh = nullptr;
+      if (!P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0) {
+        auto vit = c->mv_cache.find(vt);
+        if (vit == c->mv_cache.end()) {
+          MfmaV m;
+          if (!build_mfma_v(*vt, &m)) m = MfmaV();
+          vit = c->mv_cache.emplace(vt, std::move(m)).first;
+        }
+        auto hit = c->mh_cache.find(ht);
+        if (hit == c->mh_cache.end()) {
+          MfmaH m;
+          if (!build_mfma_h(*ht, &m)) m = MfmaH();
+          hit = c->mh_cache.emplace(ht, std::move(m)).first;
+        }
+        if (vit->second.nyb > 0 && !hit->second.strips.empty()) {
+          mv = &vit->second;
+          mh = &hit->second;
+        }
+      }
       const RingTable *ring = nullptr;
-      if (!P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0 &&
+      if (!mv && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0 &&
           d.h.maxtaps <= 64) {
         auto rit = c->ring_cache.find(vt);
         if (rit == c->ring_cache.end()) {
@@ -771,7 +803,13 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
         else
           strips = &sit->second;
       }
-      if (ring) {
+      if (mv) {
+        d.mode = 4;  // exact-integer MFMA, vertical first
+        mfma_img.push_back((int)rd.size());
+        mfma_v.push_back(mv);
+        mfma_h.push_back(mh);
+        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
+      } else if (ring) {
         d.mode = 3;  // fused vertical-first
         d.fused_k = ring->K;
         d.ring_n = (int32_t)ring->rows.size();
@@ -812,12 +850,16 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
         d.mid_cols = P.ew;
         d.mid_stride = (3 * P.ew + 7) / 8 * 8;
       }
-      if (d.mode != 3) {
+      if (d.mode != 3 && d.mode != 4) {
         d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
         src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
       }
     }
     resize_bytes += (double)src_bytes + (double)need;
+    {
+      static const char *kPath[5] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_mfma"};
+      c->stats[kPath[d.mode]].launches += 1;  // images per resample path (fi_kernel_stats)
+    }
     rd_of[i] = (int)rd.size();
     rd.push_back(d);
     if (smc) {
@@ -874,7 +916,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
   // ---- build launches
   std::vector<int> m0, m1, m2;
   for (size_t k = 0; k < rd.size(); k++) {
-    if (rd[k].mode == 3) continue;
+    if (rd[k].mode == 3 || rd[k].mode == 4) continue;
     (rd[k].mode == 0 ? m0 : rd[k].mode == 1 ? m1 : m2).push_back((int)k);
   }
   // fused tiles: (image, column strip, row band); grouped by ring size K
@@ -925,8 +967,109 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       (void)H;
     }
   }
+  // MFMA tiles: (image, strip, band of 16-row blocks); tables placed once per geometry
+  std::vector<MDesc> mdescs;
+  std::vector<MStrip> mstrips;
+  std::vector<MTile> mtiles;
+  size_t mfma_lds = 0;
+  {
+    auto align4 = [&]() {
+      while (E.ai.size() % 4) E.ai.push_back(0);
+    };
+    auto put = [&](const std::vector<int32_t> &v) {
+      const int32_t o = (int32_t)E.ai.size();
+      E.ai.insert(E.ai.end(), v.begin(), v.end());
+      return o;
+    };
+    std::map<const MfmaV *, std::array<int32_t, 5>> vplaced;
+    std::map<const MfmaH *, std::pair<int32_t, int32_t>> hplaced;  // first strip, hwsum
+    std::vector<std::array<int32_t, 3>> mpairs;                       // (image, strip, mfma index)
+    const int nm = (int)mfma_img.size();
+    for (int q = 0; q < nm; q++) {
+      const ResizeDesc &d = rd[mfma_img[q]];
+      const MfmaV &V = *mfma_v[q];
+      const MfmaH &H = *mfma_h[q];
+      auto vp = vplaced.find(&V);
+      if (vp == vplaced.end()) {
+        std::array<int32_t, 5> o;
+        o[0] = put(V.rows);
+        o[1] = put(V.ya);
+        o[2] = put(V.yn);
+        o[4] = put(V.wsum);
+        align4();
+        o[3] = put(V.frag);
+        vp = vplaced.emplace(&V, o).first;
+      }
+      auto hp = hplaced.find(&H);
+      if (hp == hplaced.end()) {
+        const int32_t first = (int32_t)mstrips.size();
+        const int32_t hw = put(H.wsum);
+        align4();
+        const int32_t frag = put(H.frag);
+        const int32_t s0 = put(H.s0);
+        const int32_t lut = put(H.lut);
+        for (const MfmaStrip &st : H.strips) {
+          MStrip m{};
+          m.x0 = st.x0;
+          m.x1 = st.x1;
+          m.b0 = st.b0;
+          m.nbytes = st.nbytes;
+          m.c_lo = st.c_lo;
+          m.ncols = st.ncols;
+          m.pitch = st.pitch;
+          m.nocb = st.nocb;
+          m.ks = st.ks;
+          m.lut_px0 = st.lut_px0;
+          m.lut_n = st.lut_n;
+          m.frag = frag + (int32_t)st.frag;
+          m.s0 = s0 + (int32_t)st.s0;
+          m.lut = lut + (int32_t)st.lut;
+          mstrips.push_back(m);
+        }
+        hp = hplaced.emplace(&H, std::make_pair(first, hw)).first;
+      }
+      MDesc m{};
+      m.src = d.src;
+      m.src_stride = d.src_stride;
+      m.dst = d.dst;
+      m.dst_stride = d.dst_stride;
+      m.ew = d.ew;
+      m.eh = d.eh;
+      m.rot = d.rot;
+      m.gray = d.gray;
+      m.rows = vp->second[0];
+      m.ya = vp->second[1];
+      m.yn = vp->second[2];
+      m.row0 = V.rows.empty() ? 0 : V.rows[0];
+      m.rstep = V.rows.size() > 1 ? V.rows[1] - V.rows[0] : 1;
+      for (size_t k = 1; k < V.rows.size() && m.rstep > 0; k++)
+        if (V.rows[k] != m.row0 + m.rstep * (int32_t)k) m.rstep = 0;
+      m.vfrag = vp->second[3];
+      m.vwsum = vp->second[4];
+      m.ks = V.ks;
+      m.hwsum = hp->second.second;
+      const int32_t img = (int32_t)mdescs.size();
+      mdescs.push_back(m);
+      for (int k = 0; k < (int)H.strips.size(); k++) mpairs.push_back({img, hp->second.first + k, q});
+    }
+    // one workgroup per (image, strip), looping over its 16-row blocks; bands of
+    // blocks only when the batch is too small to fill the chip
+    const int np = (int)mpairs.size();
+    for (int j = 0; j < np; j++) {
+      const MfmaV &V = *mfma_v[mpairs[j][2]];
+      int bands = (2048 + np - 1) / std::max(np, 1);
+      bands = std::max(1, std::min(bands, V.nyb));
+      for (int bnd = 0; bnd < bands; bnd++) {
+        const int yb0 = (int)((int64_t)V.nyb * bnd / bands), yb1 = (int)((int64_t)V.nyb * (bnd + 1) / bands);
+        if (yb1 <= yb0) continue;
+        mtiles.push_back(MTile{mpairs[j][0], mpairs[j][1], yb0, yb1});
+        mfma_lds = std::max(mfma_lds, mfma_lds_bytes(yb1 - yb0));
+      }
+    }
+  }
   Blob &B = E.blob;
   const size_t all_rd_off = B.addv(rd);
+  const size_t mdesc_off = B.addv(mdescs), mstrip_off = B.addv(mstrips), mtile_off = B.addv(mtiles);
   for (auto &g : fgroups) g.second.off = B.addv(g.second.tiles);
   auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
   auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
@@ -984,6 +1127,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       if (L0.tiles)
         hipLaunchKernelGGL(k_rs_copy, dim3(L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L0),
                            pre_p(L0), L0.n);
+      if (!mtiles.empty() &&
+          launch_mfma(c->stream, (const MDesc *)(ab + mdesc_off), (const MStrip *)(ab + mstrip_off),
+                      (const MTile *)(ab + mtile_off), (int)mtiles.size(), ai, mfma_lds) != 0)
+        return set_err(FI_EDEVICE, "MFMA resample launch rejected (LDS %zu)", mfma_lds);
       for (auto &g : fgroups) {
         const FusedGroup &G = g.second;
         if (G.tiles.empty()) continue;
@@ -1189,6 +1336,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   fi_ctx *c = new fi_ctx();
   c->device = device;
   if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
+  if (const char *e = getenv("FI_ENABLE_MFMA_RS")) c->mfma_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_MFMA")) c->sc_mfma = !(e[0] == '1');
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

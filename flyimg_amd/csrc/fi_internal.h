@@ -135,6 +135,32 @@ __host__ __device__ inline int mfma_i8_k(int l, int j) {
   return j < 8 ? 8 * (l >> 4) + j : 32 + 8 * (l >> 4) + (j - 8);
 #endif
 }
+// k_rs_mfma (fi_mfma.hip): exact-integer MFMA resample, vertical first.
+struct MDesc {                // one image
+  const uint8_t *src;
+  int64_t src_stride;
+  uint8_t *dst;
+  int64_t dst_stride;
+  int32_t ew, eh, rot, gray;
+  int32_t rows, ya, yn, vfrag, vwsum;  // arena offsets (int32 units) of the MfmaV tables
+  int32_t ks;                          // vertical k-steps (1 or 2)
+  int32_t hwsum;                       // arena offset of the horizontal per-px weight sums
+  int32_t row0, rstep;                 // rstep > 0: touched rows are row0 + rstep * k (no list lookup)
+};
+struct MStrip {               // one column strip (fi_plan.h MfmaStrip) placed in the arena
+  int32_t x0, x1, b0, nbytes;
+  int32_t c_lo, ncols, pitch, nocb, ks;
+  int32_t lut_px0, lut_n;
+  int32_t frag, s0, lut;      // arena offsets (int32 units; frag 16-B aligned)
+};
+struct MTile {                // one workgroup: image x strip x band [yb0, yb1) of 16-row blocks
+  int32_t img, strip, yb0, yb1;
+};
+constexpr int kMfmaThreads = 256;  // 4 waves; three workgroups per CU overlap their phases
+// LDS plane pitch of k_rs_mfma (bytes): fixed so row offsets are instruction
+// immediates; = 8 (mod 32) spreads rows 4 apart over the banks.
+constexpr int kMfmaPitch = 232;
+
 // k_sc_hmfma (fi_smartcrop.hip): Pillow's horizontal pass as exact integer
 // MFMA.  Per 16-column output block b: source window [s0(b), s0(b) + 64 KS),
 // coefficient limbs L0 + 256 L1 + 65536 L2 (signed i8) in fragment order;

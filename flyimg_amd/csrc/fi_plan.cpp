@@ -11,6 +11,8 @@
 #include "fi_plan.h"
 
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -250,6 +252,174 @@ void build_axis(int filter, double factor, int in_sampled, int out_size, int o0,
       if (t->w[t->woff[o] + j] != 0.0f) used[t->start[o] + j - t->src_lo] = 1;
   t->touched = 0;
   for (uint8_t u : used) t->touched += u;
+}
+
+// ---------------------------------------------------------------------------
+// MFMA resample tables
+// ---------------------------------------------------------------------------
+static void limbs3(int32_t k, int32_t l[3]) {
+  l[0] = ((k + 128) & 255) - 128;
+  const int32_t k1 = (k - l[0]) / 256;
+  l[1] = ((k1 + 128) & 255) - 128;
+  l[2] = (k1 - l[1]) / 256;
+}
+static int32_t quant_w(float w) { return (int32_t)lrint((double)w * (double)(1 << kMfmaWBits)); }
+
+// touched indices (non-zero weight) of an axis, ascending, and their list index
+static void touched_list(const AxisTable &t, std::vector<int32_t> *list, std::vector<int32_t> *idx) {
+  const int span = std::max(t.src_hi - t.src_lo, 0);
+  idx->assign(span, -1);
+  for (size_t o = 0; o < t.start.size(); o++)
+    for (int j = 0; j < t.count[o]; j++)
+      if (t.w[t.woff[o] + j] != 0.0f) (*idx)[t.start[o] + j - t.src_lo] = 1;
+  list->clear();
+  for (int r = 0; r < span; r++)
+    if ((*idx)[r] >= 0) {
+      (*idx)[r] = (int32_t)list->size();
+      list->push_back(t.src_lo + r);
+    }
+}
+// list-index range [lo, hi] of output o's non-zero taps (lo > hi: none)
+static void tap_range(const AxisTable &t, const std::vector<int32_t> &idx, int o, int *lo, int *hi) {
+  *lo = 1 << 30;
+  *hi = -1;
+  for (int j = 0; j < t.count[o]; j++)
+    if (t.w[t.woff[o] + j] != 0.0f) {
+      const int li = idx[t.start[o] + j - t.src_lo];
+      *lo = std::min(*lo, li);
+      *hi = std::max(*hi, li);
+    }
+}
+// quantized weight of output o at list index li (0 if not a tap)
+static int32_t tap_w(const AxisTable &t, const std::vector<int32_t> &list, int o, int li) {
+  if (li < 0 || li >= (int)list.size()) return 0;
+  const int j = list[li] - t.start[o];
+  if (j < 0 || j >= t.count[o]) return 0;
+  return quant_w(t.w[t.woff[o] + j]);
+}
+static void put_frag(std::vector<int32_t> &frag, size_t base, int lane, int j, const int32_t limb[3]) {
+  for (int q = 0; q < 3; q++)
+    reinterpret_cast<uint8_t *>(&frag[base + (size_t)q * 256])[lane * 16 + j] = (uint8_t)(int8_t)limb[q];
+}
+
+bool build_mfma_v(const AxisTable &v, MfmaV *m) {
+  *m = MfmaV();
+  const int ny = (int)v.start.size();
+  if (ny == 0) return false;
+  std::vector<int32_t> idx;
+  touched_list(v, &m->rows, &idx);
+  m->nyb = (ny + 15) / 16;
+  m->ya.assign(m->nyb, 0);
+  m->yn.assign(m->nyb, 0);
+  int ks = 1;
+  for (int b = 0; b < m->nyb; b++) {
+    int lo = 1 << 30, hi = -1;
+    for (int y = 16 * b; y < std::min(ny, 16 * b + 16); y++) {
+      int a, e;
+      tap_range(v, idx, y, &a, &e);
+      lo = std::min(lo, a);
+      hi = std::max(hi, e);
+    }
+    if (hi < lo) continue;
+    m->ya[b] = lo;
+    m->yn[b] = hi - lo + 1;
+    ks = std::max(ks, (m->yn[b] + 63) / 64);
+  }
+  if (ks > 2) return false;
+  m->ks = ks;
+  m->wsum.assign((size_t)16 * m->nyb, 0);
+  for (int y = 0; y < ny; y++)
+    for (int j = 0; j < v.count[y]; j++) m->wsum[y] += quant_w(v.w[v.woff[y] + j]);
+  m->frag.assign((size_t)m->nyb * ks * 3 * 256, 0);
+  for (int b = 0; b < m->nyb; b++)
+    for (int t = 0; t < ks; t++)
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int y = 16 * b + (l & 15), li = m->ya[b] + 64 * t + mfma_i8_k(l, j);
+          int32_t limb[3];
+          limbs3(y < ny && li < m->ya[b] + m->yn[b] ? tap_w(v, m->rows, y, li) : 0, limb);
+          put_frag(m->frag, (size_t)(b * ks + t) * 3 * 256, l, j, limb);
+        }
+  return true;
+}
+
+bool build_mfma_h(const AxisTable &h, MfmaH *m) {
+  *m = MfmaH();
+  const int nx = (int)h.start.size();
+  if (nx == 0) return false;
+  std::vector<int32_t> idx;
+  touched_list(h, &m->cols, &idx);
+  std::vector<int32_t> lo(nx), hi(nx);
+  for (int x = 0; x < nx; x++) {
+    tap_range(h, idx, x, &lo[x], &hi[x]);
+    if (hi[x] < lo[x]) return false;  // an output px without taps
+    if (x > 0 && (lo[x] < lo[x - 1] || hi[x] < hi[x - 1])) return false;  // not monotone
+  }
+  m->wsum.assign(nx, 0);
+  for (int x = 0; x < nx; x++)
+    for (int j = 0; j < h.count[x]; j++) m->wsum[x] += quant_w(h.w[h.woff[x] + j]);
+  auto bytes_of = [&](int x0, int x1, int *b0) {
+    *b0 = (3 * m->cols[lo[x0]]) / 16 * 16;
+    const int be = (3 * (m->cols[hi[x1 - 1]] + 1) + 15) / 16 * 16;
+    return be - *b0;
+  };
+  for (int x0 = 0; x0 < nx;) {
+    int x1 = x0 + 1, b0;
+    if (bytes_of(x0, x1, &b0) > kMfmaStripBytes) return false;
+    while (x1 < nx && x1 - x0 < kMfmaMaxNx && bytes_of(x0, x1 + 1, &b0) <= kMfmaStripBytes) x1++;
+    MfmaStrip S{};
+    S.x0 = x0;
+    S.x1 = x1;
+    S.nbytes = bytes_of(x0, x1, &S.b0);
+    S.c_lo = lo[x0];
+    S.ncols = hi[x1 - 1] + 1 - S.c_lo;
+    S.nocb = (x1 - x0 + 15) / 16;
+    S.ks = 1;
+    S.s0 = m->s0.size();
+    // per 16-px output block: window start (8-B aligned for the two 8-byte
+    // fragment reads) and its own k-steps; s0 holds (w0, ks) pairs
+    int pitch = S.ncols;
+    for (int ob = 0; ob < S.nocb; ob++) {
+      const int xa = x0 + 16 * ob, xb = std::min(x1, xa + 16);
+      const int w0 = (lo[xa] - S.c_lo) / 8 * 8;
+      const int ks = (hi[xb - 1] - S.c_lo + 1 - w0 + 63) / 64;
+      S.ks = std::max(S.ks, ks);
+      m->s0.push_back(w0);
+      m->s0.push_back(ks);
+      pitch = std::max(pitch, w0 + 64 * ks);
+    }
+    if (S.ks > 2) return false;
+    // plane pitch = 8 (mod 32) bytes: the fold's byte writes of rows 4 apart and the
+    // fragment reads of rows 1 apart spread over the LDS banks
+    S.pitch = pitch + ((8 - pitch % 32) + 32) % 32;
+    if (getenv("FI_DEBUG_MFMA_PITCH")) fprintf(stderr, "strip %d..%d ncols %d pitch %d\n", x0, x1, S.ncols, S.pitch);
+    if (S.pitch > kMfmaPitch) return false;
+    S.pitch = kMfmaPitch;
+    S.lut_px0 = S.b0 / 3;
+    S.lut_n = (S.b0 + S.nbytes + 2) / 3 - S.lut_px0;
+    S.lut = m->lut.size();
+    for (int k = 0; k < S.lut_n; k++) {
+      const int px = S.lut_px0 + k;
+      int ci = -1;
+      if (px >= h.src_lo && px < h.src_hi && idx[px - h.src_lo] >= 0) ci = idx[px - h.src_lo] - S.c_lo;
+      m->lut.push_back(ci >= 0 && ci < S.ncols ? ci : -1);
+    }
+    S.frag = m->frag.size();
+    m->frag.resize(m->frag.size() + (size_t)S.nocb * S.ks * 3 * 256, 0);
+    for (int ob = 0; ob < S.nocb; ob++)
+      for (int t = 0; t < S.ks; t++)
+        for (int l = 0; l < 64; l++)
+          for (int j = 0; j < 16; j++) {
+            const int x = x0 + 16 * ob + (l & 15);
+            const int li = S.c_lo + m->s0[S.s0 + 2 * ob] + 64 * t + mfma_i8_k(l, j);
+            int32_t limb[3];
+            limbs3(x < x1 ? tap_w(h, m->cols, x, li) : 0, limb);
+            put_frag(m->frag, S.frag + (size_t)(ob * S.ks + t) * 3 * 256, l, j, limb);
+          }
+    m->strips.push_back(S);
+    x0 = x1;
+  }
+  return true;
 }
 
 bool build_ring(const AxisTable &v, RingTable *rt) {

@@ -52,6 +52,37 @@ struct RingTable {
 // active on one source row, or a non-monotone tap layout).
 bool build_ring(const AxisTable &v, RingTable *rt);
 
+// Exact-integer MFMA resample tables (k_rs_mfma, fi_mfma.hip).  Weights are
+// quantized to W = rint(w * 2^kMfmaWBits) and split into three signed-byte
+// limbs; fragments are in the v_mfma_i32_16x16x64_i8 lane order
+// (fi_internal.h mfma_i8_k), 256 int32 (1 KB) each.
+constexpr int kMfmaWBits = 22;
+constexpr int kMfmaStripBytes = 512;   // source bytes per column strip
+constexpr int kMfmaMaxNx = 168;        // output px per strip (out tile aliases the wave tiles)
+struct MfmaV {                         // vertical pass over the touched-row list
+  std::vector<int32_t> rows;           // touched source rows, ascending
+  int nyb = 0, ks = 0;                 // blocks of 16 output rows; k-steps of 64 list rows
+  std::vector<int32_t> ya, yn;         // [nyb] window start (list index), window rows
+  std::vector<int32_t> frag;           // [nyb][ks][3] A fragments (weights)
+  std::vector<int32_t> wsum;           // [16 nyb] sum of quantized weights per output row
+};
+bool build_mfma_v(const AxisTable &v, MfmaV *m);
+struct MfmaStrip {                     // one column strip of the horizontal pass
+  int32_t x0, x1;                      // output px [x0, x1)
+  int32_t b0, nbytes;                  // source bytes loaded (16-B aligned)
+  int32_t c_lo, ncols, pitch;          // compacted touched columns of the strip, LDS plane pitch
+  int32_t nocb, ks;                    // 16-px output blocks, k-steps of 64 columns
+  int32_t lut_px0, lut_n;              // px -> compact column LUT over [lut_px0, lut_px0 + lut_n)
+  size_t frag, s0, lut;                // offsets into MfmaH::frag / s0 / lut
+};
+struct MfmaH {
+  std::vector<int32_t> cols;           // touched source columns, ascending
+  std::vector<MfmaStrip> strips;
+  std::vector<int32_t> frag, s0, lut;  // B fragments [strip][nocb][ks][3]; (w0, ks) per block; LUTs
+  std::vector<int32_t> wsum;           // [ew] sum of quantized weights per output px
+};
+bool build_mfma_h(const AxisTable &h, MfmaH *m);
+
 // Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)
 // to `out_size`; taps mapped back to the `in_src` source indices through the
 // SampleImage offsets (identity when !sample) and merged.

@@ -1,0 +1,228 @@
+// CPU check of the k_rs_mfma / k_sc_hmfma host tables (fi_plan.cpp): the
+// weight matrices rebuilt from the fragment bytes through mfma_i8_k must give,
+// with the kernel's integer algebra, exactly sum(quant(w) * p) for every
+// output -- for the vertical pass over the touched-row list, the horizontal
+// pass over each strip's compacted columns (plus the px -> column LUT and
+// byte ranges), and the Pillow horizontal pass (exact int32 of Resample.c).
+// Built and run by tests/test_native_cpu.py (hipcc, host only).
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <random>
+#include <vector>
+
+#include "../../flyimg_amd/csrc/fi_plan.h"
+
+using namespace fi;
+
+static int g_fail = 0;
+#define CHECK(c, ...)                 \
+  do {                                \
+    if (!(c)) {                       \
+      if (g_fail < 20) {              \
+        printf("FAIL %s:%d ", __FILE__, __LINE__); \
+        printf(__VA_ARGS__);          \
+        printf("\n");                 \
+      }                               \
+      g_fail++;                       \
+    }                                 \
+  } while (0)
+
+static int32_t qw(float w) { return (int32_t)lrint((double)w * (double)(1 << kMfmaWBits)); }
+static int8_t frag_byte(const std::vector<int32_t> &f, size_t base, int q, int lane, int j) {
+  return (int8_t)reinterpret_cast<const uint8_t *>(&f[base + (size_t)q * 256])[lane * 16 + j];
+}
+static int64_t limb_w(const std::vector<int32_t> &f, size_t base, int lane, int j) {
+  return (int64_t)frag_byte(f, base, 0, lane, j) + 256 * (int64_t)frag_byte(f, base, 1, lane, j) +
+         65536 * (int64_t)frag_byte(f, base, 2, lane, j);
+}
+
+static bool g_required = false;  // the geometry must take the MFMA path
+static void check_v(const AxisTable &v, const char *name) {
+  MfmaV m;
+  if (!build_mfma_v(v, &m)) {
+    printf("  %s: vertical tables not built (ks > 2), skipped\n", name);
+    CHECK(!g_required, "%s: vertical MFMA tables required", name);
+    return;
+  }
+  const int ny = (int)v.start.size();
+  std::mt19937 rng(1234);
+  const int H = v.src_hi;
+  std::vector<int> p(H);
+  for (auto &x : p) x = (int)(rng() & 255);
+  for (int b = 0; b < m.nyb; b++) {
+    // W[m][k] over the block's k-steps
+    std::vector<int64_t> W((size_t)16 * 64 * m.ks, 0);
+    for (int t = 0; t < m.ks; t++)
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++)
+          W[(size_t)(l & 15) * 64 * m.ks + 64 * t + mfma_i8_k(l, j)] =
+              limb_w(m.frag, (size_t)(b * m.ks + t) * 3 * 256, l, j);
+    for (int r = 0; r < 16; r++) {
+      const int y = 16 * b + r;
+      if (y >= ny) continue;
+      int64_t s = 0;  // kernel: sum W (p - 128) + 128 wsum
+      for (int k = 0; k < 64 * m.ks; k++) {
+        const int64_t w = W[(size_t)r * 64 * m.ks + k];
+        if (k >= m.yn[b]) {
+          CHECK(w == 0, "%s: weight beyond the window y=%d k=%d", name, y, k);
+          continue;
+        }
+        s += w * (p[m.rows[m.ya[b] + k]] - 128);
+      }
+      s += 128 * (int64_t)m.wsum[y];
+      int64_t ref = 0;
+      for (int j = 0; j < v.count[y]; j++) ref += (int64_t)qw(v.w[v.woff[y] + j]) * p[v.start[y] + j];
+      CHECK(s == ref, "%s: vertical y=%d %lld != %lld", name, y, (long long)s, (long long)ref);
+      CHECK(llabs(s) < (1ll << 31), "%s: vertical sum exceeds int32", name);
+    }
+  }
+  printf("  %s: vertical %d blocks ks=%d rows=%zu ok\n", name, m.nyb, m.ks, m.rows.size());
+}
+
+static void check_h(const AxisTable &h, const char *name) {
+  MfmaH m;
+  if (!build_mfma_h(h, &m)) {
+    printf("  %s: horizontal tables not built, skipped\n", name);
+    CHECK(!g_required, "%s: horizontal MFMA tables required", name);
+    return;
+  }
+  const int nx = (int)h.start.size();
+  std::mt19937 rng(99);
+  std::vector<int> V(h.src_hi);
+  for (auto &x : V) x = (int)(rng() % 65536);
+  int covered = 0;
+  for (const MfmaStrip &S : m.strips) {
+    CHECK(S.b0 % 16 == 0 && S.nbytes % 16 == 0 && S.nbytes <= kMfmaStripBytes, "%s: strip bytes", name);
+    // compact column c (relative) -> source px, through the LUT
+    std::vector<int> colpx(S.pitch, -1);
+    for (int k = 0; k < S.lut_n; k++) {
+      const int ci = m.lut[S.lut + k];
+      if (ci < 0) continue;
+      const int px = S.lut_px0 + k;
+      CHECK(3 * px >= S.b0 && 3 * px + 3 <= S.b0 + S.nbytes, "%s: px %d outside strip bytes", name, px);
+      CHECK(ci < S.ncols && colpx[ci] < 0, "%s: LUT column %d", name, ci);
+      if (ci < S.ncols) colpx[ci] = px;
+    }
+    for (int c = 0; c < S.ncols; c++) CHECK(colpx[c] == m.cols[S.c_lo + c], "%s: column %d not mapped", name, c);
+    for (int ob = 0; ob < S.nocb; ob++) {
+      const int w0 = m.s0[S.s0 + 2 * ob], ksob = m.s0[S.s0 + 2 * ob + 1];
+      CHECK(w0 % 8 == 0 && ksob >= 1 && ksob <= S.ks && w0 + 64 * ksob <= S.pitch, "%s: window", name);
+      for (int t = ksob; t < S.ks; t++)
+        for (int l = 0; l < 64; l++)
+          for (int j = 0; j < 16; j++)
+            CHECK(limb_w(m.frag, S.frag + (size_t)(ob * S.ks + t) * 3 * 256, l, j) == 0, "%s: weight past ks", name);
+      std::vector<int64_t> W((size_t)16 * 64 * S.ks, 0);
+      for (int t = 0; t < S.ks; t++)
+        for (int l = 0; l < 64; l++)
+          for (int j = 0; j < 16; j++)
+            W[(size_t)(l & 15) * 64 * S.ks + 64 * t + mfma_i8_k(l, j)] =
+                limb_w(m.frag, S.frag + (size_t)(ob * S.ks + t) * 3 * 256, l, j);
+      for (int n = 0; n < 16; n++) {
+        const int x = S.x0 + 16 * ob + n;
+        if (x >= S.x1) continue;
+        covered++;
+        // kernel: 256 sum W (Vh - 128) + sum W (Vl - 128) + 32896 wsum
+        int64_t sh = 0, sl = 0;
+        for (int k = 0; k < 64 * S.ks; k++) {
+          const int64_t w = W[(size_t)n * 64 * S.ks + k];
+          const int c = w0 + k;
+          if (w == 0) continue;
+          CHECK(c < S.ncols, "%s: weight on padding column", name);
+          const int v = V[colpx[c]];
+          sh += w * ((v >> 8) - 128);
+          sl += w * ((v & 255) - 128);
+        }
+        const int64_t s = 256 * sh + sl + 32896 * (int64_t)m.wsum[x];
+        int64_t ref = 0;
+        for (int j = 0; j < h.count[x]; j++) ref += (int64_t)qw(h.w[h.woff[x] + j]) * V[h.start[x] + j];
+        CHECK(s == ref, "%s: horizontal x=%d %lld != %lld", name, x, (long long)s, (long long)ref);
+        CHECK(llabs(sh) < (1ll << 31) && llabs(sl) < (1ll << 31), "%s: horizontal limb sum exceeds int32", name);
+      }
+    }
+  }
+  CHECK(covered == nx, "%s: strips cover %d of %d px", name, covered, nx);
+  printf("  %s: horizontal %zu strips ok\n", name, m.strips.size());
+}
+
+static void check_pillow(int W, int H, int tw, int th, const char *name) {
+  fi_smartcrop_options o;
+  o.prescale = 1;
+  o.max_scale = 1;
+  o.min_scale = 0.9;
+  o.scale_step = 0.1;
+  o.step = 8;
+  o.exact_all = 0;
+  ScPlan p;
+  if (plan_sc(W, H, tw, th, o, &p) != FI_OK || !p.hm_ok) {
+    printf("  %s: no MFMA prescale plan, skipped\n", name);
+    return;
+  }
+  std::mt19937 rng(5);
+  const int sw = p.rw;
+  std::vector<int> px(sw);
+  for (auto &x : px) x = (int)(rng() & 255);
+  for (int b = 0; b < p.hm_nb; b++)
+    for (int n = 0; n < 16; n++) {
+      const int x = 16 * b + n;
+      if (x >= p.aw) continue;
+      int64_t s = p.hmC[x];
+      for (int t = 0; t < p.hm_ks; t++)
+        for (int l = 0; l < 64; l++) {
+          if ((l & 15) != n) continue;
+          for (int j = 0; j < 16; j++) {
+            const int col = p.hmS0[b] + 64 * t + mfma_i8_k(l, j);
+            const int64_t w = limb_w(p.hmB, (size_t)((b * p.hm_ks + t) * 3) * 256, l, j);
+            if (w == 0) continue;
+            CHECK(col < sw, "%s: Pillow weight beyond the row", name);
+            s += w * (px[col] - 128);
+          }
+        }
+      int64_t ref = 1 << 21;
+      for (int j = 0; j < p.hb[2 * x + 1]; j++) ref += (int64_t)p.hk[(size_t)x * p.ksh + j] * px[p.hb[2 * x] + j];
+      CHECK(s == ref, "%s: Pillow x=%d %lld != %lld", name, x, (long long)s, (long long)ref);
+    }
+  printf("  %s: Pillow horizontal %d blocks ok\n", name, p.hm_nb);
+}
+
+static void geometry(int W, int H, int tw, int th, uint32_t flags, const char *name) {
+  fi_image im{};
+  im.src_w = W;
+  im.src_h = H;
+  im.src_stride = W * 3;
+  im.src_channels = 3;
+  im.target_w = tw;
+  im.target_h = th;
+  im.flags = flags;
+  ImPlan P;
+  if (plan_im(im, &P) != FI_OK || !P.resize) {
+    printf("  %s: no resize\n", name);
+    return;
+  }
+  AxisTable v, h;
+  build_axis(P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &v);
+  build_axis(P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &h);
+  check_v(v, name);
+  check_h(h, name);
+}
+
+int main() {
+  const uint32_t T = FI_OP_THUMBNAIL, F = FI_GEOM_FILL, X = FI_OP_EXTENT, S = FI_GEOM_SHRINK_ONLY;
+  g_required = true;  // the BASELINE configurations run on the MFMA kernel
+  geometry(1920, 1080, 500, 0, T | S, "cfg2 1920x1080 w_500");
+  geometry(3840, 2160, 512, 512, T | F | X, "cfg3 3840x2160 512x512 c_1");
+  geometry(6000, 4000, 400, 400, T | F | X, "cfg5 6000x4000 400x400 c_1");
+  geometry(3000, 2000, 300, 250, T | F | X, "cfg1 3000x2000 300x250 c_1");
+  g_required = false;
+  geometry(1200, 800, 400, 400, T | F | X, "1200x800 400x400 c_1");
+  geometry(300, 200, 150, 100, T | S, "300x200 -> 150");
+  geometry(900, 600, 250, 300, FI_OP_RESIZE | F | X, "resize 900x600 250x300");
+  geometry(120, 90, 300, 0, T, "enlarge 120x90 -> 300");
+  check_pillow(500, 281, 100, 100, "smartcrop 500x281");
+  check_pillow(400, 400, 100, 100, "smartcrop 400x400");
+  check_pillow(512, 512, 100, 100, "smartcrop 512x512");
+  check_pillow(1000, 750, 100, 100, "smartcrop 1000x750 (reduce)");
+  printf("%s (%d failures)\n", g_fail ? "FAILED" : "OK", g_fail);
+  return g_fail ? 1 : 0;
+}

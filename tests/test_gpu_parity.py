@@ -44,22 +44,47 @@ def _context_with(env):
                 os.environ[k] = v
 
 
+_ENV = {"FI_DISABLE_FUSED": "0", "FI_ENABLE_MFMA_RS": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0"}
 PATHS = {
-    # default kernels: fused resample; MFMA horizontal prescale, k_sc_vmaps, k_sc_score2
-    "fused": {"FI_DISABLE_FUSED": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0"},
-    # generic kernels: two-pass resample, per-row prescale/maps kernels
-    "generic": {"FI_DISABLE_FUSED": "1", "FI_DISABLE_SC_PREP": "1", "FI_DISABLE_SC_MFMA": "1"},
-    # per-image prescale with the VALU horizontal pass (k_sc_hrows)
-    "valu_h": {"FI_DISABLE_FUSED": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "1"},
+    # default kernels: k_rs_fused resample; k_sc_hmfma + k_sc_vmaps prescale; k_sc_score2
+    "valu": dict(_ENV),
+    # exact-integer MFMA resample (opt-in) with the VALU horizontal prescale (k_sc_hrows)
+    "mfma": dict(_ENV, FI_ENABLE_MFMA_RS="1", FI_DISABLE_SC_MFMA="1"),
+    # generic kernels: two-pass resample; per-row prescale/maps kernels
+    "generic": dict(_ENV, FI_DISABLE_FUSED="1", FI_DISABLE_SC_PREP="1", FI_DISABLE_SC_MFMA="1"),
 }
 
 
-@pytest.fixture(scope="module", params=["fused", "generic"])
+@pytest.fixture(scope="module", params=sorted(PATHS))
 def rctx(request):
     """Kernel path under test (environment read at context creation)."""
     c = _context_with(PATHS[request.param])
+    c.path_name = request.param
     yield c
     c.close()
+
+
+EXPECTED_PATH = {"mfma": "path_mfma", "valu": "path_fused", "generic": "path_generic_v"}
+
+
+@pytest.mark.parametrize("W,H,opts", [
+    (1920, 1080, "w_500"),                       # cfg2
+    (3840, 2160, "w_512,h_512,c_1"),             # cfg3
+    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray"),  # cfg5
+    (3000, 2000, "w_300,h_250,c_1"),             # cfg1
+])
+def test_baseline_geometries_take_the_path(rctx, W, H, opts):
+    """The BASELINE geometries run on the kernel the path names (no silent
+    fallback to another resample kernel)."""
+    from flyimg_amd.processor import ImageProcessor, OptionsBag
+
+    op = ImageProcessor(OptionsBag(opts), W, H).to_op()
+    src = synth_rgb(W, H, 7)
+    want = EXPECTED_PATH[rctx.path_name]
+    before = rctx.stats(want)[1]
+    outs, recs, rc = rctx.process([src], [op])
+    assert rc == 0 and recs[0].status == 0
+    assert rctx.stats(want)[1] == before + 1, (want, {k: rctx.stats(k)[1] for k in EXPECTED_PATH.values()})
 
 
 @pytest.fixture(scope="module", params=sorted(PATHS))

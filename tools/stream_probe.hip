@@ -76,6 +76,71 @@ __global__ void k_strips(const uint8_t *base, int64_t img_bytes, int64_t stride,
   if (acc == 0x12345678u) sink[0] = acc + lds_pad[0];
 }
 
+// the k_rs_mfma pattern: one WG (8 waves) = (image, 1 KB strip, block of 16
+// output rows) reading a window of WIN rows starting at 61 * block; each wave
+// loads its column chunks of CW bytes (CW / 16 lanes per row, 64 * 16 / CW
+// rows per instruction), 2 chunks... all as k_rs_mfma (no compute)
+template <int CW>
+__global__ __launch_bounds__(512) void k_windows(const uint8_t *base, int64_t img_bytes, int64_t stride,
+                                                 int nstrips, int nblocks, int win, uint32_t *sink) {
+  extern __shared__ uint32_t lds_w[];
+  const int t = blockIdx.x;
+  const int img = t / (nstrips * nblocks), rem = t % (nstrips * nblocks);
+  const int strip = rem / nblocks, blk = rem % nblocks;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int LPR = CW / 16;          // lanes per row
+  constexpr int RPI = 64 / LPR;         // rows per instruction
+  const uint8_t *p = base + img * img_bytes + (int64_t)(61 * blk) * stride + strip * 1024;
+  uint32_t acc = 0;
+  for (int ch = wave; ch < 1024 / CW; ch += 8) {
+    u32x4 v[128 / RPI];
+#pragma unroll
+    for (int i = 0; i < 128 / RPI; i++) {
+      int row = RPI * i + lane / LPR;
+      row = row < win ? row : 0;
+      v[i] = *(g_u32x4 *)(p + (int64_t)row * stride + ch * CW + 16 * (lane % LPR));
+    }
+#pragma unroll
+    for (int i = 0; i < 128 / RPI; i++) acc += v[i].x ^ v[i].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc + lds_w[0];
+}
+
+// k_rs_mfma's loop: one WG per (image, 1 KB strip) walking down its blocks
+// (window WIN rows at 61 * block), a barrier per block, each wave 2 chunks
+// of 64 B; PREF: the next block's first chunk is loaded before the barrier.
+template <int PREF, int BAR>
+__global__ __launch_bounds__(512) void k_loop(const uint8_t *base, int64_t img_bytes, int64_t stride, int nstrips,
+                                              int nblocks, int win, uint32_t *sink) {
+  extern __shared__ uint32_t lds_w[];
+  const int img = blockIdx.x / nstrips, strip = blockIdx.x % nstrips;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint8_t *p0 = base + img * img_bytes + strip * 1024;
+  uint32_t acc = 0;
+  u32x4 v[8];
+  auto issue = [&](int blk, int ch) {
+    const uint8_t *p = p0 + (int64_t)(61 * blk) * stride + ch * 64 + 16 * (lane & 3);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      int row = 16 * i + (lane >> 2);
+      row = row < win ? row : 0;
+      v[i] = *(g_u32x4 *)(p + (int64_t)row * stride);
+    }
+  };
+  if (PREF) issue(0, wave);
+  for (int blk = 0; blk < nblocks; blk++) {
+    for (int u = 0; u < 2; u++) {
+      const int ch = wave + 8 * u;
+      if (!PREF || u == 1) issue(blk, ch);
+#pragma unroll
+      for (int i = 0; i < 8; i++) acc += v[i].x ^ v[i].w;
+      if (PREF && u == 1 && blk + 1 < nblocks) issue(blk + 1, wave);
+    }
+    if (BAR) __syncthreads();
+  }
+  if (acc == 0x12345678u) sink[0] = acc + lds_w[0];
+}
+
 // reference: each WG reads a contiguous chunk (memcpy-like read)
 __global__ void k_linear(const u32x4 *base, int64_t n16, uint32_t *sink) {
   uint32_t acc = 0;
@@ -128,6 +193,32 @@ int main(int argc, char **argv) {
                                                stride, W3, H, ns, sink); }, 5);                           \
     printf("strips LW=%2d D=%2d threads=%4d lds=%2dKB %8.3f ms %8.1f GB/s\n", LW, D, TH, lds_opts[li], ms, \
            gb / ms * 1e3);                                                                               \
+  }
+  {
+    const int nstrips = 5, nblocks = 17, win = 82;  // 5 KB of each row, rows 0 .. 61*16+82
+    const double wgb = (double)nimg * nstrips * nblocks * win * 1024 / 1e9;
+    {
+      const double lgb = (double)nimg * 5 * 17 * win * 1024 / 1e9;  // 5 strips x 17 blocks; rows < 61*16+82 < 1080
+      float a = timeit([&] { hipLaunchKernelGGL((k_loop<0, 1>), dim3(nimg * 5), dim3(512), 78 * 1024, 0, buf, img_bytes, stride, 5, 17, win, sink); }, 5);
+      float b = timeit([&] { hipLaunchKernelGGL((k_loop<1, 1>), dim3(nimg * 5), dim3(512), 78 * 1024, 0, buf, img_bytes, stride, 5, 17, win, sink); }, 5);
+      float c = timeit([&] { hipLaunchKernelGGL((k_loop<1, 0>), dim3(nimg * 5), dim3(512), 78 * 1024, 0, buf, img_bytes, stride, 5, 17, win, sink); }, 5);
+      float d = timeit([&] { hipLaunchKernelGGL((k_loop<1, 1>), dim3(nimg * 5), dim3(512), 0, 0, buf, img_bytes, stride, 5, 17, win, sink); }, 5);
+      printf("loop per strip (%.2f GB req): no-pref+bar %.3f ms | pref+bar %.3f ms | pref no-bar %.3f ms | pref+bar lds0 %.3f ms\n",
+             lgb, a, b, c, d);
+    }
+    for (int kb : {40, 60, 78}) {
+      float m = timeit([&] { hipLaunchKernelGGL(k_windows<64>, dim3(nimg * nstrips * nblocks), dim3(512), kb * 1024, 0, buf,
+                                                img_bytes, stride, nstrips, nblocks, win, sink); }, 5);
+      printf("windows 64 B/row with %d KB LDS: %.3f ms %.0f GB/s\n", kb, m, wgb / m * 1e3);
+    }
+    float ms64 = timeit([&] { hipLaunchKernelGGL(k_windows<64>, dim3(nimg * nstrips * nblocks), dim3(512), 0, 0, buf,
+                                                 img_bytes, stride, nstrips, nblocks, win, sink); }, 5);
+    float ms128 = timeit([&] { hipLaunchKernelGGL(k_windows<128>, dim3(nimg * nstrips * nblocks), dim3(512), 0, 0, buf,
+                                                  img_bytes, stride, nstrips, nblocks, win, sink); }, 5);
+    float ms256 = timeit([&] { hipLaunchKernelGGL(k_windows<256>, dim3(nimg * nstrips * nblocks), dim3(512), 0, 0, buf,
+                                                  img_bytes, stride, nstrips, nblocks, win, sink); }, 5);
+    printf("windows (k_rs_mfma pattern, %.2f GB requested): 64 B/row %.3f ms %.0f GB/s | 128 B/row %.3f ms %.0f GB/s | 256 B/row %.3f ms %.0f GB/s\n",
+           wgb, ms64, wgb / ms64 * 1e3, ms128, wgb / ms128 * 1e3, ms256, wgb / ms256 * 1e3);
   }
   RUN(8, 8, 256);
   RUN(8, 16, 256);
