@@ -3,7 +3,8 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2]
 
-One step = one fi_process_batch_device call over the rank's device-resident
+One step = one batch (fi_submit_batch_device; batch k+1 is planned on the
+host while batch k runs, every batch is finalized inside the timed region) over the rank's device-resident
 batch of synthetic RGB8 images (inputs already in HBM when timing starts):
 ImageMagick-semantics resample -> smartcrop (prescale, maps, scoring, argmax)
 -> crop apply, plus -- for N > 1 -- the RCCL gather of the per-image result
@@ -129,40 +130,56 @@ def main():
     for i in range(nimg):
         ctx.fill_synthetic(pool + i * src_bytes, W, H, src_stride, 0x5EED + rank * nimg + i)
     log(f"rank {rank}: pool {nimg} x {W}x{H} ({src_bytes * nimg / 1e9:.2f} GB) filled in {time.perf_counter() - t0:.1f} s")
-    arr = (L.FiImage * nimg)()
-    for i in range(nimg):
-        a = arr[i]
-        a.src, a.src_w, a.src_h, a.src_stride, a.src_channels = pool + i * src_bytes, W, H, src_stride, 3
-        a.target_w, a.target_h, a.flags, a.gravity, a.rotate = op.target_w, op.target_h, op.flags, op.gravity, op.rotate
-        a.smartcrop_w, a.smartcrop_h = op.smartcrop_w, op.smartcrop_h
-        a.dst, a.dst_capacity = dst + i * dst_cap, dst_cap
+    # two descriptor arrays: batch k+1 is planned and launched while batch k
+    # runs (fi_submit_batch_device); batch k's records are finalized and
+    # gathered once k+1 is queued.
+    arrs = [(L.FiImage * nimg)() for _ in range(2)]
+    for arr in arrs:
+        for i in range(nimg):
+            a = arr[i]
+            a.src, a.src_w, a.src_h, a.src_stride, a.src_channels = pool + i * src_bytes, W, H, src_stride, 3
+            a.target_w, a.target_h, a.flags, a.gravity, a.rotate = op.target_w, op.target_h, op.flags, op.gravity, op.rotate
+            a.smartcrop_w, a.smartcrop_h = op.smartcrop_w, op.smartcrop_h
+            a.dst, a.dst_capacity = dst + i * dst_cap, dst_cap
+    bad = [0]
 
-    def step():
-        L.check(ctx.process_device(arr, nimg))
+    def records(arr):
+        bad[0] += sum(1 for i in range(nimg) if arr[i].status != 0)
         if world > 1:
-            recs = [(rank * nimg + i, arr[i].status, arr[i].out_w, arr[i].out_h, arr[i].crop_x, arr[i].crop_y,
-                     arr[i].crop_w, arr[i].crop_h) for i in range(nimg)]
-            gather.gather(recs)
+            gather.gather([(rank * nimg + i, arr[i].status, arr[i].out_w, arr[i].out_h, arr[i].crop_x,
+                            arr[i].crop_y, arr[i].crop_w, arr[i].crop_h) for i in range(nimg)])
 
-    for _ in range(args.warmup):
-        step()
+    def run(k0, count):
+        """Batches k0..k0+count-1, pipelined; returns after all are finalized."""
+        if count <= 0:
+            return
+        for k in range(k0, k0 + count):
+            L.check(ctx.submit_device(arrs[k % 2], nimg))
+            if k > k0:
+                L.check(ctx.wait(1))  # batch k-1 done (batch k still queued)
+                records(arrs[(k - 1) % 2])
+        L.check(ctx.wait(0))
+        records(arrs[(k0 + count - 1) % 2])
+
+    run(0, args.warmup)
+    bad[0] = 0
     ctx.set_timing(True)
     ctx.reset_stats()
     comm.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()  # synchronous: returns after the stream drained
+    run(args.warmup, args.steps)  # ends with every batch drained (stream idle)
     t1 = time.perf_counter()
     comm.barrier()
     ctx.set_timing(False)
     el = t1 - t0
     stats = {k: ctx.stats(k) for k in ("batch", "resize", "sc_prep", "sc_score", "crop_apply",
-                                      "host_plan", "host_launch", "host_after_sync", "host_total")}
+                                      "host_plan", "host_launch", "host_wait", "host_total")}
     # images per resample kernel over the timed steps (counts kept by the library)
     paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in KERNEL_OF_PATH}
+    last = arrs[(args.warmup + args.steps - 1) % 2]
     allv = comm.allgather_obj({"elapsed": el, "stats": stats,
-                               "ncand": sum(arr[i].n_candidates for i in range(nimg)),
-                               "bad": sum(1 for i in range(nimg) if arr[i].status != 0)})
+                               "ncand": sum(last[i].n_candidates for i in range(nimg)),
+                               "bad": bad[0]})
     if rank == 0:
         T = max(v["elapsed"] for v in allv)
         mpix = world * nimg * W * H * args.steps / 1e6

@@ -130,6 +130,8 @@ def lib():
     L.fi_plan.argtypes = [P(FiImage), i32]
     L.fi_process_batch.argtypes = [vp, P(FiImage), i32]
     L.fi_process_batch_device.argtypes = [vp, P(FiImage), i32]
+    L.fi_submit_batch_device.argtypes = [vp, P(FiImage), i32]
+    L.fi_wait.argtypes = [vp, i32]
     L.fi_smartcrop_default_params.argtypes = [P(FiSmartcropParams)]
     L.fi_smartcrop_default_params.restype = None
     L.fi_smartcrop_default_options.argtypes = [P(FiSmartcropOptions)]

@@ -103,8 +103,39 @@ struct StripTab {
   std::vector<int32_t> starts;  // [nx]
   std::vector<float> wT;        // [htaps][nx]
 };
+// One in-flight batch (fi_submit_batch_device): what fi_wait needs to fill
+// the caller's fi_image records once the stream has drained.
+struct PendingBatch {
+  fi_image *imgs = nullptr;
+  int n = 0;
+  int slot = 0;
+  double t_start = 0;
+  std::vector<int> status, sc_of;
+  std::vector<std::string> errs;
+  std::vector<int> sstatus;
+  std::vector<std::string> serrs;
+  std::vector<int32_t> crop0;   // per smartcrop item: first crop of its list
+  std::vector<fi::DevCrop> crops;
+  size_t nres = 0;              // ScResult records in the slot's pinned readback
+  bool any_apply = false;
+  std::vector<TimedRange> timers;  // this batch's HIP-event ranges
+};
+// Pinned host staging of one in-flight batch: the upload blob and the result
+// readback.  Two slots: batch k+1 is planned and uploaded while batch k runs.
+struct Slot {
+  void *blob = nullptr;
+  size_t blob_cap = 0;
+  void *res = nullptr;
+  size_t res_cap = 0;
+  hipEvent_t done = nullptr;  // recorded after the batch's last readback
+  bool busy = false;
+};
+constexpr int kSlots = 2;
 struct fi_ctx {
   int device = 0;
+  Slot slots[kSlots];
+  int next_slot = 0;
+  std::vector<PendingBatch> inflight;  // submission order
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevBuf arena, work, io;
@@ -132,6 +163,7 @@ struct fi_ctx {
 
 static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
   if (b->cap >= bytes) return FI_OK;
+  (void)hipStreamSynchronize(c->stream);  // in-flight batches may still read it
   if (b->p) (void)hipFree(b->p);
   b->p = nullptr;
   b->cap = 0;
@@ -141,6 +173,19 @@ static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
     return set_err(FI_ENOMEM, "hipMalloc(%zu) failed on device %d", cap, c->device);
   }
   b->cap = cap;
+  return FI_OK;
+}
+static int ensure_pinned_buf(void **p, size_t *cap_io, size_t bytes) {
+  if (*cap_io >= bytes) return FI_OK;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap_io = 0;
+  size_t cap = std::max(bytes + bytes / 4, (size_t)1 << 16);
+  if (hipHostMalloc(p, cap, hipHostMallocDefault) != hipSuccess) {
+    *p = nullptr;
+    return set_err(FI_ENOMEM, "hipHostMalloc(%zu) failed", cap);
+  }
+  *cap_io = cap;
   return FI_OK;
 }
 static int ensure_pinned(fi_ctx *c, size_t bytes) {
@@ -183,8 +228,8 @@ struct Timer {
     c->pending.push_back(r);
   }
 };
-static void collect_timers(fi_ctx *c) {
-  for (auto &r : c->pending) {
+static void collect_ranges(fi_ctx *c, std::vector<TimedRange> &ranges) {
+  for (auto &r : ranges) {
     float ms = 0;
     (void)hipEventSynchronize(r.b);
     (void)hipEventElapsedTime(&ms, r.a, r.b);
@@ -195,8 +240,9 @@ static void collect_timers(fi_ctx *c) {
     c->event_pool.push_back(r.a);
     c->event_pool.push_back(r.b);
   }
-  c->pending.clear();
+  ranges.clear();
 }
+static void collect_timers(fi_ctx *c) { collect_ranges(c, c->pending); }
 
 // ---------------------------------------------------------------------------
 // upload blob
@@ -678,8 +724,9 @@ static void host_stat(fi_ctx *c, const char *name, double ms) {
   s.launches += 1;
 }
 
-static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) {
-  (void)device_ptrs_ok;
+static int drain(fi_ctx *c);
+static int wait_slot(fi_ctx *c, int slot);
+static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   const double t_start = now_ms();
   Exec E;
   E.c = c;
@@ -1102,13 +1149,21 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
   }
   const size_t apply_off = B.addv(apply);
   const size_t ai_off = B.addv(E.ai), af_off = B.addv(E.af), ad_off = B.addv(E.ad);
-  // ---- upload
+  // ---- upload (pinned slot: the previous batch may still be running)
+  const int slot = c->next_slot;
+  rc = wait_slot(c, slot);
+  if (rc) return rc;
+  Slot &S = c->slots[slot];
   rc = ensure(c, &c->arena, B.b.size() + 256);
   if (rc) return rc;
-  rc = ensure_pinned(c, B.b.size() + 256);
+  rc = ensure_pinned_buf(&S.blob, &S.blob_cap, B.b.size() + 256);
   if (rc) return rc;
-  memcpy(c->pinned, B.b.data(), B.b.size());
-  HIP_TRY(hipMemcpyAsync(c->arena.p, c->pinned, B.b.size(), hipMemcpyHostToDevice, c->stream));
+  const size_t res_bytes = sizeof(ScResult) * sitems.size();
+  const size_t outwh_bytes = sizeof(int32_t) * 2 * (size_t)n;
+  rc = ensure_pinned_buf(&S.res, &S.res_cap, res_bytes + outwh_bytes + 64);
+  if (rc) return rc;
+  memcpy(S.blob, B.b.data(), B.b.size());
+  HIP_TRY(hipMemcpyAsync(c->arena.p, S.blob, B.b.size(), hipMemcpyHostToDevice, c->stream));
   const double t_planned = now_ms();
   host_stat(c, "host_plan", t_planned - t_start);
   if (c->timing) c->stats["host_plan"].bytes += (double)B.b.size();
@@ -1164,43 +1219,75 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
       HIP_TRY(hipGetLastError());
     }
   }
-  // ---- results
-  std::vector<ScResult> res(sitems.size());
-  std::vector<int32_t> outwh(2 * (size_t)std::max(n, 1), 0);
+  // ---- results: per-image records into the slot's pinned readback
+  uint8_t *rp = (uint8_t *)S.res;
   if (!sitems.empty())
-    HIP_TRY(hipMemcpyAsync(res.data(), wb + results_off, sizeof(ScResult) * res.size(), hipMemcpyDeviceToHost,
-                           c->stream));
+    HIP_TRY(hipMemcpyAsync(rp, wb + results_off, res_bytes, hipMemcpyDeviceToHost, c->stream));
   if (!apply.empty())
-    HIP_TRY(hipMemcpyAsync(outwh.data(), wb + outwh_off, sizeof(int32_t) * 2 * n, hipMemcpyDeviceToHost, c->stream));
-  const double t_launched = now_ms();
-  host_stat(c, "host_launch", t_launched - t_planned);
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  collect_timers(c);
+    HIP_TRY(hipMemcpyAsync(rp + res_bytes, wb + outwh_off, outwh_bytes, hipMemcpyDeviceToHost, c->stream));
+  if (!S.done) HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(S.done, c->stream));
+  S.busy = true;
+  c->next_slot = (slot + 1) % kSlots;
+  PendingBatch pb;
+  pb.imgs = imgs;
+  pb.n = n;
+  pb.slot = slot;
+  pb.t_start = t_start;
+  pb.status = std::move(status);
+  pb.errs = std::move(errs);
+  pb.sc_of = std::move(sc_of);
+  pb.sstatus = std::move(sstatus);
+  pb.serrs = std::move(serrs);
+  pb.crop0.resize(SL.descs.size());
+  for (size_t k = 0; k < SL.descs.size(); k++) pb.crop0[k] = SL.descs[k].crop0;
+  pb.crops = std::move(SL.crops);
+  pb.nres = sitems.size();
+  pb.any_apply = !apply.empty();
+  pb.timers.swap(c->pending);  // waited for when this batch is finalized
+  c->inflight.push_back(std::move(pb));
+  host_stat(c, "host_launch", now_ms() - t_planned);
+  if (async) return FI_OK;
+  return drain(c);
+}
+
+// Wait for the oldest in-flight batch and fill its fi_image records.
+static int finalize_front(fi_ctx *c) {
+  PendingBatch pb = std::move(c->inflight.front());
+  c->inflight.erase(c->inflight.begin());
+  Slot &S = c->slots[pb.slot];
+  const double t_wait = now_ms();
+  HIP_TRY(hipEventSynchronize(S.done));
+  S.busy = false;
+  collect_ranges(c, pb.timers);
   const double t_done = now_ms();
+  host_stat(c, "host_wait", t_done - t_wait);
+  const ScResult *res = (const ScResult *)S.res;
+  const int32_t *outwh = (const int32_t *)((const uint8_t *)S.res + sizeof(ScResult) * pb.nres);
   int first_bad = FI_OK;
   std::string first_err;
-  for (int i = 0; i < n; i++) {
-    fi_image &im = imgs[i];
+  for (int i = 0; i < pb.n; i++) {
+    fi_image &im = pb.imgs[i];
     im.n_candidates = 0;
-    if (status[i] == FI_OK && sc_of[i] >= 0) {
-      const int k = sc_of[i];
-      if (sstatus[k] != FI_OK) {
-        status[i] = sstatus[k];
-        errs[i] = serrs[k];
+    if (pb.status[i] == FI_OK && pb.sc_of[i] >= 0) {
+      const int k = pb.sc_of[i];
+      if (pb.sstatus[k] != FI_OK) {
+        pb.status[i] = pb.sstatus[k];
+        pb.errs[i] = pb.serrs[k];
       } else {
         const ScResult &r = res[k];
         if (r.top < 0) {
-          status[i] = FI_EUNSUPPORTED;
-          errs[i] = "smartcrop: too many crop windows for the scoring kernel";
+          pb.status[i] = FI_EUNSUPPORTED;
+          pb.errs[i] = "smartcrop: too many crop windows for the scoring kernel";
         } else {
-          const DevCrop &dc = SL.crops[SL.descs[k].crop0 + r.top];
+          const DevCrop &dc = pb.crops[pb.crop0[k] + r.top];
           im.crop_x = dc.rx;
           im.crop_y = dc.ry;
           im.crop_w = dc.rw;
           im.crop_h = dc.rh;
           im.crop_score = r.total;
           im.n_candidates = r.n_candidates;
-          if (im.flags & FI_OP_SMARTCROP_APPLY) {
+          if ((im.flags & FI_OP_SMARTCROP_APPLY) && pb.any_apply) {
             im.out_w = outwh[2 * i];
             im.out_h = outwh[2 * i + 1];
             im.out_stride = im.out_w * im.out_channels;
@@ -1208,16 +1295,33 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool device_ptrs_ok) 
         }
       }
     }
-    im.status = status[i];
-    if (status[i] != FI_OK && first_bad == FI_OK) {
-      first_bad = status[i];
-      first_err = "image " + std::to_string(i) + ": " + errs[i];
+    im.status = pb.status[i];
+    if (pb.status[i] != FI_OK && first_bad == FI_OK) {
+      first_bad = pb.status[i];
+      first_err = "image " + std::to_string(i) + ": " + pb.errs[i];
     }
   }
-  host_stat(c, "host_total", now_ms() - t_start);
-  host_stat(c, "host_after_sync", now_ms() - t_done);
+  host_stat(c, "host_total", now_ms() - pb.t_start);
   if (first_bad != FI_OK) return set_err(first_bad, "%s", first_err.c_str());
   return FI_OK;
+}
+// Finalize every in-flight batch (in order); returns the first error.
+static int drain(fi_ctx *c) {
+  int first = FI_OK;
+  while (!c->inflight.empty()) {
+    const int rc = finalize_front(c);
+    if (rc != FI_OK && first == FI_OK) first = rc;
+  }
+  if (first != FI_OK) return first;  // message of the first failure is in g_err... of the last
+  return FI_OK;
+}
+static int wait_slot(fi_ctx *c, int slot) {
+  int first = FI_OK;
+  while (c->slots[slot].busy && !c->inflight.empty()) {
+    const int rc = finalize_front(c);
+    if (rc != FI_OK && first == FI_OK) first = rc;
+  }
+  return first;
 }
 
 // ---------------------------------------------------------------------------
@@ -1350,11 +1454,17 @@ int fi_create(fi_ctx **out, int32_t device) {
 void fi_destroy(fi_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  (void)drain(c);
   (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
   for (DevBuf *b : {&c->arena, &c->work, &c->io})
     if (b->p) (void)hipFree(b->p);
   if (c->pinned) (void)hipHostFree(c->pinned);
+  for (Slot &sl : c->slots) {
+    if (sl.blob) (void)hipHostFree(sl.blob);
+    if (sl.res) (void)hipHostFree(sl.res);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1384,7 +1494,27 @@ int fi_process_batch_device(fi_ctx *c, fi_image *imgs, int32_t n) {
   if (n == 0) return FI_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device));
+  return run_batch(c, imgs, n, false);
+}
+
+int fi_submit_batch_device(fi_ctx *c, fi_image *imgs, int32_t n) {
+  if (!c || n < 0 || (n > 0 && !imgs)) return set_err(FI_EINVAL, "bad arguments");
+  if (n == 0) return FI_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
   return run_batch(c, imgs, n, true);
+}
+
+int fi_wait(fi_ctx *c, int32_t keep) {
+  if (!c || keep < 0) return set_err(FI_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  int first = FI_OK;
+  while ((int32_t)c->inflight.size() > keep) {
+    const int rc = finalize_front(c);
+    if (rc != FI_OK && first == FI_OK) first = rc;
+  }
+  return first;
 }
 
 int fi_process_batch(fi_ctx *c, fi_image *imgs, int32_t n) {
@@ -1392,6 +1522,10 @@ int fi_process_batch(fi_ctx *c, fi_image *imgs, int32_t n) {
   if (n == 0) return FI_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device));
+  {
+    const int rc0 = drain(c);  // the io buffer may be read by in-flight batches
+    if (rc0) return rc0;
+  }
   // stage host images into device memory with 16-byte aligned rows
   std::vector<fi_image> dev(imgs, imgs + n);
   std::vector<size_t> soff(n), doff(n);
@@ -1422,7 +1556,7 @@ int fi_process_batch(fi_ctx *c, fi_image *imgs, int32_t n) {
     dev[i].src = io + soff[i];
     dev[i].dst = imgs[i].dst ? io + doff[i] : nullptr;
   }
-  rc = run_batch(c, dev.data(), n, true);
+  rc = run_batch(c, dev.data(), n, false);
   for (int i = 0; i < n; i++) {
     fi_image &o = imgs[i];
     const fi_image &d = dev[i];
@@ -1493,8 +1627,10 @@ int fi_smartcrop_ex(fi_ctx *c, const uint8_t *rgb, int32_t w, int32_t h, int32_t
   if (opts) O = *opts;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device));
+  int rc = drain(c);  // io / pinned staging are shared with in-flight batches
+  if (rc) return rc;
   const int64_t dstride = ((int64_t)w * 3 + 15) / 16 * 16;
-  int rc = ensure(c, &c->io, (size_t)dstride * h + 256);
+  rc = ensure(c, &c->io, (size_t)dstride * h + 256);
   if (rc) return rc;
   HIP_TRY(hipMemcpy2DAsync(c->io.p, dstride, rgb, stride, (size_t)w * 3, h, hipMemcpyHostToDevice, c->stream));
   std::vector<CropScore> scores;

@@ -156,6 +156,16 @@ class Context:
         """fi_process_batch_device on a prepared FiImage array (device pointers)."""
         return self._lib.fi_process_batch_device(self.h, arr, n)
 
+    def submit_device(self, arr, n: int) -> int:
+        """fi_submit_batch_device: plan + upload + launch, returns before the GPU
+        finishes; ``arr`` must stay alive until ``wait()``."""
+        return self._lib.fi_submit_batch_device(self.h, arr, n)
+
+    def wait(self, keep: int = 0) -> int:
+        """fi_wait: finalize submitted batches (oldest first) until at most
+        ``keep`` remain in flight, filling their records."""
+        return self._lib.fi_wait(self.h, keep)
+
     # ---- timing ----------------------------------------------------------------
     def set_timing(self, on: bool):
         L.check(self._lib.fi_set_timing(self.h, int(on)))

@@ -157,6 +157,15 @@ int fi_process_batch(fi_ctx *ctx, fi_image *imgs, int32_t n);
 /* Device-resident buffers (src/dst are device pointers on ctx's device).
  * Synchronous; the timed kernels are recorded in fi_kernel_stats. */
 int fi_process_batch_device(fi_ctx *ctx, fi_image *imgs, int32_t n);
+/* Asynchronous form of fi_process_batch_device for pipelined serving: plans,
+ * uploads and launches the batch, then returns; `imgs` must stay valid until
+ * fi_wait().  Batch k+1 is planned on the host while batch k runs on the GPU
+ * (two pinned staging slots; a third submit waits for the oldest batch).
+ * fi_wait(ctx, keep) finalizes submitted batches in order -- fills their
+ * result fields -- until at most `keep` remain in flight (0 = drain all) and
+ * returns the first error. */
+int fi_submit_batch_device(fi_ctx *ctx, fi_image *imgs, int32_t n);
+int fi_wait(fi_ctx *ctx, int32_t keep);
 
 /* smartcrop.py SmartCrop().crop(rgb, target_w, target_h) on host RGB8.
  * out_xywh = top_crop x, y, width, height; *out_score = its total. */

@@ -272,3 +272,54 @@ def test_full_size_pipeline_smartcrop_box_bit_exact(rctx, W, H, opts):
     flags = op.flags
     ref_img = orc.im_convert(src, op.target_w, op.target_h, _oracle_flags(flags), rotate=op.rotate)
     _cmp(resized, ref_img, opts)
+
+
+def test_pipelined_submit_matches_synchronous(ctx):
+    """fi_submit_batch_device x3 + fi_wait (two pinned slots, a third submit
+    waits for the oldest) gives the same pixels and records as the
+    synchronous fi_process_batch_device, batch by batch."""
+    import ctypes
+
+    from flyimg_amd.processor import ImageProcessor, OptionsBag
+    from flyimg_amd.runtime import plan as fi_plan
+
+    W, H, n = 960, 540, 6
+    op = ImageProcessor(OptionsBag("w_300,smc_1"), W, H).to_op()
+    stride = W * 3
+    ow, oh, oc = fi_plan(W, H, op)
+    cap = ow * oh * oc
+    pool = ctx.malloc(stride * H * n)
+    dst = ctx.malloc(cap * n * 4)
+    try:
+        for i in range(n):
+            ctx.fill_synthetic(pool + i * stride * H, W, H, stride, 900 + i)
+
+        def arr_for(b):
+            arr = (L.FiImage * n)()
+            for i in range(n):
+                a = arr[i]
+                a.src, a.src_w, a.src_h, a.src_stride, a.src_channels = pool + i * stride * H, W, H, stride, 3
+                a.target_w, a.target_h, a.flags, a.gravity = op.target_w, op.target_h, op.flags, op.gravity
+                a.dst, a.dst_capacity = dst + (b * n + i) * cap, cap
+            return arr
+
+        sync = arr_for(0)
+        L.check(ctx.process_device(sync, n))
+        ref_px = ctx.d2h(dst, cap * n)
+        arrs = [arr_for(b) for b in (1, 2, 3)]
+        for a in arrs:
+            L.check(ctx.submit_device(a, n))
+        L.check(ctx.wait(0))
+        for b, a in enumerate(arrs, start=1):
+            got = ctx.d2h(dst + b * n * cap, cap * n)
+            for i in range(n):
+                r, g = sync[i], a[i]
+                assert g.status == 0
+                assert (g.crop_x, g.crop_y, g.crop_w, g.crop_h, g.out_w, g.out_h) == \
+                    (r.crop_x, r.crop_y, r.crop_w, r.crop_h, r.out_w, r.out_h)
+                m = r.out_w * r.out_h * oc
+                assert np.array_equal(got[i * cap:i * cap + m], ref_px[i * cap:i * cap + m])
+        assert ctx.wait(0) == 0  # nothing left in flight
+    finally:
+        ctx.free(pool)
+        ctx.free(dst)
