@@ -39,6 +39,7 @@ WORKLOADS = {
 
 
 KERNEL_OF_PATH = {
+    "path_vm": "k_rs_vm (streaming exact-integer MFMA, vertical first)",
     "path_mfma": "k_rs_mfma (exact-integer MFMA, vertical first)",
     "path_fused": "k_rs_fused (VALU, vertical first)",
     "path_generic_v": "k_rs_v_u8 + k_rs_h_final (two-pass)",

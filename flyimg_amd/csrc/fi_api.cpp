@@ -53,6 +53,10 @@ __global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
 size_t mfma_lds_bytes(int nblocks);
 int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const MTile *tiles, int ntiles,
                 const int32_t *ai, size_t lds);
+// streaming exact-integer MFMA resample (fi_vm.hip)
+size_t vm_lds_bytes(int nocb, int ks);
+int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
+              const int32_t *ai, size_t lds);
 int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
                  const int32_t *ai, const float *af, int hw_pitch, int max_taps, int max_nbytes);
 }  // namespace fi
@@ -157,6 +161,9 @@ struct fi_ctx {
   std::map<const AxisTable *, MfmaH> mh_cache;  // ok iff !strips.empty()
   bool fused = true;    // FI_DISABLE_FUSED=1 forces the generic two-pass resample
   bool mfma_rs = false;  // FI_ENABLE_MFMA_RS=1: k_rs_mfma instead of the VALU fused kernel
+  bool vm_rs = true;     // FI_DISABLE_VM_RS=1: no k_rs_vm (streaming MFMA resample, the default)
+  std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
+  std::map<const AxisTable *, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
   bool sc_mfma = true;  // FI_DISABLE_SC_MFMA=1: VALU horizontal pass (k_sc_hrows) instead of k_sc_hmfma
 };
@@ -336,6 +343,8 @@ static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, 
       c->strip_cache.clear();
       c->mv_cache.clear();
       c->mh_cache.clear();
+      c->vmv_cache.clear();
+      c->vmh_cache.clear();
     }
     AxisTable t;
     build_axis(filter, factor, in_sampled, out_size, o0, o1, sample, in_src, &t);
@@ -748,6 +757,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   std::vector<int> mfma_img;   // indices into rd (mode 4)
   std::vector<const MfmaV *> mfma_v;
   std::vector<const MfmaH *> mfma_h;
+  std::vector<int> vm_img;     // indices into rd (mode 5)
+  std::vector<const VmV *> vm_v;
+  std::vector<const MfmaH *> vm_h;
   // per image resized-buffer workspace offsets (for smartcrop-apply)
   std::vector<size_t> res_off(n, 0);
   double resize_bytes = 0;
@@ -808,7 +820,28 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           add_axis(c, E, P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &d.h, placed);
       const MfmaV *mv = nullptr;
       const MfmaH *mh = nullptr;
-      if (!P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0) {
+      const VmV *vv = nullptr;
+      const MfmaH *vh = nullptr;
+      if (!P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
+          (im.src_stride % 16) == 0) {
+        auto vit = c->vmv_cache.find(vt);
+        if (vit == c->vmv_cache.end()) {
+          VmV m;
+          if (!build_vm_v(*vt, &m)) m = VmV();
+          vit = c->vmv_cache.emplace(vt, std::move(m)).first;
+        }
+        auto hit = c->vmh_cache.find(ht);
+        if (hit == c->vmh_cache.end()) {
+          MfmaH m;
+          if (!build_mfma_h(*ht, &m, kVmMaxNx)) m = MfmaH();
+          hit = c->vmh_cache.emplace(ht, std::move(m)).first;
+        }
+        if (vit->second.nblk > 0 && !hit->second.strips.empty()) {
+          vv = &vit->second;
+          vh = &hit->second;
+        }
+      }
+      if (!vv && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0) {
         auto vit = c->mv_cache.find(vt);
         if (vit == c->mv_cache.end()) {
           MfmaV m;
@@ -827,7 +860,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         }
       }
       const RingTable *ring = nullptr;
-      if (!mv && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0 &&
+      if (!vv && !mv && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0 &&
           d.h.maxtaps <= 64) {
         auto rit = c->ring_cache.find(vt);
         if (rit == c->ring_cache.end()) {
@@ -850,7 +883,13 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         else
           strips = &sit->second;
       }
-      if (mv) {
+      if (vv) {
+        d.mode = 5;  // streaming exact-integer MFMA, vertical first
+        vm_img.push_back((int)rd.size());
+        vm_v.push_back(vv);
+        vm_h.push_back(vh);
+        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
+      } else if (mv) {
         d.mode = 4;  // exact-integer MFMA, vertical first
         mfma_img.push_back((int)rd.size());
         mfma_v.push_back(mv);
@@ -897,14 +936,15 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         d.mid_cols = P.ew;
         d.mid_stride = (3 * P.ew + 7) / 8 * 8;
       }
-      if (d.mode != 3 && d.mode != 4) {
+      if (d.mode != 3 && d.mode != 4 && d.mode != 5) {
         d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
         src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
       }
     }
     resize_bytes += (double)src_bytes + (double)need;
     {
-      static const char *kPath[5] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_mfma"};
+      static const char *kPath[6] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_mfma",
+                                     "path_vm"};
       c->stats[kPath[d.mode]].launches += 1;  // images per resample path (fi_kernel_stats)
     }
     rd_of[i] = (int)rd.size();
@@ -963,7 +1003,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   // ---- build launches
   std::vector<int> m0, m1, m2;
   for (size_t k = 0; k < rd.size(); k++) {
-    if (rd[k].mode == 3 || rd[k].mode == 4) continue;
+    if (rd[k].mode >= 3) continue;
     (rd[k].mode == 0 ? m0 : rd[k].mode == 1 ? m1 : m2).push_back((int)k);
   }
   // fused tiles: (image, column strip, row band); grouped by ring size K
@@ -1114,9 +1154,131 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       }
     }
   }
+  // streaming MFMA tiles (k_rs_vm): (image, strip, band of blocks); tables placed once per geometry
+  std::vector<VDesc> vdescs;
+  std::vector<MStrip> vstrips;
+  std::vector<VTile> vtiles;
+  size_t vm_lds = 0;
+  {
+    auto align4 = [&]() {
+      while (E.ai.size() % 4) E.ai.push_back(0);
+    };
+    auto put = [&](const std::vector<int32_t> &v) {
+      const int32_t o = (int32_t)E.ai.size();
+      E.ai.insert(E.ai.end(), v.begin(), v.end());
+      return o;
+    };
+    std::map<const VmV *, std::array<int32_t, 7>> vplaced;
+    std::map<const MfmaH *, std::pair<int32_t, int32_t>> hplaced;  // first strip, hwsum
+    struct Work1 {
+      int32_t img, first_strip, nstrips;
+      const VmV *V;
+    };
+    std::vector<Work1> work;
+    const int nv = (int)vm_img.size();
+    for (int q = 0; q < nv; q++) {
+      const ResizeDesc &d = rd[vm_img[q]];
+      const VmV &V = *vm_v[q];
+      const MfmaH &H = *vm_h[q];
+      auto vp = vplaced.find(&V);
+      if (vp == vplaced.end()) {
+        std::array<int32_t, 7> o;
+        o[0] = put(V.rows);
+        o[1] = put(V.plo);
+        o[2] = put(V.pn);
+        o[3] = put(V.pblk);
+        o[4] = put(V.plast);
+        align4();
+        o[5] = put(V.w128);
+        align4();
+        o[6] = put(V.frag);
+        vp = vplaced.emplace(&V, o).first;
+      }
+      auto hp = hplaced.find(&H);
+      if (hp == hplaced.end()) {
+        const int32_t first = (int32_t)vstrips.size();
+        const int32_t hw = put(H.wsum);
+        align4();
+        const int32_t frag = put(H.frag);
+        const int32_t s0 = put(H.s0);
+        const int32_t lut = put(H.lut);
+        for (const MfmaStrip &st : H.strips) {
+          MStrip m{};
+          m.x0 = st.x0;
+          m.x1 = st.x1;
+          m.b0 = st.b0;
+          m.nbytes = st.nbytes;
+          m.c_lo = st.c_lo;
+          m.ncols = st.ncols;
+          m.pitch = st.pitch;
+          m.nocb = st.nocb;
+          m.ks = st.ks;
+          m.lut_px0 = st.lut_px0;
+          m.lut_n = st.lut_n;
+          m.frag = frag + (int32_t)st.frag;
+          m.s0 = s0 + (int32_t)st.s0;
+          m.lut = lut + (int32_t)st.lut;
+          vstrips.push_back(m);
+          vm_lds = std::max(vm_lds, vm_lds_bytes(st.nocb, st.ks));
+        }
+        hp = hplaced.emplace(&H, std::make_pair(first, hw)).first;
+      }
+      VDesc m{};
+      m.src = d.src;
+      m.src_stride = d.src_stride;
+      m.dst = d.dst;
+      m.dst_stride = d.dst_stride;
+      m.ew = d.ew;
+      m.eh = d.eh;
+      m.rot = d.rot;
+      m.gray = d.gray;
+      m.rows = vp->second[0];
+      m.nrows = (int32_t)V.rows.size();
+      m.row0 = V.row0;
+      m.rstep = V.rstep;
+      m.plo = vp->second[1];
+      m.pn = vp->second[2];
+      m.pblk = vp->second[3];
+      m.plast = vp->second[4];
+      m.w128 = vp->second[5];
+      m.frag = vp->second[6];
+      m.hwsum = hp->second.second;
+      m.nblk = V.nblk;
+      work.push_back({(int32_t)vdescs.size(), hp->second.first, (int32_t)H.strips.size(), &V});
+      vdescs.push_back(m);
+    }
+    // bands of blocks only when the batch is too small to fill the chip
+    int64_t nst = 0;
+    for (const Work1 &w : work) nst += w.nstrips;
+    // XCD-aware order: the strips of one image go to one XCD queue (blockIdx % 8 under
+    // round-robin dispatch) back to back, so the halo columns they share hit that L2
+    std::vector<std::vector<VTile>> q8(8);
+    for (size_t k = 0; k < work.size(); k++) {
+      const Work1 &w = work[k];
+      const VmV &V = *w.V;
+      int bands = nst > 0 ? (int)((2048 + nst - 1) / nst) : 1;
+      bands = std::max(1, std::min(bands, V.nblk));
+      std::vector<int> first_piece(V.nblk + 1, (int)V.plo.size());
+      for (int p = (int)V.plo.size() - 1; p >= 0; p--) first_piece[V.pblk[p]] = p;
+      for (int bnd = 0; bnd < bands; bnd++) {
+        const int b0 = (int)((int64_t)V.nblk * bnd / bands), b1 = (int)((int64_t)V.nblk * (bnd + 1) / bands);
+        if (b1 <= b0) continue;
+        const int p0 = first_piece[b0 > 0 ? b0 - 1 : 0];
+        const int p1 = first_piece[b1];
+        for (int st = 0; st < w.nstrips; st++)
+          q8[k % 8].push_back(VTile{w.img, w.first_strip + st, p0, p1, b0, 0});
+      }
+    }
+    size_t mx = 0;
+    for (auto &q : q8) mx = std::max(mx, q.size());
+    for (size_t i = 0; i < mx; i++)
+      for (int x = 0; x < 8; x++)
+        if (i < q8[x].size()) vtiles.push_back(q8[x][i]);
+  }
   Blob &B = E.blob;
   const size_t all_rd_off = B.addv(rd);
   const size_t mdesc_off = B.addv(mdescs), mstrip_off = B.addv(mstrips), mtile_off = B.addv(mtiles);
+  const size_t vdesc_off = B.addv(vdescs), vstrip_off = B.addv(vstrips), vtile_off = B.addv(vtiles);
   for (auto &g : fgroups) g.second.off = B.addv(g.second.tiles);
   auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
   auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
@@ -1182,6 +1344,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       if (L0.tiles)
         hipLaunchKernelGGL(k_rs_copy, dim3(L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L0),
                            pre_p(L0), L0.n);
+      if (!vtiles.empty() &&
+          launch_vm(c->stream, (const VDesc *)(ab + vdesc_off), (const MStrip *)(ab + vstrip_off),
+                    (const VTile *)(ab + vtile_off), (int)vtiles.size(), ai, vm_lds) != 0)
+        return set_err(FI_EDEVICE, "streaming MFMA resample launch rejected (LDS %zu)", vm_lds);
       if (!mtiles.empty() &&
           launch_mfma(c->stream, (const MDesc *)(ab + mdesc_off), (const MStrip *)(ab + mstrip_off),
                       (const MTile *)(ab + mtile_off), (int)mtiles.size(), ai, mfma_lds) != 0)
@@ -1441,6 +1607,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   c->device = device;
   if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
   if (const char *e = getenv("FI_ENABLE_MFMA_RS")) c->mfma_rs = e[0] == '1';
+  if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_MFMA")) c->sc_mfma = !(e[0] == '1');
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

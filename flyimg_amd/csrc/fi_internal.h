@@ -167,6 +167,29 @@ constexpr int kMfmaPitch = 232;
 // s0(b) is 8-B aligned (two 8-byte fragment reads), ks <= 2.
 constexpr int kHmMaxLds = 64 * 1024;
 
+// k_rs_vm (fi_vm.hip): streaming exact-integer MFMA resample, vertical first.
+struct VDesc {                // one image
+  const uint8_t *src;
+  int64_t src_stride;
+  uint8_t *dst;
+  int64_t dst_stride;
+  int32_t ew, eh, rot, gray;
+  int32_t rows, nrows, row0, rstep;  // touched-row list (ai offset) / rows[k] = row0 + rstep k when rstep > 0
+  int32_t plo, pn, pblk, plast;      // ai offsets of the piece tables (fi_plan.h VmV)
+  int32_t frag;                      // ai offset (16-B aligned) of the piece fragments [p][2][3][64 lanes][16 B]
+  int32_t w128;                      // ai offset (16-B aligned): 128 * sum of quantized weights per output row
+  int32_t hwsum;                     // ai offset of the horizontal per-px weight sums
+  int32_t nblk;
+};
+struct VTile {                // one workgroup: image x strip x pieces [p0, p1); blocks < emit0 are halo only
+  int32_t img, strip, p0, p1, emit0, pad;
+};
+constexpr int kVmThreads = 256;      // 4 waves x 8 column tiles of 16 B = 512-B strips
+constexpr int kVmPitch = 528;        // LDS row pitch of the piece buffer (16 x odd: rows 4 banks apart)
+// byte c of row r lives at r * pitch + (c ^ (128 * ((r >> 4) & 1))): the two
+// 8-row groups of a ds_read_b64_tr_b8 half-wave (rows 16 apart) land 32 banks apart
+constexpr int kVmChunkBytes = 64 * kVmPitch;
+
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;
   double saturation_bias, saturation_brightness_max, saturation_brightness_min,

@@ -343,7 +343,7 @@ bool build_mfma_v(const AxisTable &v, MfmaV *m) {
   return true;
 }
 
-bool build_mfma_h(const AxisTable &h, MfmaH *m) {
+bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
   *m = MfmaH();
   const int nx = (int)h.start.size();
   if (nx == 0) return false;
@@ -366,7 +366,7 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m) {
   for (int x0 = 0; x0 < nx;) {
     int x1 = x0 + 1, b0;
     if (bytes_of(x0, x1, &b0) > kMfmaStripBytes) return false;
-    while (x1 < nx && x1 - x0 < kMfmaMaxNx && bytes_of(x0, x1 + 1, &b0) <= kMfmaStripBytes) x1++;
+    while (x1 < nx && x1 - x0 < max_nx && bytes_of(x0, x1 + 1, &b0) <= kMfmaStripBytes) x1++;
     MfmaStrip S{};
     S.x0 = x0;
     S.x1 = x1;
@@ -419,6 +419,83 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m) {
     m->strips.push_back(S);
     x0 = x1;
   }
+  return true;
+}
+
+bool build_vm_v(const AxisTable &v, VmV *m) {
+  *m = VmV();
+  const int ny = (int)v.start.size();
+  if (ny == 0) return false;
+  std::vector<int32_t> idx;
+  touched_list(v, &m->rows, &idx);
+  const int nl = (int)m->rows.size();
+  if (nl == 0) return false;
+  m->nblk = (ny + 15) / 16;
+  std::vector<int> L(m->nblk), R(m->nblk);
+  for (int b = 0; b < m->nblk; b++) {
+    int lo = 1 << 30, hi = -1;
+    for (int y = 16 * b; y < std::min(ny, 16 * b + 16); y++) {
+      int a, e;
+      tap_range(v, idx, y, &a, &e);
+      if (e < a) return false;  // an output row without taps
+      lo = std::min(lo, a);
+      hi = std::max(hi, e);
+    }
+    L[b] = lo;
+    R[b] = hi + 1;
+    if (b > 0 && (L[b] < L[b - 1] || R[b] < R[b - 1])) return false;  // not monotone
+  }
+  // pieces: block b owns [R(b-1), R(b)), R(-1) = L(0)
+  std::vector<int> pstart(m->nblk + 1);  // first piece of block b
+  for (int b = 0; b < m->nblk; b++) {
+    pstart[b] = (int)m->plo.size();
+    const int a = b == 0 ? L[0] : R[b - 1], e = R[b];
+    // the taps of block b must lie in the pieces of blocks b - 1 and b
+    const int own_lo = b == 0 ? L[0] : (b == 1 ? L[0] : R[b - 2]);
+    if (L[b] < own_lo) return false;
+    int k = a;
+    do {
+      const int n = std::min(64, e - k);
+      m->plo.push_back(k);
+      m->pn.push_back(std::max(n, 0));
+      m->pblk.push_back(b);
+      m->plast.push_back(0);
+      k += std::max(n, 0);
+    } while (k < e);
+    m->plast.back() = 1;
+  }
+  pstart[m->nblk] = (int)m->plo.size();
+  const int np = (int)m->plo.size();
+  m->frag.assign((size_t)np * 6 * 256, 0);
+  for (int p = 0; p < np; p++)
+    for (int s = 0; s < 2; s++) {
+      const int bb = m->pblk[p] + s;
+      if (bb >= m->nblk) continue;
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int y = 16 * bb + (l & 15), k = mfma_i8_k(l, j);
+          int32_t limb[3];
+          limbs3(y < ny && k < m->pn[p] ? tap_w(v, m->rows, y, m->plo[p] + k) : 0, limb);
+          put_frag(m->frag, (size_t)(p * 2 + s) * 3 * 256, l, j, limb);
+        }
+    }
+  // every tap is covered exactly once by (its block's pieces) U (previous block's pieces)
+  for (int y = 0; y < ny; y++) {
+    const int b = y / 16;
+    const int lo_list = b == 0 ? L[0] : m->plo[pstart[b - 1]];
+    for (int j = 0; j < v.count[y]; j++) {
+      if (v.w[v.woff[y] + j] == 0.0f) continue;
+      const int li = idx[v.start[y] + j - v.src_lo];
+      if (li < lo_list || li >= R[b]) return false;
+    }
+  }
+  m->w128.assign((size_t)16 * m->nblk, 0);
+  for (int y = 0; y < ny; y++)
+    for (int j = 0; j < v.count[y]; j++) m->w128[y] += 128 * quant_w(v.w[v.woff[y] + j]);
+  m->row0 = m->rows[0];
+  m->rstep = nl > 1 ? m->rows[1] - m->rows[0] : 1;
+  for (int k = 1; k < nl && m->rstep > 0; k++)
+    if (m->rows[k] != m->row0 + m->rstep * k) m->rstep = 0;
   return true;
 }
 

@@ -81,7 +81,27 @@ struct MfmaH {
   std::vector<int32_t> frag, s0, lut;  // B fragments [strip][nocb][ks][3]; (w0, ks) per block; LUTs
   std::vector<int32_t> wsum;           // [ew] sum of quantized weights per output px
 };
-bool build_mfma_h(const AxisTable &h, MfmaH *m);
+bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx = kMfmaMaxNx);
+
+// Streaming vertical tables of k_rs_vm (fi_vm.hip).  The touched-row list is
+// cut into pieces of <= 64 rows aligned to the 16-row output blocks: the
+// pieces of block b hold the rows first needed by b, [R(b-1), R(b)), with
+// R(b) = one past the last tap row of block b.  A piece feeds two
+// accumulator slots: slot 0 = its own block b, slot 1 = block b + 1 (whose
+// window starts inside it).  Block b is complete after its last piece.
+// Requires every tap of block b to lie in the pieces of b - 1 and b
+// (checked: taps span <= 21 output rows' worth of rows for Lanczos/Mitchell
+// at any downscale).
+constexpr int kVmMaxNx = 64;           // output px per strip: 4 16-px blocks, one per wave
+struct VmV {
+  std::vector<int32_t> rows;           // touched source rows, ascending
+  int nblk = 0;                        // 16-row output blocks
+  std::vector<int32_t> plo, pn, pblk, plast;  // per piece: list start, rows, block, block completes
+  std::vector<int32_t> frag;           // [piece][slot 0/1][limb 0..2] fragments (256 int32 each)
+  std::vector<int32_t> w128;           // [16 nblk] 128 * sum of quantized weights of each output row
+  int32_t row0 = 0, rstep = 0;         // rstep > 0: rows[k] == row0 + rstep * k
+};
+bool build_vm_v(const AxisTable &v, VmV *m);
 
 // Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)
 // to `out_size`; taps mapped back to the `in_src` source indices through the

@@ -81,6 +81,63 @@ static void check_v(const AxisTable &v, const char *name) {
   printf("  %s: vertical %d blocks ks=%d rows=%zu ok\n", name, m.nyb, m.ks, m.rows.size());
 }
 
+// k_rs_vm: stream the pieces in order with two accumulator slots exactly as
+// the kernel does (slot 0 = the piece's block, slot 1 = the next block,
+// started at its w128 correction) and compare every completed block.
+static void check_vm(const AxisTable &v, const char *name) {
+  VmV m;
+  if (!build_vm_v(v, &m)) {
+    printf("  %s: streaming vertical tables not built, skipped\n", name);
+    CHECK(!g_required, "%s: streaming vertical tables required", name);
+    return;
+  }
+  const int ny = (int)v.start.size(), np = (int)m.plo.size();
+  std::mt19937 rng(4321);
+  std::vector<int> px(v.src_hi);
+  for (auto &x : px) x = (int)(rng() & 255);
+  auto w128 = [&](int b, int r) -> int64_t { return b < m.nblk ? m.w128[16 * b + r] : 0; };
+  std::vector<int64_t> acc0(16), acc1(16);
+  int b0 = m.pblk[0], done = 0;
+  for (int r = 0; r < 16; r++) {
+    acc0[r] = w128(b0, r);
+    acc1[r] = w128(b0 + 1, r);
+  }
+  for (int p = 0; p < np; p++) {
+    CHECK(m.pn[p] >= 0 && m.pn[p] <= 64, "%s: piece %d has %d rows", name, p, m.pn[p]);
+    CHECK(p == 0 || m.plo[p] == m.plo[p - 1] + m.pn[p - 1], "%s: pieces not contiguous at %d", name, p);
+    for (int s = 0; s < 2; s++)
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int k = mfma_i8_k(l, j);
+          const int64_t w = limb_w(m.frag, (size_t)(p * 2 + s) * 3 * 256, l, j);
+          if (k >= m.pn[p]) {
+            CHECK(w == 0, "%s: weight past the piece", name);
+            continue;
+          }
+          const int64_t add = w * (px[m.rows[m.plo[p] + k]] - 128);
+          (s == 0 ? acc0 : acc1)[l & 15] += add;
+        }
+    if (m.plast[p]) {
+      const int b = m.pblk[p];
+      CHECK(b == done, "%s: block %d completes out of order", name, b);
+      for (int r = 0; r < 16; r++) {
+        const int y = 16 * b + r;
+        if (y >= ny) continue;
+        int64_t ref = 0;
+        for (int j = 0; j < v.count[y]; j++) ref += (int64_t)qw(v.w[v.woff[y] + j]) * px[v.start[y] + j];
+        CHECK(acc0[r] == ref, "%s: streaming vertical y=%d %lld != %lld", name, y, (long long)acc0[r],
+              (long long)ref);
+        CHECK(llabs(acc0[r]) < (1ll << 31), "%s: accumulator exceeds int32", name);
+      }
+      done++;
+      acc0 = acc1;
+      for (int r = 0; r < 16; r++) acc1[r] = w128(b + 2, r);
+    }
+  }
+  CHECK(done == m.nblk, "%s: %d of %d blocks completed", name, done, m.nblk);
+  printf("  %s: streaming vertical %d blocks, %d pieces, rstep %d ok\n", name, m.nblk, np, m.rstep);
+}
+
 static void check_h(const AxisTable &h, const char *name) {
   MfmaH m;
   if (!build_mfma_h(h, &m)) {
@@ -205,6 +262,7 @@ static void geometry(int W, int H, int tw, int th, uint32_t flags, const char *n
   build_axis(P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &h);
   check_v(v, name);
   check_h(h, name);
+  check_vm(v, name);
 }
 
 int main() {

@@ -44,10 +44,13 @@ def _context_with(env):
                 os.environ[k] = v
 
 
-_ENV = {"FI_DISABLE_FUSED": "0", "FI_ENABLE_MFMA_RS": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0"}
+_ENV = {"FI_DISABLE_FUSED": "0", "FI_ENABLE_MFMA_RS": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0",
+        "FI_DISABLE_VM_RS": "0"}
 PATHS = {
-    # default kernels: k_rs_fused resample; k_sc_hmfma + k_sc_vmaps prescale; k_sc_score2
-    "valu": dict(_ENV),
+    # default kernels: k_rs_vm streaming MFMA resample; k_sc_hmfma + k_sc_vmaps prescale; k_sc_score2
+    "vm": dict(_ENV),
+    # VALU fused resample (k_rs_fused)
+    "valu": dict(_ENV, FI_DISABLE_VM_RS="1"),
     # exact-integer MFMA resample (opt-in) with the VALU horizontal prescale (k_sc_hrows)
     "mfma": dict(_ENV, FI_ENABLE_MFMA_RS="1", FI_DISABLE_SC_MFMA="1"),
     # generic kernels: two-pass resample; per-row prescale/maps kernels
@@ -64,7 +67,7 @@ def rctx(request):
     c.close()
 
 
-EXPECTED_PATH = {"mfma": "path_mfma", "valu": "path_fused", "generic": "path_generic_v"}
+EXPECTED_PATH = {"vm": "path_vm", "mfma": "path_mfma", "valu": "path_fused", "generic": "path_generic_v"}
 
 
 @pytest.mark.parametrize("W,H,opts", [
