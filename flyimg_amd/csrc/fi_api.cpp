@@ -55,6 +55,7 @@ int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const M
                 const int32_t *ai, size_t lds);
 // streaming exact-integer MFMA resample (fi_vm.hip)
 size_t vm_lds_bytes(int nocb, int ks);
+int vm_read_stamps(uint64_t *out, int slots);
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
 int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
@@ -1168,7 +1169,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       E.ai.insert(E.ai.end(), v.begin(), v.end());
       return o;
     };
-    std::map<const VmV *, std::array<int32_t, 7>> vplaced;
+    std::map<const VmV *, std::array<int32_t, 8>> vplaced;
     std::map<const MfmaH *, std::pair<int32_t, int32_t>> hplaced;  // first strip, hwsum
     struct Work1 {
       int32_t img, first_strip, nstrips;
@@ -1182,7 +1183,16 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       const MfmaH &H = *vm_h[q];
       auto vp = vplaced.find(&V);
       if (vp == vplaced.end()) {
-        std::array<int32_t, 7> o;
+        std::array<int32_t, 8> o;
+        std::vector<int32_t> meta;
+        for (size_t k = 0; k < V.plo.size(); k++) {
+          meta.push_back(V.plo[k]);
+          meta.push_back(V.pn[k]);
+          meta.push_back(V.pblk[k]);
+          meta.push_back(V.plast[k]);
+        }
+        align4();
+        o[7] = put(meta);
         o[0] = put(V.rows);
         o[1] = put(V.plo);
         o[2] = put(V.pn);
@@ -1242,6 +1252,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       m.plast = vp->second[4];
       m.w128 = vp->second[5];
       m.frag = vp->second[6];
+      m.pmeta = vp->second[7];
       m.hwsum = hp->second.second;
       m.nblk = V.nblk;
       work.push_back({(int32_t)vdescs.size(), hp->second.first, (int32_t)H.strips.size(), &V});
@@ -1584,6 +1595,13 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
 extern "C" {
 
 int32_t fi_abi_version(void) { return FI_ABI_VERSION; }
+// profiling only (not in the public header): k_rs_vm MODE 9 phase sums, 8 u64 per workgroup
+int fi_debug_vm_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
+  if (!c || !out) return FI_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return vm_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
+}
 const char *fi_last_error(void) { return g_err.c_str(); }
 
 int fi_device_count(int32_t *count) {

@@ -176,6 +176,7 @@ struct VDesc {                // one image
   int32_t ew, eh, rot, gray;
   int32_t rows, nrows, row0, rstep;  // touched-row list (ai offset) / rows[k] = row0 + rstep k when rstep > 0
   int32_t plo, pn, pblk, plast;      // ai offsets of the piece tables (fi_plan.h VmV)
+  int32_t pmeta;                     // ai offset (16-B aligned): per piece {plo, pn, pblk, plast}
   int32_t frag;                      // ai offset (16-B aligned) of the piece fragments [p][2][3][64 lanes][16 B]
   int32_t w128;                      // ai offset (16-B aligned): 128 * sum of quantized weights per output row
   int32_t hwsum;                     // ai offset of the horizontal per-px weight sums
@@ -189,6 +190,10 @@ constexpr int kVmPitch = 528;        // LDS row pitch of the piece buffer (16 x 
 // byte c of row r lives at r * pitch + (c ^ (128 * ((r >> 4) & 1))): the two
 // 8-row groups of a ds_read_b64_tr_b8 half-wave (rows 16 apart) land 32 banks apart
 constexpr int kVmChunkBytes = 64 * kVmPitch;
+constexpr int kVmPlane = kMfmaPitch * 16;       // one Q16 limb plane: [column <= kMfmaPitch][16 rows]
+constexpr int kVmPlaneBytes = 6 * kVmPlane;     // [hi, lo][3 channels]
+constexpr int kVmOtilePitch = 64 * 3 + 4;      // 8-bit output tile row (nx <= kVmMaxNx = 64, + alignment shift)
+constexpr int kVmOtileBytes = 16 * kVmOtilePitch;
 
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;

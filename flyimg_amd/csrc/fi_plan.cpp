@@ -489,7 +489,7 @@ bool build_vm_v(const AxisTable &v, VmV *m) {
       if (li < lo_list || li >= R[b]) return false;
     }
   }
-  m->w128.assign((size_t)16 * m->nblk, 0);
+  m->w128.assign((size_t)16 * (m->nblk + 2), 0);  // two zero blocks: k_rs_vm loads block b + 2 unconditionally
   for (int y = 0; y < ny; y++)
     for (int j = 0; j < v.count[y]; j++) m->w128[y] += 128 * quant_w(v.w[v.woff[y] + j]);
   m->row0 = m->rows[0];
