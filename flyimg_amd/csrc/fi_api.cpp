@@ -163,6 +163,7 @@ struct fi_ctx {
   bool fused = true;    // FI_DISABLE_FUSED=1 forces the generic two-pass resample
   bool mfma_rs = false;  // FI_ENABLE_MFMA_RS=1: k_rs_mfma instead of the VALU fused kernel
   bool vm_rs = true;     // FI_DISABLE_VM_RS=1: no k_rs_vm (streaming MFMA resample, the default)
+  bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
   std::map<const AxisTable *, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
@@ -642,7 +643,8 @@ struct ScLaunches {
   int nsl = 0, nsg = 0, sl_px = 0;
   size_t crops_off = 0;
 };
-static void add_sc_launches(Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus, ScLaunches *X) {
+static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
+                            ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
   std::vector<ScDesc> prep, hv, hm, sl, sg;
   for (size_t k = 0; k < SL.descs.size(); k++) {
@@ -668,7 +670,7 @@ static void add_sc_launches(Blob &B, const ScLaunchData &SL, const std::vector<i
       if (d.pre) svp.push_back((int)k);
       smaps.push_back((int)k);
     }
-    if ((int64_t)d.aw * d.ah * 4 <= kScoreLdsMaps) {
+    if (c->sc_lds_maps && (int64_t)d.aw * d.ah * 4 <= kScoreLdsMaps) {
       sl.push_back(d);
       X->sl_px = std::max(X->sl_px, d.aw * d.ah);
     } else {
@@ -833,8 +835,19 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         }
         auto hit = c->vmh_cache.find(ht);
         if (hit == c->vmh_cache.end()) {
+          // strips of <= 64 px; narrower when the horizontal fragments would not
+          // leave room for two workgroups per CU
           MfmaH m;
-          if (!build_mfma_h(*ht, &m, kVmMaxNx)) m = MfmaH();
+          for (int mx : {kVmMaxNx, 48, 32}) {
+            if (!build_mfma_h(*ht, &m, mx)) {
+              m = MfmaH();
+              break;
+            }
+            bool fits = true;
+            for (const MfmaStrip &st : m.strips) fits = fits && vm_lds_bytes(st.nocb, st.ks) <= kVmMaxLds;
+            if (fits) break;
+            m = MfmaH();
+          }
           hit = c->vmh_cache.emplace(ht, std::move(m)).first;
         }
         if (vit->second.nblk > 0 && !hit->second.strips.empty()) {
@@ -1298,7 +1311,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   Launch L2a = add_launch(B, rd, m2, mid_tiles);
   Launch L2b = add_launch(B, rd, m2, eh_tiles);
   ScLaunches SX;
-  add_sc_launches(B, SL, sstatus, &SX);
+  add_sc_launches(c, B, SL, sstatus, &SX);
   const bool any_sc = SX.nsl + SX.nsg > 0;
   std::vector<ApplyDesc> apply;
   std::vector<int> apply_img;
@@ -1539,7 +1552,7 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   fix_ptr(d.maps, wb);
   Blob &B = E.blob;
   ScLaunches SX;
-  add_sc_launches(B, SL, st, &SX);
+  add_sc_launches(c, B, SL, st, &SX);
   const size_t ai_off = B.addv(E.ai), ad_off = B.addv(E.ad);
   rc = ensure(c, &c->arena, B.b.size() + 256);
   if (rc) return rc;
@@ -1626,6 +1639,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
   if (const char *e = getenv("FI_ENABLE_MFMA_RS")) c->mfma_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
+  if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_MFMA")) c->sc_mfma = !(e[0] == '1');
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

@@ -190,6 +190,7 @@ constexpr int kVmPitch = 528;        // LDS row pitch of the piece buffer (16 x 
 // byte c of row r lives at r * pitch + (c ^ (128 * ((r >> 4) & 1))): the two
 // 8-row groups of a ds_read_b64_tr_b8 half-wave (rows 16 apart) land 32 banks apart
 constexpr int kVmChunkBytes = 64 * kVmPitch;
+constexpr int kVmMaxLds = 80 * 1024;  // two workgroups per CU
 constexpr int kVmPlane = kMfmaPitch * 16;       // one Q16 limb plane: [column <= kMfmaPitch][16 rows]
 constexpr int kVmPlaneBytes = 6 * kVmPlane;     // [hi, lo][3 channels]
 constexpr int kVmOtilePitch = 64 * 3 + 4;      // 8-bit output tile row (nx <= kVmMaxNx = 64, + alignment shift)

@@ -10,7 +10,7 @@
 //                 (:116-133), maps resident in LDS: fast f64 pass with a
 //                 rigorous error bound, exact sequential re-score of the
 //                 crops whose interval reaches the best lower bound.
-//   k_crop_apply2 convert -crop of the winning box (SmartCropProcessor.php:30-34).
+//   k_crop_apply3 convert -crop of the winning box (SmartCropProcessor.php:30-34).
 //
 // The generic per-row kernels in fi_kernels.hip remain for geometries whose
 // staging does not fit LDS (ScPlan::prep_ok == 0).
@@ -496,26 +496,66 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
 // convert <out> -crop WxH+X+Y with W = w + x, H = h + y as smartcrop.py prints
 // them (:372-377); CropImage clips to the image.  kApplyBands workgroups per
 // image, rows interleaved.
-constexpr int kApplyBands = 8;
-__global__ __launch_bounds__(256) void k_crop_apply2(const ApplyDesc *__restrict__ descs,
+constexpr int kApplyChunks = 16;  // workgroups per image
+// The output is one contiguous byte array (oh rows of ow * C bytes): 16-byte
+// destination chunks, each assembled from 5 aligned source dwords with
+// v_alignbyte (the crop origin has any byte alignment); chunks that straddle a
+// row end, and the unaligned head/tail of the array, go byte by byte.
+__device__ __forceinline__ uint32_t ap_align(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+__global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict__ descs,
                                                      const DevCrop *__restrict__ crops,
                                                      const ScResult *__restrict__ results) {
-  const ApplyDesc &A = descs[blockIdx.x / kApplyBands];
-  const int band = blockIdx.x % kApplyBands;
+  const ApplyDesc &A = descs[blockIdx.y];
   const ScResult r = results[A.result];
   if (r.top < 0) return;
   const DevCrop c = crops[A.crop0 + r.top];
   const int gw = c.rw + c.rx, gh = c.rh + c.ry;
   const int ow = min(gw, A.W - c.rx), oh = min(gh, A.H - c.ry);
-  if (band == 0 && threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     A.out_wh[0] = ow;
     A.out_wh[1] = oh;
   }
   const int rowb = ow * A.C;
-  for (int y = band; y < oh; y += kApplyBands) {
-    const uint8_t *__restrict__ s = A.src + (int64_t)(c.ry + y) * A.src_stride + (int64_t)c.rx * A.C;
-    uint8_t *__restrict__ d = A.dst + (int64_t)y * rowb;
-    for (int k = threadIdx.x; k < rowb; k += 256) d[k] = s[k];
+  const int64_t total = (int64_t)rowb * oh;
+  if (total <= 0) return;
+  const uint8_t *src0 = A.src + (int64_t)c.ry * A.src_stride + (int64_t)c.rx * A.C;
+  auto src_of = [&](int64_t o) {
+    const int y = (int)(o / rowb), x = (int)(o - (int64_t)y * rowb);
+    return src0 + (int64_t)y * A.src_stride + x;
+  };
+  const int head = (int)((16 - ((uintptr_t)A.dst & 15)) & 15);
+  const int64_t nchunk = head < total ? (total - head) / 16 : 0;
+  const int64_t tail0 = head + 16 * nchunk;
+  const int tid = threadIdx.x;
+  if (blockIdx.x == 0) {
+    for (int64_t o = tid; o < min<int64_t>(head, total); o += 256) A.dst[o] = *src_of(o);
+    for (int64_t o = tail0 + tid; o < total; o += 256) A.dst[o] = *src_of(o);
+  }
+  for (int64_t k = (int64_t)blockIdx.x * 256 + tid; k < nchunk; k += (int64_t)gridDim.x * 256) {
+    const int64_t o = head + 16 * k;
+    const int y = (int)(o / rowb), x = (int)(o - (int64_t)y * rowb);
+    uint4 out;
+    if (x + 16 <= rowb) {
+      const uint8_t *s = src0 + (int64_t)y * A.src_stride + x;
+      const uint32_t *sa = reinterpret_cast<const uint32_t *>((uintptr_t)s & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
+      const uint32_t w0 = sa[0], w1 = sa[1], w2 = sa[2], w3 = sa[3], w4 = sh ? sa[4] : 0u;
+      out.x = ap_align(w1, w0, sh);
+      out.y = ap_align(w2, w1, sh);
+      out.z = ap_align(w3, w2, sh);
+      out.w = ap_align(w4, w3, sh);
+    } else {
+      uint8_t b[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) b[j] = *src_of(o + j);
+      out.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+      out.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+      out.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
+      out.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
+    }
+    *reinterpret_cast<uint4 *>(A.dst + o) = out;
   }
 }
 
@@ -551,7 +591,7 @@ int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, in
 }
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_crop_apply2, dim3(n * kApplyBands), dim3(256), 0, s, descs, crops, results);
+  hipLaunchKernelGGL(k_crop_apply3, dim3(kApplyChunks, n), dim3(256), 0, s, descs, crops, results);
   return 0;
 }
 

@@ -438,7 +438,7 @@ size_t vm_lds_bytes(int nocb, int ks) {
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds) {
   if (ntiles <= 0) return 0;
-  if (lds > 80 * 1024) return -1;  // two workgroups per CU
+  if (lds > (size_t)kVmMaxLds) return -1;  // two workgroups per CU
   static const char *variant = getenv("FI_VM_VARIANT");  // profiling ablations only
   const int v = variant ? atoi(variant) : 0;
   if (v == 1)
