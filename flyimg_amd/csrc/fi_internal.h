@@ -185,7 +185,7 @@ struct VDesc {                // one image
 struct VTile {                // one workgroup: image x strip x pieces [p0, p1); blocks < emit0 are halo only
   int32_t img, strip, p0, p1, emit0, pad;
 };
-constexpr int kVmThreads = 256;      // 4 waves x 8 column tiles of 16 B = 512-B strips
+constexpr int kVmThreads = 512;      // 8 waves x 4 column tiles of 16 B = 512-B strips
 constexpr int kVmPitch = 528;        // LDS row pitch of the piece buffer (16 x odd: rows 4 banks apart)
 // byte c of row r lives at r * pitch + (c ^ (128 * ((r >> 4) & 1))): the two
 // 8-row groups of a ds_read_b64_tr_b8 half-wave (rows 16 apart) land 32 banks apart
@@ -193,8 +193,8 @@ constexpr int kVmChunkBytes = 64 * kVmPitch;
 constexpr int kVmMaxLds = 80 * 1024;  // two workgroups per CU
 constexpr int kVmPlane = kMfmaPitch * 16;       // one Q16 limb plane: [column <= kMfmaPitch][16 rows]
 constexpr int kVmPlaneBytes = 6 * kVmPlane;     // [hi, lo][3 channels]
-constexpr int kVmOtilePitch = 64 * 3 + 4;      // 8-bit output tile row (nx <= kVmMaxNx = 64, + alignment shift)
-constexpr int kVmOtileBytes = 16 * kVmOtilePitch;
+constexpr int kVmOtilePitch = 64 * 3 + 4;      // Q16 output tile row, u16 units (nx <= kVmMaxNx = 64)
+constexpr int kVmOtileBytes = 16 * kVmOtilePitch * 2;
 
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;

@@ -307,7 +307,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_sc_vmaps(const ScDesc *__restr
 }
 
 // ---------------------------------------------------------------------------
-constexpr int kScoreThreads = 512;
+constexpr int kScoreThreads = 1024;
 constexpr int kScoreWaves = kScoreThreads / 64;
 
 template <bool LDS_MAPS>
