@@ -195,6 +195,7 @@ constexpr int kVmPlane = kMfmaPitch * 16;       // one Q16 limb plane: [column <
 constexpr int kVmPlaneBytes = 6 * kVmPlane;     // [hi, lo][3 channels]
 constexpr int kVmOtilePitch = 64 * 3 + 4;      // Q16 output tile row, u16 units (nx <= kVmMaxNx = 64)
 constexpr int kVmOtileBytes = 16 * kVmOtilePitch * 2;
+constexpr int kVmOtile8Pitch = 64 * 3 + 4;     // 8-bit tile row (fast RGB path), aliases the Q16 tile
 
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;

@@ -112,6 +112,14 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
   i32x4 *hbl = reinterpret_cast<i32x4 *>(vpl + kVmPlaneBytes + kVmOtileBytes);  // [nocb][ks][3][64]
   const int oc = D.gray ? 1 : 3;
   const int nx = S.x1 - S.x0;
+  // RGB without rotation: the horizontal pass writes final bytes into an 8-bit
+  // tile whose row yl starts at byte sh(yl) = (destination address of the row
+  // segment) & 3, so the stores are plain dword copies; otherwise a Q16 tile.
+  const bool fast8 = !D.gray && D.rot == 0;
+  uint8_t *otile8 = reinterpret_cast<uint8_t *>(otile);  // [16][kVmOtile8Pitch] (aliases the Q16 tile)
+  const uint32_t sh0 = (uint32_t)(((uintptr_t)D.dst + (uint64_t)S.x0 * 3) & 3u);
+  const uint32_t shs = (uint32_t)(D.dst_stride & 3);
+  auto row_sh = [&](int y) -> int { return (int)((sh0 + (uint32_t)y * shs) & 3u); };
   const int64_t sstride = D.src_stride;
 
   // ---- per-lane constants -------------------------------------------------
@@ -207,6 +215,26 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
   auto store_block = [&](int b) {
     const int rows_here = min(16, D.eh - 16 * b);
     const int nb = nx * oc;
+    if (fast8) {
+      // items = (row, destination dword): interior dwords copied from the
+      // shifted 8-bit tile as one dword, the partial first/last dword byte by byte
+      const int ndw = (nb + 3) / 4 + 1;
+      const float inv = 1.0f / (float)ndw;
+      for (int it = tid; it < rows_here * ndw; it += kVmThreads) {
+        const int yl = (int)(((float)it + 0.5f) * inv), d = it - yl * ndw;
+        const int sh = row_sh(16 * b + yl);
+        const int k0 = 4 * d - sh;  // segment byte of the dword's first byte
+        if (k0 >= nb) continue;
+        uint8_t *a0 = D.dst + (int64_t)(16 * b + yl) * D.dst_stride + (int64_t)S.x0 * 3;
+        const uint8_t *o = otile8 + yl * kVmOtile8Pitch;
+        if (k0 >= 0 && k0 + 4 <= nb) {
+          *(g_u32v *)(a0 + k0) = *reinterpret_cast<const uint32_t *>(o + 4 * d);
+        } else {
+          for (int k = max(k0, 0); k < min(k0 + 4, nb); k++) *(g_u8v *)(a0 + k) = o[sh + k];
+        }
+      }
+      return;
+    }
     if (D.rot == 0) {
       // items = (row, destination dword): interior dwords as one dword store,
       // the partial first/last dword of a row byte by byte
@@ -360,7 +388,12 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
               for (int i = 0; i < 4; i++) {
                 const float tot = 256.0f * (float)vm_fold3(hh[0][i], hh[1][i], hh[2][i]) +
                                   (float)vm_fold3(hl[0][i], hl[1][i], hl[2][i]) + hws;
-                o[i * kVmOtilePitch] = (uint16_t)min(__float2uint_rz(fmaf(tot, 1.0f / 4194304.0f, 0.5f)), 65535u);
+                const uint32_t q = min(__float2uint_rz(fmaf(tot, 1.0f / 4194304.0f, 0.5f)), 65535u);
+                const int yl = 4 * (lane >> 4) + i;
+                if (fast8)
+                  otile8[yl * kVmOtile8Pitch + row_sh(16 * b + yl) + 3 * hx + chn] = (uint8_t)vm_q16_to_u8(q);
+                else
+                  o[i * kVmOtilePitch] = (uint16_t)q;
               }
             }
           }
