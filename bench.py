@@ -225,6 +225,18 @@ def main():
             "exact_rescored_crops_per_step": allv[0]["ncand"],
             "failed_images": sum(v["bad"] for v in allv),
         }
+        # HBM traffic of the dominant kernel from the committed rocprofv3 PMC
+        # passes (tools/gpu_profile.sh -> profiles/traffic_<workload>_<kernel>.json)
+        kern = [p for p, n in paths.items() if n]
+        if len(kern) == 1:
+            kname = KERNEL_OF_PATH[kern[0]].split()[0]
+            tf = os.path.join(REPO, "profiles", f"traffic_{args.workload}_{kname}.json")
+            if os.path.exists(tf):
+                t = json.load(open(tf))
+                ipl = rs_n and (nimg * args.steps) // rs_n or nimg
+                result["roofline"]["traffic"] = round(t["hbm_bytes_per_image"] * ipl)
+                result["roofline"]["traffic_source"] = (f"profiles/traffic_{args.workload}_{kname}.json: "
+                                                        f"{t['correction']}, measured per image x {ipl} images")
         if not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(W, H, options)

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Per-dispatch HBM traffic of one kernel from rocprofv3 --pmc passes
+(FETCH_SIZE, WRITE_SIZE in KiB summed over the XCDs) -> JSON for bench.py's
+roofline.traffic.  gfx950 correction (MI355X_MICROARCH.md, HBM section):
+FETCH_SIZE counts half the bytes of wide (16 B/lane) coalesced reads, so it
+is doubled; WRITE_SIZE is taken as is (dword/byte stores: uncalibrated).
+
+  pmc_to_json.py <pmc dir> <kernel substring> <images per dispatch> <out.json>
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+root, kname, ipd, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+vals = collections.defaultdict(lambda: collections.defaultdict(float))
+for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if kname not in r.get("Kernel_Name", ""):
+            continue
+        vals[r["Counter_Name"]][r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
+res = {"kernel": kname, "images_per_dispatch": ipd}
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    d = vals.get(c, {})
+    if d:
+        res[c.lower() + "_kib_per_dispatch"] = sum(d.values()) / len(d)
+        res["dispatches"] = len(d)
+if "fetch_size_kib_per_dispatch" in res and "write_size_kib_per_dispatch" in res:
+    b = 2 * res["fetch_size_kib_per_dispatch"] * 1024 + res["write_size_kib_per_dispatch"] * 1024
+    res["hbm_bytes_per_dispatch"] = b
+    res["hbm_bytes_per_image"] = b / ipd
+    res["correction"] = "2 x FETCH_SIZE (gfx950 wide-read half count) + WRITE_SIZE"
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res))
