@@ -44,6 +44,8 @@ __global__ void k_sc_maps(const ScDesc *, const int32_t *, int, const ScParamsDe
 int launch_sc_h(hipStream_t s, bool mfma, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai);
 int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
                 const ScParamsDev &P);
+int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
+                 const ScParamsDev &P);
 int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, int max_px, const DevCrop *crops,
                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P);
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
@@ -164,6 +166,7 @@ struct fi_ctx {
   bool mfma_rs = false;  // FI_ENABLE_MFMA_RS=1: k_rs_mfma instead of the VALU fused kernel
   bool vm_rs = true;     // FI_DISABLE_VM_RS=1: no k_rs_vm (streaming MFMA resample, the default)
   bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
+  bool sc_vq = true;        // FI_DISABLE_SC_VQ=1: k_sc_vmaps (VALU vertical pass) instead of k_sc_vq
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
   std::map<const AxisTable *, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
@@ -439,7 +442,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
   const bool fast_ok = E.params.skin_bias >= 0 && E.params.saturation_bias >= 0;
   struct Placed {
     int32_t hb = 0, hk = 0, hkT = 0, vb = 0, vk = 0, crop0 = 0, ncrops = 0;
-    int32_t hmB = 0, hmC = 0, hmS0 = 0;
+    int32_t hmB = 0, hmC = 0, hmS0 = 0, vqA = 0, vqC = 0, vqK0 = 0;
   };
   std::map<const ScPlan *, Placed> placed;
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_placed;
@@ -495,6 +498,15 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
           E.ai.insert(E.ai.end(), P.hmC.begin(), P.hmC.end());
           q.hmS0 = (int32_t)E.ai.size();
           E.ai.insert(E.ai.end(), P.hmS0.begin(), P.hmS0.end());
+        }
+        if (P.vq_ok) {
+          while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
+          q.vqA = (int32_t)E.ai.size();
+          E.ai.insert(E.ai.end(), P.vqA.begin(), P.vqA.end());
+          q.vqC = (int32_t)E.ai.size();
+          E.ai.insert(E.ai.end(), P.vqC.begin(), P.vqC.end());
+          q.vqK0 = (int32_t)E.ai.size();
+          E.ai.insert(E.ai.end(), P.vqK0.begin(), P.vqK0.end());
         }
       }
       // crops + importance tables (one table per distinct window size)
@@ -586,6 +598,10 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.hmB = q.hmB;
     d.hmC = q.hmC;
     d.hmS0 = q.hmS0;
+    d.vq = prep && P.vq_ok && c->sc_vq ? 1 : 0;
+    d.vqA = q.vqA;
+    d.vqC = q.vqC;
+    d.vqK0 = q.vqK0;
     d.prescale = P.prescale;
     d.exact_all = o.exact_all || !fast_ok;
     // workspace (offsets; converted to pointers after allocation)
@@ -637,8 +653,9 @@ static Launch add_launch(Blob &blob, const std::vector<Desc> &all, const std::ve
 // otherwise.
 struct ScLaunches {
   Launch red, hp, vp, maps;        // generic (fi_kernels.hip)
-  size_t prep_off = 0, hv_off = 0, hm_off = 0;  // k_sc_vmaps / k_sc_hrows / k_sc_hmfma
+  size_t prep_off = 0, hv_off = 0, hm_off = 0, vq_off = 0;  // k_sc_vmaps / k_sc_hrows / k_sc_hmfma / k_sc_vq
   int nprep = 0, nhv = 0, nhm = 0, h_chunks = 0, h_lds = 0, hm_chunks = 0, hm_lds = 0, v_chunks = 0, v_lds = 0;
+  int nvq = 0, vq_chunks = 0, vq_lds = 0;
   size_t sl_off = 0, sg_off = 0;   // k_sc_score2 with maps in LDS / global
   int nsl = 0, nsg = 0, sl_px = 0;
   size_t crops_off = 0;
@@ -646,14 +663,20 @@ struct ScLaunches {
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> prep, hv, hm, sl, sg;
+  std::vector<ScDesc> prep, hv, hm, sl, sg, vq;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
     const ScDesc &d = SL.descs[k];
     const ScPlan &P = *SL.plans[k];
     if (d.red) sred.push_back((int)k);
     if (d.prep) {
-      prep.push_back(d);
+      if (d.vq) {
+        vq.push_back(d);
+        X->vq_chunks = std::max(X->vq_chunks, P.vq_chunks);
+        X->vq_lds = std::max(X->vq_lds, P.vq_lds);
+      } else {
+        prep.push_back(d);
+      }
       if (d.hm) {
         hm.push_back(d);
         X->hm_chunks = std::max(X->hm_chunks, P.hm_chunks);
@@ -663,8 +686,10 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
         X->h_chunks = std::max(X->h_chunks, P.h_chunks);
         X->h_lds = std::max(X->h_lds, P.h_lds);
       }
-      X->v_chunks = std::max(X->v_chunks, P.v_chunks);
-      X->v_lds = std::max(X->v_lds, P.v_lds);
+      if (!d.vq) {
+        X->v_chunks = std::max(X->v_chunks, P.v_chunks);
+        X->v_lds = std::max(X->v_lds, P.v_lds);
+      }
     } else {
       if (d.hbuf) shp.push_back((int)k);
       if (d.pre) svp.push_back((int)k);
@@ -687,6 +712,8 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->nhv = (int)hv.size();
   X->hm_off = B.addv(hm);
   X->nhm = (int)hm.size();
+  X->vq_off = B.addv(vq);
+  X->nvq = (int)vq.size();
   X->sl_off = B.addv(sl);
   X->nsl = (int)sl.size();
   X->sg_off = B.addv(sg);
@@ -703,7 +730,8 @@ static int enqueue_sc(fi_ctx *c, uint8_t *ab, const ScLaunches &X, const int32_t
       hipLaunchKernelGGL(k_sc_reduce, dim3(X.red.tiles), dim3(256), 0, c->stream, desc(X.red), pre(X.red), X.red.n);
     if (launch_sc_h(c->stream, true, (const ScDesc *)(ab + X.hm_off), X.nhm, X.hm_chunks, X.hm_lds, ai) != 0 ||
         launch_sc_h(c->stream, false, (const ScDesc *)(ab + X.hv_off), X.nhv, X.h_chunks, X.h_lds, ai) != 0 ||
-        launch_sc_v(c->stream, (const ScDesc *)(ab + X.prep_off), X.nprep, X.v_chunks, X.v_lds, ai, PD) != 0)
+        launch_sc_v(c->stream, (const ScDesc *)(ab + X.prep_off), X.nprep, X.v_chunks, X.v_lds, ai, PD) != 0 ||
+        launch_sc_vq(c->stream, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0)
       return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d)", X.hm_lds, X.h_lds, X.v_lds);
     if (X.hp.tiles)
       hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, c->stream, desc(X.hp), pre(X.hp), X.hp.n, ai);
@@ -1640,6 +1668,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_ENABLE_MFMA_RS")) c->mfma_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
+  if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_MFMA")) c->sc_mfma = !(e[0] == '1');
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

@@ -101,6 +101,8 @@ struct ScDesc {
   int32_t hm;          // 1: horizontal pass by k_sc_hmfma (tables below), 0: k_sc_hrows
   int32_t hm_rows, hm_ks, hm_pitch, hm_nb;
   int32_t hmB, hmC, hmS0;  // arena offsets (int32 units; hmB 16-B aligned)
+  int32_t vq;              // 1: vertical pass + maps by k_sc_vq (tables below)
+  int32_t vqA, vqC, vqK0;  // arena offsets (int32 units; vqA 16-B aligned)
   uint8_t *red;        // reduce scratch rw*rh*3
   uint8_t *hbuf;       // H-pass scratch aw*hrows*3
   uint8_t *pre;        // prescaled image aw*ah*3
@@ -117,6 +119,7 @@ struct ScDesc {
 // apitch = 16-B rounded aw*3 (hbuf and LDS row pitch), spitch = 16-B rounded
 // source width*3.  LDS per workgroup <= kPrepMaxLds (host-checked).
 constexpr int kPrepRows = 16;
+constexpr int kVqRows = 14;  // k_sc_vq: analysed rows per workgroup (16 prescaled rows with the edge halo)
 constexpr int kPrepMaxLds = 64 * 1024;
 // k_sc_score2: maps resident in LDS when aw*ah*4 <= this; crops per image.
 constexpr int kScoreLdsMaps = 112 * 1024;

@@ -833,6 +833,46 @@ static void plan_sc_hmfma(ScPlan *p, int sw) {
   p->hm_ok = true;
 }
 
+// k_sc_vq tables: per chunk of kVqRows analysed rows, the 16 prescaled rows
+// [pa, pa + 16) (pa = y0 - 1 clamped) as one MFMA block over a window of <= 64
+// H-stage rows starting at vqK0; coefficients as three signed-byte limbs.
+static void plan_sc_vq(ScPlan *p) {
+  p->vq_ok = false;
+  if (!(p->thumb && p->need_h && p->need_v)) return;
+  const int ah = p->ah, chunks = (ah + kVqRows - 1) / kVqRows;
+  p->vqK0.assign(chunks, 0);
+  p->vqA.assign((size_t)chunks * 3 * 256, 0);
+  for (int c = 0; c < chunks; c++) {
+    const int y0 = kVqRows * c, pa = std::max(0, y0 - 1), pe = std::min(ah, pa + 16);
+    const int k0 = p->vb[2 * pa];
+    for (int y = pa; y < pe; y++)
+      if (p->vb[2 * y] < k0 || p->vb[2 * y] + p->vb[2 * y + 1] - k0 > 64) return;
+    p->vqK0[c] = k0;
+    for (int l = 0; l < 64; l++)
+      for (int j = 0; j < 16; j++) {
+        const int y = pa + (l & 15), k = k0 + mfma_i8_k(l, j);
+        int32_t w = 0;
+        if (y < pe && k >= p->vb[2 * y] && k < p->vb[2 * y] + p->vb[2 * y + 1])
+          w = p->vk[(size_t)y * p->ksv + (k - p->vb[2 * y])];
+        int32_t limb[3];
+        limbs3(w, limb);
+        for (int q = 0; q < 3; q++)
+          reinterpret_cast<uint8_t *>(&p->vqA[((size_t)c * 3 + q) * 256])[l * 16 + j] = (uint8_t)(int8_t)limb[q];
+      }
+  }
+  p->vqC.assign(ah, 0);
+  for (int y = 0; y < ah; y++) {
+    int64_t sum = 0;
+    for (int j = 0; j < p->vb[2 * y + 1]; j++) sum += p->vk[(size_t)y * p->ksv + j];
+    p->vqC[y] = (int32_t)((1 << 21) + 128 * sum);
+  }
+  const int apitch = (p->aw * 3 + 15) / 16 * 16;
+  p->vq_lds = 64 * apitch + 16 * apitch + 16 * ((p->aw + 3) / 4 * 4);
+  if (p->vq_lds > kPrepMaxLds) return;
+  p->vq_chunks = chunks;
+  p->vq_ok = true;
+}
+
 void plan_sc_prep(ScPlan *p) {
   p->prep_ok = false;
   p->hkT.clear();
@@ -871,6 +911,7 @@ void plan_sc_prep(ScPlan *p) {
   if (vmax > kPrepMaxLds) return;
   p->v_lds = (int)vmax;
   p->prep_ok = true;
+  plan_sc_vq(p);
 }
 
 static double thirds(double x) {

@@ -136,6 +136,14 @@ struct ScPlan {
   std::vector<int32_t> hmB;   // [nb][ks][3 limbs] fragments of 64 lanes x 16 B (256 int32)
   std::vector<int32_t> hmC;   // [aw] 2^21 + 128 * sum_j k[x][j]  (pixels enter as p - 128)
   std::vector<int32_t> hmS0;  // [nb] first source column of the block's window (multiple of 16)
+  // k_sc_vq: Pillow's vertical pass as exact integer MFMA fused with the maps;
+  // one workgroup per kVqRows analysed rows (+1 halo row each side = one
+  // 16-row MFMA block), its H-stage window starts at vqK0[chunk] (<= 64 rows)
+  bool vq_ok = false;
+  int vq_chunks = 0, vq_lds = 0;
+  std::vector<int32_t> vqA;   // [chunk][3 limbs] fragments of 64 lanes x 16 B (256 int32)
+  std::vector<int32_t> vqC;   // [ah] 2^21 + 128 * sum_j k[y][j]
+  std::vector<int32_t> vqK0;  // [chunk] first H-stage row of the window
   std::vector<CropHost> crops;
 };
 void plan_sc_prep(ScPlan *p);

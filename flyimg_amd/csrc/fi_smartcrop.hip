@@ -306,6 +306,100 @@ __global__ __launch_bounds__(kPrepThreads) void k_sc_vmaps(const ScDesc *__restr
   }
 }
 
+// ---- k_sc_vq: Pillow's vertical pass (Resample.c ImagingResampleVertical_8bpc)
+// as exact integer MFMA, fused with analyse()'s maps.  One workgroup per
+// (image, chunk of kVqRows analysed rows): the chunk's 16 prescaled rows
+// (with the one-row edge halo) are ONE 16-row MFMA block over a window of <= 64
+// H-stage rows; N = 16 interleaved channel bytes per tile (the vertical pass
+// never mixes columns).  sum = D0 + 256 D1 + 65536 D2 + C[y] is Pillow's int32
+// accumulator bit for bit (pixels enter as p - 128, C = 2^21 + 128 sum k).
+// Luma is computed once per prescaled pixel into LDS for the 3x3 edge filter.
+typedef __attribute__((address_space(3))) i32x2 l_i32x2q;
+__global__ __launch_bounds__(kPrepThreads) void k_sc_vq(const ScDesc *__restrict__ descs,
+                                                        const int32_t *__restrict__ ai, const ScParamsDev P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const ScDesc &D = descs[blockIdx.x];
+  const int c = blockIdx.y;
+  const int aw = D.aw, ah = D.ah;
+  const int y0 = kVqRows * c;
+  if (y0 >= ah) return;
+  const int y1 = min(y0 + kVqRows, ah), pa = max(0, y0 - 1), pe = min(ah, pa + 16);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int apitch = (aw * 3 + 15) & ~15, lpitch = (aw + 3) & ~3;
+  uint8_t *stg = lds8;                    // [64][apitch] H-stage rows as p - 128
+  uint8_t *prer = lds8 + 64 * apitch;     // [16][apitch] prescaled rows pa..pe-1
+  uint8_t *lum = prer + 16 * apitch;      // [16][lpitch] their luma
+  const int k0 = ai[D.vqK0 + c], hrows = D.hrows;
+  // ---- stage the window (rows past the H stage are zero-weight: any bytes)
+  const int nq = apitch >> 4;
+  for (int it = tid; it < 64 * nq; it += kPrepThreads) {
+    const int r = it / nq, q = it - r * nq;
+    const int hr = min(k0 + r, hrows - 1);
+    uint4 v = reinterpret_cast<const uint4 *>(D.hbuf + (int64_t)hr * apitch)[q];
+    v.x ^= 0x80808080u;
+    v.y ^= 0x80808080u;
+    v.z ^= 0x80808080u;
+    v.w ^= 0x80808080u;
+    reinterpret_cast<uint4 *>(stg + r * apitch)[q] = v;
+  }
+  const i32x4 *af = reinterpret_cast<const i32x4 *>(ai + D.vqA) + (size_t)c * 3 * 64;
+  const i32x4 A0 = af[lane], A1 = af[64 + lane], A2 = af[128 + lane];
+  int32_t cy[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) cy[i] = ai[D.vqC + min(pa + 4 * (lane >> 4) + i, ah - 1)];
+  __syncthreads();
+  // ---- vertical pass: tiles of 16 byte columns over the waves
+  const int rA = 16 * (lane >> 4) + ((lane & 15) >> 1);
+  const uint8_t *pA = stg + rA * apitch + 8 * (lane & 1), *pB = pA + 8 * apitch;
+  const int nbytes = 3 * aw;
+  for (int t = wave; t < nq; t += kPrepThreads / 64) {
+    const i32x2 lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pA + 16 * t));
+    const i32x2 hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pB + 16 * t));
+    const i32x4 B = {lo.x, lo.y, hi.x, hi.y};
+    const i32x4 d2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+    const i32x4 d1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, B, d2 << 8, 0, 0, 0);
+    const i32x4 d0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+    const int col = 16 * t + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int m = 4 * (lane >> 4) + i;
+      // modular int32: the limbs' partial products may wrap, the sum fits
+      const int32_t sv = (int32_t)((uint32_t)d0[i] + ((uint32_t)d1[i] << 8) + (uint32_t)cy[i]);
+      if (col < nbytes && pa + m < pe) prer[m * apitch + col] = pil_clip8(sv);
+    }
+  }
+  __syncthreads();
+  // ---- luma of every prescaled pixel (and the prescaled image when kept)
+  const int nr = pe - pa;
+  for (int it = tid; it < nr * aw; it += kPrepThreads) {
+    const int m = it / aw, x = it - m * aw;
+    const uint8_t *q = prer + m * apitch + 3 * x;
+    lum[m * lpitch + x] = (uint8_t)sc_luma(q[0], q[1], q[2]);
+    const int y = pa + m;
+    if (D.pre && y >= y0 && y < y1) {
+      uint8_t *o = D.pre + ((int64_t)y * aw + x) * 3;
+      o[0] = q[0];
+      o[1] = q[1];
+      o[2] = q[2];
+    }
+  }
+  __syncthreads();
+  // ---- maps of the chunk's rows: detect_edge (ImagingFilter3x3 interior,
+  // border copies L), skin and saturation
+  for (int it = tid; it < (y1 - y0) * aw; it += kPrepThreads) {
+    const int yr = it / aw, x = it - yr * aw, y = y0 + yr, m = y - pa;
+    const uint8_t *lrow = lum + m * lpitch;
+    const uint32_t L = lrow[x];
+    uint32_t E = L;
+    if (aw >= 3 && ah >= 3 && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
+      const int v = 4 * (int)L - (int)lrow[x - lpitch] - (int)lrow[x + lpitch] - (int)lrow[x - 1] - (int)lrow[x + 1] + 1;
+      E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
+    }
+    const uint8_t *q = prer + m * apitch + 3 * x;
+    D.maps[(int64_t)y * aw + x] = sc_skin_sat(q[0], q[1], q[2], L, P) | (E << 8);
+  }
+}
+
 // ---------------------------------------------------------------------------
 constexpr int kScoreThreads = 1024;
 constexpr int kScoreWaves = kScoreThreads / 64;
@@ -566,6 +660,13 @@ int launch_sc_h(hipStream_t s, bool mfma, const ScDesc *descs, int n, int chunks
     hipLaunchKernelGGL(k_sc_hmfma, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai);
   else
     hipLaunchKernelGGL(k_sc_hrows, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai);
+  return 0;
+}
+int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
+                 const ScParamsDev &P) {
+  if (n <= 0) return 0;
+  if (lds > kPrepMaxLds) return -1;
+  hipLaunchKernelGGL(k_sc_vq, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai, P);
   return 0;
 }
 int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,

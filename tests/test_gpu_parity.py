@@ -45,12 +45,12 @@ def _context_with(env):
 
 
 _ENV = {"FI_DISABLE_FUSED": "0", "FI_ENABLE_MFMA_RS": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0",
-        "FI_DISABLE_VM_RS": "0"}
+        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0"}
 PATHS = {
     # default kernels: k_rs_vm streaming MFMA resample; k_sc_hmfma + k_sc_vmaps prescale; k_sc_score2
     "vm": dict(_ENV),
-    # VALU fused resample (k_rs_fused)
-    "valu": dict(_ENV, FI_DISABLE_VM_RS="1"),
+    # VALU fused resample (k_rs_fused); VALU vertical prescale + maps (k_sc_vmaps)
+    "valu": dict(_ENV, FI_DISABLE_VM_RS="1", FI_DISABLE_SC_VQ="1"),
     # exact-integer MFMA resample (opt-in) with the VALU horizontal prescale (k_sc_hrows)
     "mfma": dict(_ENV, FI_ENABLE_MFMA_RS="1", FI_DISABLE_SC_MFMA="1"),
     # generic kernels: two-pass resample; per-row prescale/maps kernels
