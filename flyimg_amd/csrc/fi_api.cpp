@@ -866,7 +866,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           // strips of <= 64 px; narrower when the horizontal fragments would not
           // leave room for two workgroups per CU
           MfmaH m;
-          for (int mx : {kVmMaxNx, 48, 32}) {
+          static const int first_nx = getenv("FI_VM_MAXNX") ? atoi(getenv("FI_VM_MAXNX")) : kVmMaxNx;  // tuning
+          for (int mx : {first_nx, 48, 32}) {
             if (!build_mfma_h(*ht, &m, mx)) {
               m = MfmaH();
               break;
