@@ -56,7 +56,7 @@ size_t mfma_lds_bytes(int nblocks);
 int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const MTile *tiles, int ntiles,
                 const int32_t *ai, size_t lds);
 // streaming exact-integer MFMA resample (fi_vm.hip)
-size_t vm_lds_bytes(int nocb, int ks);
+size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16);
 int vm_read_stamps(uint64_t *out, int slots);
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
@@ -168,7 +168,7 @@ struct fi_ctx {
   bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
   bool sc_vq = true;        // FI_DISABLE_SC_VQ=1: k_sc_vmaps (VALU vertical pass) instead of k_sc_vq
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
-  std::map<const AxisTable *, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
+  std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
   bool sc_mfma = true;  // FI_DISABLE_SC_MFMA=1: VALU horizontal pass (k_sc_hrows) instead of k_sc_hmfma
 };
@@ -861,7 +861,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           if (!build_vm_v(*vt, &m)) m = VmV();
           vit = c->vmv_cache.emplace(vt, std::move(m)).first;
         }
-        auto hit = c->vmh_cache.find(ht);
+        // the Q16 output tile (gray / rotation) needs more LDS than the 8-bit one
+        const bool q16 = P.gray || P.rot != 0;
+        auto hit = c->vmh_cache.find({ht, q16});
         if (hit == c->vmh_cache.end()) {
           // strips of <= 64 px; narrower when the horizontal fragments would not
           // leave room for two workgroups per CU
@@ -873,11 +875,11 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
               break;
             }
             bool fits = true;
-            for (const MfmaStrip &st : m.strips) fits = fits && vm_lds_bytes(st.nocb, st.ks) <= kVmMaxLds;
+            for (const MfmaStrip &st : m.strips) fits = fits && vm_lds_bytes(st.vpitch, st.nocb, st.ks, q16) <= kVmMaxLds;
             if (fits) break;
             m = MfmaH();
           }
-          hit = c->vmh_cache.emplace(ht, std::move(m)).first;
+          hit = c->vmh_cache.emplace(std::make_pair(ht, q16), std::move(m)).first;
         }
         if (vit->second.nblk > 0 && !hit->second.strips.empty()) {
           vv = &vit->second;
@@ -1270,11 +1272,13 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           m.frag = frag + (int32_t)st.frag;
           m.s0 = s0 + (int32_t)st.s0;
           m.lut = lut + (int32_t)st.lut;
+          m.vpitch = st.vpitch;
           vstrips.push_back(m);
-          vm_lds = std::max(vm_lds, vm_lds_bytes(st.nocb, st.ks));
         }
         hp = hplaced.emplace(&H, std::make_pair(first, hw)).first;
       }
+      for (const MfmaStrip &st : H.strips)  // the workgroup's LDS layout follows its strip and tile kind
+        vm_lds = std::max(vm_lds, vm_lds_bytes(st.vpitch, st.nocb, st.ks, d.gray || d.rot != 0));
       VDesc m{};
       m.src = d.src;
       m.src_stride = d.src_stride;

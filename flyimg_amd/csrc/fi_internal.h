@@ -155,6 +155,7 @@ struct MStrip {               // one column strip (fi_plan.h MfmaStrip) placed i
   int32_t c_lo, ncols, pitch, nocb, ks;
   int32_t lut_px0, lut_n;
   int32_t frag, s0, lut;      // arena offsets (int32 units; frag 16-B aligned)
+  int32_t vpitch;             // k_rs_vm: Q16 plane columns (multiple of 16)
 };
 struct MTile {                // one workgroup: image x strip x band [yb0, yb1) of 16-row blocks
   int32_t img, strip, yb0, yb1;
@@ -189,16 +190,17 @@ struct VTile {                // one workgroup: image x strip x pieces [p0, p1);
   int32_t img, strip, p0, p1, emit0, pad;
 };
 constexpr int kVmThreads = 512;      // 8 waves x 4 column tiles of 16 B = 512-B strips
-constexpr int kVmPitch = 528;        // LDS row pitch of the piece buffer (16 x odd: rows 4 banks apart)
-// byte c of row r lives at r * pitch + (c ^ (128 * ((r >> 4) & 1))): the two
-// 8-row groups of a ds_read_b64_tr_b8 half-wave (rows 16 apart) land 32 banks apart
-constexpr int kVmChunkBytes = 64 * kVmPitch;
-constexpr int kVmMaxLds = 80 * 1024;  // two workgroups per CU
-constexpr int kVmPlane = kMfmaPitch * 16;       // one Q16 limb plane: [column <= kMfmaPitch][16 rows]
-constexpr int kVmPlaneBytes = 6 * kVmPlane;     // [hi, lo][3 channels]
+// piece buffer: 64 rows x 512 B; 16-byte chunk c of row r at r * 512 + 16 (c ^ f(r)),
+// f(r) = (r & 7) | 8 ((r >> 4) & 1): the 8 rows of a ds_read_b64_tr_b8 quarter
+// wave hit 8 different chunk columns and the two 8-row groups of a half-wave
+// (rows 16 apart) the two halves of the banks
+constexpr int kVmChunkBytes = 64 * 512;
+constexpr int kVmABytes = 6 * 1024 + 64;  // the piece's A fragments [slot][limb][64 lanes][16 B] + 16 w128 rows
+constexpr int kVmMaxLds = 80 * 1024;      // two workgroups per CU
 constexpr int kVmOtilePitch = 64 * 3 + 4;      // Q16 output tile row, u16 units (nx <= kVmMaxNx = 64)
 constexpr int kVmOtileBytes = 16 * kVmOtilePitch * 2;
-constexpr int kVmOtile8Pitch = 64 * 3 + 4;     // 8-bit tile row (fast RGB path), aliases the Q16 tile
+constexpr int kVmOtile8Pitch = 64 * 3 + 4;     // 8-bit tile row (fast RGB path)
+constexpr int kVmOtile8Bytes = 16 * kVmOtile8Pitch;
 
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;

@@ -395,6 +395,7 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
     if (getenv("FI_DEBUG_MFMA_PITCH")) fprintf(stderr, "strip %d..%d ncols %d pitch %d\n", x0, x1, S.ncols, S.pitch);
     if (S.pitch > kMfmaPitch) return false;
     S.pitch = kMfmaPitch;
+    S.vpitch = (pitch + 15) / 16 * 16;
     S.lut_px0 = S.b0 / 3;
     S.lut_n = (S.b0 + S.nbytes + 2) / 3 - S.lut_px0;
     S.lut = m->lut.size();

@@ -71,6 +71,7 @@ struct MfmaStrip {                     // one column strip of the horizontal pas
   int32_t x0, x1;                      // output px [x0, x1)
   int32_t b0, nbytes;                  // source bytes loaded (16-B aligned)
   int32_t c_lo, ncols, pitch;          // compacted touched columns of the strip, LDS plane pitch
+  int32_t vpitch;                      // k_rs_vm plane columns: covers every fragment window, multiple of 16
   int32_t nocb, ks;                    // 16-px output blocks, k-steps of 64 columns
   int32_t lut_px0, lut_n;              // px -> compact column LUT over [lut_px0, lut_px0 + lut_n)
   size_t frag, s0, lut;                // offsets into MfmaH::frag / s0 / lut

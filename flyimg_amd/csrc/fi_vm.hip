@@ -8,16 +8,19 @@
 // loads of a piece (two full 512-byte row segments per wave-instruction);
 // piece p+1 is in flight in registers while piece p is computed.
 //
-//   piece buffer  64 rows x 512 B in LDS (pixels as p - 128), byte c of row
-//                 r at r * 528 + (c ^ 128 ((r >> 4) & 1)): the
-//                 ds_read_b64_tr_b8 transposing reads of both 8-row groups
-//                 of a half-wave hit disjoint banks.
+//   piece buffer  64 rows x 512 B in LDS (pixels as p - 128), 16-byte chunk
+//                 c of row r at r * 512 + 16 (c ^ f(r)) (fi_internal.h): the
+//                 ds_read_b64_tr_b8 transposing reads hit disjoint banks.
+//   A fragments   the piece's vertical weight fragments (6 KB) and the w128
+//                 rows of block + 2 are fetched once per workgroup (one
+//                 16-byte load per lane of waves 0-6, one piece ahead) and
+//                 shared through LDS, not fetched by each wave.
 //   vertical      wave w owns byte columns [64 w, 64 w + 64) = 4 tiles of
 //                 16.  Per tile: B = 2 tr8 reads (64 rows x 16 columns);
 //                 two accumulator slots -- the block the piece belongs to and
 //                 the next one (whose window starts inside it) -- each 3
 //                 MFMAs (weight limbs L0 + 256 L1 + 65536 L2, A fragments
-//                 from the host table) folded into one int32 accumulator:
+//                 from LDS) folded into one int32 accumulator:
 //                 acc += A0 B + ((A1 B + ((A2 B) << 8)) << 8), exact.
 //   block done    ClampToQuantum(257 * acc / 2^22) -> Q16 hi/lo byte planes
 //                 per channel, compacted to the touched columns, stored
@@ -88,7 +91,8 @@ __device__ __forceinline__ int32_t vm_fold3(int32_t d0, int32_t d1, int32_t d2) 
 
 // per-workgroup phase sums of MODE 9 (read by fi_debug_vm_stamps)
 constexpr int kVmStampSlots = 4096;
-__device__ uint64_t g_vm_stamps[kVmStampSlots * 9];
+constexpr int kVmStampN = 12;  // phase sums + piece count per workgroup
+__device__ uint64_t g_vm_stamps[kVmStampSlots * (kVmStampN + 1)];
 
 // MODE (profiling ablations, FI_VM_VARIANT; wrong pixels): 0 production,
 // 1 loads + LDS writes only, 2 no horizontal pass / epilogue, 3 no stores,
@@ -106,17 +110,20 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
   const MStrip S = strips[T.strip];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  // LDS: [piece buffer][Q16 planes [limb][ch][column][16 rows]][Q16 tile][horizontal fragments]
-  uint8_t *vpl = lds + kVmChunkBytes;
-  uint16_t *otile = reinterpret_cast<uint16_t *>(vpl + kVmPlaneBytes);          // [16][kVmOtilePitch] Q16
-  i32x4 *hbl = reinterpret_cast<i32x4 *>(vpl + kVmPlaneBytes + kVmOtileBytes);  // [nocb][ks][3][64]
   const int oc = D.gray ? 1 : 3;
   const int nx = S.x1 - S.x0;
   // RGB without rotation: the horizontal pass writes final bytes into an 8-bit
   // tile whose row yl starts at byte sh(yl) = (destination address of the row
   // segment) & 3, so the stores are plain dword copies; otherwise a Q16 tile.
   const bool fast8 = !D.gray && D.rot == 0;
-  uint8_t *otile8 = reinterpret_cast<uint8_t *>(otile);  // [16][kVmOtile8Pitch] (aliases the Q16 tile)
+  // LDS (vm_lds_bytes): [piece buffer][A fragments, w128][Q16 planes [limb][ch][column][16 rows]]
+  //                     [output tile: 8-bit or Q16][horizontal fragments]
+  uint8_t *apl = lds + kVmChunkBytes;
+  uint8_t *vpl = apl + kVmABytes;
+  const int plane = 16 * S.vpitch;  // one limb plane of one channel
+  uint16_t *otile = reinterpret_cast<uint16_t *>(vpl + 6 * plane);  // [16][kVmOtilePitch] Q16
+  uint8_t *otile8 = vpl + 6 * plane;                                 // [16][kVmOtile8Pitch]
+  i32x4 *hbl = reinterpret_cast<i32x4 *>(vpl + 6 * plane + (fast8 ? kVmOtile8Bytes : kVmOtileBytes));  // [nocb][ks][3][64]
   const uint32_t sh0 = (uint32_t)(((uintptr_t)D.dst + (uint64_t)S.x0 * 3) & 3u);
   const uint32_t shs = (uint32_t)(D.dst_stride & 3);
   auto row_sh = [&](int y) -> int { return (int)((sh0 + (uint32_t)y * shs) & 3u); };
@@ -132,7 +139,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
     const int col = 64 * wave + 16 * j + (lane & 15);
     const int abs = S.b0 + min(col, S.nbytes - 1), px = abs / 3, chn = abs - 3 * px;
     const int ci = lut[px - S.lut_px0];
-    const int o = (col < S.nbytes && ci >= 0) ? chn * kVmPlane + vm_col_off(ci) + 4 * (lane >> 4) : 0xFFFF;
+    const int o = (col < S.nbytes && ci >= 0) ? chn * plane + vm_col_off(ci) + 4 * (lane >> 4) : 0xFFFF;
     if (j & 1)
       vcolp[j >> 1] |= (uint32_t)o << 16;
     else
@@ -170,16 +177,17 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
       v[i] = *(g_u32x4v *)(sb + (hi_row ? o1 : o0));
     }
   };
-  // A fragments of piece p: [slot][limb], and the w128 rows of block pblk(p) + 2
-  // (w128 is padded with two zero blocks: the load is unconditional)
+  // A fragments of piece p ([slot][limb][lane], 384 x 16 B) and the w128 rows
+  // of block pblk(p) + 2 (4 x 16 B; w128 is padded with two zero blocks): one
+  // 16-byte load per thread < 388, staged into LDS at the top of the piece
+  // (the other lanes repeat a fragment load: every wave issues exactly one)
   const g_i32x4 *vfrag = (const g_i32x4 *)(ai + D.frag);
-  const g_i32x4 *w128 = (const g_i32x4 *)(ai + D.w128) + (lane >> 4);
-  auto load_a = [&](int p, int blk, i32x4 (&A)[2][3], i32x4 &w2) {
-#pragma unroll
-    for (int s2 = 0; s2 < 2; s2++)
-#pragma unroll
-      for (int q = 0; q < 3; q++) A[s2][q] = vfrag[((size_t)(2 * p + s2) * 3 + q) * 64 + lane];
-    w2 = w128[4 * (blk + 2)];
+  const g_i32x4 *w128g = (const g_i32x4 *)(ai + D.w128);
+  const g_i32x4 *w128 = w128g + (lane >> 4);
+  auto load_a = [&](int p, int blk) -> i32x4 {
+    const g_i32x4 *a = tid < 384 ? vfrag + (size_t)p * 384 + tid
+                                 : (tid < 388 ? w128g + 4 * (blk + 2) + (tid - 384) : vfrag + (size_t)p * 384);
+    return *a;
   };
 
   // accumulators: slot 0 = block pblk(p0), slot 1 = the next block
@@ -193,16 +201,19 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
       acc1[j] = w1;
     }
   }
-  i32x4 A[2][3], W2;
   i32x4m mc = pmeta[T.p0];
+  i32x4 aq = load_a(T.p0, mc.z);
   issue(mc);
 
   // transposing-read offsets: lane reads rows 16 (l >> 4) + (l & 15) / 2 (+8), bytes 8 (l & 1)
   // (rows rA and rA + 8 share the 16-row group (lane >> 4): same column swizzle)
+  // (rows rA and rA + 8 have the same chunk swizzle f)
   const int rA = 16 * (lane >> 4) + ((lane & 15) >> 1);
-  const int csw = ((64 * wave) ^ (128 * ((lane >> 4) & 1))) + 8 * (lane & 1);
-  const int offA = rA * kVmPitch + csw, offB = (rA + 8) * kVmPitch + csw;
-  const int woff_st = rs * kVmPitch;  // row 16 i + rs: group i, column swizzle below
+  const int fA = (rA & 7) | (((rA >> 4) & 1) << 3);
+  int offA[kVmTiles];
+#pragma unroll
+  for (int j = 0; j < kVmTiles; j++) offA[j] = rA * 512 + 16 * ((4 * wave + j) ^ fA) + 8 * (lane & 1);
+  const int woff_st = rs * 512;  // row 16 i + rs: f = (rs & 7) | 8 (i & 1)
 
   // ---- epilogue of a completed block (run one piece later, before that
   // piece's loads are issued, so the stores never sit behind a prefetch in
@@ -276,7 +287,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
 
   int pend = -1;  // block whose Q16 tile waits in otile for its stores
   constexpr bool kStamp = MODE == 9;
-  uint64_t tsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = 0;
+  uint64_t tsum[kVmStampN] = {}, tprev = 0;
   auto stamp = [&](int k) {
     if (kStamp) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -294,29 +305,36 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
 #pragma unroll
     for (int i = 0; i < kVmLoads; i++) {
       const u32x4v x = v[i] ^ u32x4v{0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
-      // row 16 i + rs (rs < 16): its 16-row group is i, a compile-time column swizzle
-      *reinterpret_cast<u32x4v *>(lds + woff_st + 16 * i * kVmPitch + ((16 * c16) ^ (128 * (i & 1)))) = x;
+      const int f = (rs & 7) | ((i & 1) << 3);
+      *reinterpret_cast<u32x4v *>(lds + woff_st + 16 * i * 512 + 16 * (c16 ^ f)) = x;
     }
+    if (tid < 388) *reinterpret_cast<i32x4 *>(apl + 16 * tid) = aq;
     stamp(2);
     if ((MODE == 0 || MODE == 4 || MODE == 9) && pend >= 0) {
       store_block(pend);
       pend = -1;
     }
     stamp(7);
-    // this piece's weight fragments, then the next piece's source rows (in
-    // flight during compute; the fragments are waited for with vmcnt(4))
-    // (unconditional: the last piece re-issues itself, an L2 hit, so the
-    // count of younger loads -- and so every vmcnt -- is the same on all paths)
-    load_a(p, mc.z, A, W2);
+    // the next piece's weight fragments and source rows, in flight during
+    // compute (unconditional: the last piece re-issues itself, an L2 hit, so
+    // the count of outstanding loads -- and so every vmcnt -- is the same on all paths)
+    aq = load_a(min(p + 1, T.p1 - 1), mn.z);
     issue(mn);
     stamp(3);
     __syncthreads();
     stamp(4);
     const bool last = mc.w != 0;
+    const i32x4 *al = reinterpret_cast<const i32x4 *>(apl);
+    const i32x4 W2 = al[384 + (lane >> 4)];
     if (MODE != 1) {
+      i32x4 A[2][3];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+        for (int q = 0; q < 3; q++) A[s2][q] = al[(s2 * 3 + q) * 64 + lane];
 #pragma unroll
       for (int j = 0; j < kVmTiles; j++) {
-        const i32x2 lo = vm_tr8(lds + offA + 16 * j), hi = vm_tr8(lds + offB + 16 * j);
+        const i32x2 lo = vm_tr8(lds + offA[j]), hi = vm_tr8(lds + offA[j] + 8 * 512);
         const i32x4 B = {lo.x, lo.y, hi.x, hi.y};
         {
           const i32x4 d2 = vm_mfma(A[0][2], B, i32x4{0, 0, 0, 0});
@@ -351,9 +369,11 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
           const uint32_t x01 = __builtin_bit_cast(uint32_t, p01) ^ 0x80808080u;
           const uint32_t x23 = __builtin_bit_cast(uint32_t, p23) ^ 0x80808080u;
           *reinterpret_cast<uint32_t *>(vpl + o) = __builtin_amdgcn_perm(x23, x01, 0x07050301u);
-          *reinterpret_cast<uint32_t *>(vpl + o + 3 * kVmPlane) = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
+          *reinterpret_cast<uint32_t *>(vpl + o + 3 * plane) = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
         }
+        stamp(8);
         __syncthreads();
+        stamp(9);
         // ---- horizontal: items (16-px output block, channel) over the waves
         if (MODE != 4) {
           for (int it = wv; it < 3 * S.nocb; it += kVmWaves) {
@@ -362,7 +382,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
             i32x4 hh[3], hl[3];
 #pragma unroll
             for (int q = 0; q < 3; q++) hh[q] = hl[q] = i32x4{0, 0, 0, 0};
-            const uint8_t *ph = vpl + chn * kVmPlane, *pl = ph + 3 * kVmPlane;
+            const uint8_t *ph = vpl + chn * plane, *pl = ph + 3 * plane;
 #pragma unroll
             for (int t = 0; t < 2; t++) {
               if (t >= hks) break;
@@ -423,19 +443,22 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
     store_block(pend);
   }
   if (kStamp && tid == 0 && blockIdx.x < kVmStampSlots) {
-    for (int k = 0; k < 8; k++) g_vm_stamps[blockIdx.x * 9 + k] = tsum[k];
-    g_vm_stamps[blockIdx.x * 9 + 8] = (uint64_t)(T.p1 - T.p0);
+    for (int k = 0; k < kVmStampN; k++) g_vm_stamps[blockIdx.x * (kVmStampN + 1) + k] = tsum[k];
+    g_vm_stamps[blockIdx.x * (kVmStampN + 1) + kVmStampN] = (uint64_t)(T.p1 - T.p0);
   }
 }
 
 int vm_read_stamps(uint64_t *out, int slots) {
   if (slots > kVmStampSlots) slots = kVmStampSlots;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vm_stamps), (size_t)slots * 9 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vm_stamps), (size_t)slots * (kVmStampN + 1) * sizeof(uint64_t)) == hipSuccess
+             ? 0
+             : -1;
 }
 
-// piece buffer + Q16 planes + Q16 output tile + the strip's horizontal fragments
-size_t vm_lds_bytes(int nocb, int ks) {
-  return (size_t)kVmChunkBytes + kVmPlaneBytes + kVmOtileBytes + (size_t)nocb * ks * 3 * 1024;
+// piece buffer + A fragments + Q16 planes + output tile + the strip's horizontal fragments
+size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16) {
+  return (size_t)kVmChunkBytes + kVmABytes + (size_t)6 * 16 * vpitch + (q16 ? kVmOtileBytes : kVmOtile8Bytes) +
+         (size_t)nocb * ks * 3 * 1024;
 }
 
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,

@@ -36,15 +36,16 @@ with Context(0) as ctx:
     for _ in range(3):
         L.check(ctx.process_device(arr, n))
     import ctypes
-    buf = np.zeros(4096 * 9, np.uint64)
+    NS = 12
+    buf = np.zeros(4096 * (NS + 1), np.uint64)
     L.lib().fi_debug_vm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
     L.check(L.lib().fi_debug_vm_stamps(ctx.h, buf.ctypes.data, 4096))
-    rows = [r for r in buf.reshape(4096, 9) if 0 < r[8] < 1000]
+    rows = [r for r in buf.reshape(4096, NS + 1) if 0 < r[NS] < 1000]
     a = np.array(rows, dtype=np.float64)
-    tot = a[:, :8].sum(axis=1)
-    print(f"{len(a)} workgroups; pieces/WG {a[:, 8].mean():.1f}; total ticks/WG {tot.mean():.0f}")
-    names = ["tail/prev", "barrier1", "piece write", "A+row issue", "barrier2", "V-MFMA issue", "block phase",
-             "stores"]
-    for k in range(8):
+    tot = a[:, :NS].sum(axis=1)
+    print(f"{len(a)} workgroups; pieces/WG {a[:, NS].mean():.1f}; total ticks/WG {tot.mean():.0f}")
+    names = ["tail/prev", "barrier1", "piece write", "A+row issue", "barrier2", "V-MFMA issue", "H pass",
+             "stores", "planes+drain", "plane barrier", "-", "-"]
+    for k in range(NS):
         print(f"  {names[k]:14s} {a[:, k].mean():10.0f}  ({a[:, k].mean() / tot.mean() * 100:5.1f} %)  "
-              f"per piece {a[:, k].mean() / a[:, 8].mean():8.0f}")
+              f"per piece {a[:, k].mean() / a[:, NS].mean():8.0f}")
