@@ -145,6 +145,20 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
     else
       vcolp[j >> 1] = (uint32_t)o;
   }
+  // this wave's horizontal items it = wv + 8 k (k < 2: 3 nocb <= 12): fragment
+  // window start / k-steps (uniform) and the lane's weight-sum term, loaded once
+  // (a per-block global load here put an L2 round trip on every block)
+  int hw0k[2], hksk[2];
+  float hwsk[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int it = wv + kVmWaves * k, ob = it / 3;
+    const bool ok = it < 3 * S.nocb;
+    hw0k[k] = ok ? ai[S.s0 + 2 * ob] : 0;
+    hksk[k] = ok ? ai[S.s0 + 2 * ob + 1] : 0;
+    const int hx = 16 * ob + (lane & 15);
+    hwsk[k] = (ok && hx < nx) ? 32896.0f * (float)ai[D.hwsum + S.x0 + hx] : 0.0f;
+  }
   // the strip's horizontal B fragments, staged in LDS once
   {
     const g_i32x4 *hf = (const g_i32x4 *)(ai + S.frag);
@@ -376,9 +390,12 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
         stamp(9);
         // ---- horizontal: items (16-px output block, channel) over the waves
         if (MODE != 4) {
-          for (int it = wv; it < 3 * S.nocb; it += kVmWaves) {
+#pragma unroll
+          for (int k = 0; k < 2; k++) {
+            const int it = wv + kVmWaves * k;
+            if (it >= 3 * S.nocb) break;
             const int ob = it / 3, chn = it - 3 * ob;
-            const int hw0 = ai[S.s0 + 2 * ob], hks = ai[S.s0 + 2 * ob + 1];
+            const int hw0 = hw0k[k], hks = hksk[k];
             i32x4 hh[3], hl[3];
 #pragma unroll
             for (int q = 0; q < 3; q++) hh[q] = hl[q] = i32x4{0, 0, 0, 0};
@@ -402,7 +419,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
             const int hx = 16 * ob + (lane & 15);
             if (hx < nx) {
               // V = 256 (h - 128) + (l - 128) + 32896; ClampToQuantum
-              const float hws = 32896.0f * (float)ai[D.hwsum + S.x0 + hx];
+              const float hws = hwsk[k];
               uint16_t *o = otile + (4 * (lane >> 4)) * kVmOtilePitch + 3 * hx + chn;
 #pragma unroll
               for (int i = 0; i < 4; i++) {
