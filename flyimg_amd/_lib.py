@@ -150,6 +150,7 @@ def lib():
     L.fi_rccl_get_unique_id.argtypes = [ctypes.c_char_p]
     L.fi_rccl_init.argtypes = [vp, i32, i32, ctypes.c_char_p]
     L.fi_rccl_gather_records.argtypes = [vp, P(FiRecord), i32, P(FiRecord)]
+    L.fi_debug_monochrome.argtypes = [vp, vp, i32, i32, i32, vp, i32]
     _lib = L
     return L
 

@@ -55,6 +55,9 @@ __global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
 size_t mfma_lds_bytes(int nblocks);
 int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const MTile *tiles, int ntiles,
                 const int32_t *ai, size_t lds);
+// -monochrome (fi_mono.hip)
+size_t mono_lds_bytes();
+int launch_mono(hipStream_t s, const MonoDesc *descs, int n, const double *wts);
 // streaming exact-integer MFMA resample (fi_vm.hip)
 size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16);
 int vm_read_stamps(uint64_t *out, int slots);
@@ -793,6 +796,14 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   std::vector<const MfmaH *> vm_h;
   // per image resized-buffer workspace offsets (for smartcrop-apply)
   std::vector<size_t> res_off(n, 0);
+  // final 8-bit output of each image (dst or the apply workspace, tagged); differs
+  // from its ResizeDesc dst only for -monochrome images (Q16 gray scratch)
+  std::vector<uint8_t *> out_of(n, nullptr);
+  struct MonoItem {
+    int img;
+    size_t g_off, st_off;
+  };
+  std::vector<MonoItem> mono;
   double resize_bytes = 0;
   for (int i = 0; i < n; i++) {
     fi_image &im = imgs[i];
@@ -840,6 +851,20 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     } else {
       d.dst = im.dst;
     }
+    out_of[i] = d.dst;
+    if (P.mono) {
+      // the resample epilogue writes the extent window's Q16 gray, unrotated;
+      // fi_mono.hip quantizes it and writes the rotated 0/255 output
+      MonoItem m;
+      m.img = i;
+      m.g_off = E.work.take((size_t)P.ew * P.eh * 2);
+      m.st_off = E.work.take(sizeof(MonoState));
+      mono.push_back(m);
+      d.dst = (uint8_t *)(uintptr_t)(m.g_off + 1);
+      d.dst_stride = (int64_t)P.ew * 2;
+      d.gray = 2;
+      d.rot = 0;
+    }
     int64_t src_bytes = 0;
     if (!P.resize) {
       d.mode = 0;
@@ -886,7 +911,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           vh = &hit->second;
         }
       }
-      if (!vv && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0) {
+      if (!vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
+          (im.src_stride % 16) == 0) {
         auto vit = c->mv_cache.find(vt);
         if (vit == c->mv_cache.end()) {
           MfmaV m;
@@ -905,8 +931,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         }
       }
       const RingTable *ring = nullptr;
-      if (!vv && !mv && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0 &&
-          d.h.maxtaps <= 64) {
+      if (!vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
+          (im.src_stride % 16) == 0 && d.h.maxtaps <= 64) {
         auto rit = c->ring_cache.find(vt);
         if (rit == c->ring_cache.end()) {
           RingTable rt;
@@ -1018,8 +1044,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     if (sc_of[i] >= 0) {
       // smartcrop input: the resized image (workspace if apply, else dst)
       ScItem &it = sitems[sc_of[i]];
-      const ResizeDesc &d = rd[rd_of[i]];
-      it.img = d.dst;  // may still be a workspace offset (+1 tagged); fixed below
+      it.img = out_of[i];  // may still be a workspace offset (+1 tagged); fixed below
     }
   plan_smartcrop(c, E, sitems, &SL, &sstatus, &serrs, false);
   const size_t results_off = E.work.take(sizeof(ScResult) * std::max<size_t>(sitems.size(), 1));
@@ -1034,7 +1059,24 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     ResizeDesc &d = rd[rd_of[i]];
     if (d.mid) fix_ptr(d.mid, wb);
     const bool apply = (imgs[i].flags & FI_OP_SMARTCROP) && (imgs[i].flags & FI_OP_SMARTCROP_APPLY);
-    if (apply) fix_ptr(d.dst, wb);
+    if (apply) fix_ptr(out_of[i], wb);
+    if (d.gray == 2)
+      fix_ptr(d.dst, wb);
+    else
+      d.dst = out_of[i];
+  }
+  std::vector<MonoDesc> mdesc_mono;
+  for (const MonoItem &m : mono) {
+    const ResizeDesc &d = rd[rd_of[m.img]];
+    MonoDesc md{};
+    md.g = (const uint16_t *)(wb + m.g_off);
+    md.w = d.ew;
+    md.h = d.eh;
+    md.rot = plans[m.img].rot;
+    md.dst = out_of[m.img];
+    md.dst_stride = imgs[m.img].out_stride;
+    md.st = (MonoState *)(wb + m.st_off);
+    mdesc_mono.push_back(md);
   }
   for (size_t k = 0; k < SL.descs.size(); k++) {
     ScDesc &d = SL.descs[k];
@@ -1044,7 +1086,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     fix_ptr(d.maps, wb);
   }
   for (int i = 0; i < n; i++)
-    if (sc_of[i] >= 0) SL.descs[sc_of[i]].img = rd[rd_of[i]].dst;
+    if (sc_of[i] >= 0) SL.descs[sc_of[i]].img = out_of[i];
   // ---- build launches
   std::vector<int> m0, m1, m2;
   for (size_t k = 0; k < rd.size(); k++) {
@@ -1354,8 +1396,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     if (sstatus[sc_of[i]] != FI_OK) continue;
     const ResizeDesc &d = rd[rd_of[i]];
     ApplyDesc a{};
-    a.src = d.dst;
-    a.src_stride = d.dst_stride;
+    a.src = out_of[i];
+    a.src_stride = imgs[i].out_stride;
     a.W = d.out_w;
     a.H = d.out_h;
     a.C = d.out_c;
@@ -1367,6 +1409,21 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     apply_img.push_back(i);
   }
   const size_t apply_off = B.addv(apply);
+  const size_t mono_off = B.addv(mdesc_mono);
+  size_t mono_wts = 0;
+  if (!mono.empty()) {
+    // the Riemersma error-queue weights (quantize.c), computed with libm at run
+    // time exactly as oracle/fi_oracle.c does
+    mono_wts = E.ad.size();
+    volatile double qr1 = 65535.0 + 1.0, span = 16 - 1.0;
+    const double step = exp(log((double)qr1) / (double)span);
+    double weight = 1.0, wts[16];
+    for (int k = 0; k < 16; k++) {
+      wts[16 - k - 1] = 1.0 / weight;
+      weight *= step;
+    }
+    E.ad.insert(E.ad.end(), wts, wts + 16);
+  }
   const size_t ai_off = B.addv(E.ai), af_off = B.addv(E.af), ad_off = B.addv(E.ad);
   // ---- upload (pinned slot: the previous batch may still be running)
   const int slot = c->next_slot;
@@ -1429,6 +1486,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         hipLaunchKernelGGL(k_rs_v_final, dim3(L2b.tiles), dim3(256), 0, c->stream,
                            (const ResizeDesc *)desc_p(L2b), pre_p(L2b), L2b.n, ai, af);
       }
+    }
+    if (!mono.empty()) {
+      Timer t(c, "mono", 0);
+      (void)launch_mono(c->stream, (const MonoDesc *)(ab + mono_off), (int)mono.size(), ad + mono_wts);
     }
     HIP_TRY(hipGetLastError());
     if (any_sc) {
@@ -1648,6 +1709,52 @@ int fi_debug_vm_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   return vm_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
 }
+// Test hook: the -monochrome kernels (fi_mono.hip) on a caller-supplied Q16
+// gray image (host buffers), so the parity tests can feed the oracle the
+// identical input; out is w x h (rot 0/180) or h x w (rot 90/270), 8-bit.
+int fi_debug_monochrome(fi_ctx *c, const uint16_t *gray, int32_t w, int32_t h, int32_t rot, uint8_t *out,
+                        int32_t out_stride) {
+  if (!c || !gray || !out || w <= 0 || h <= 0) return set_err(FI_EINVAL, "bad arguments");
+  if (rot != 0 && rot != 90 && rot != 180 && rot != 270) return set_err(FI_EINVAL, "rot must be 0/90/180/270");
+  const int ow = (rot == 90 || rot == 270) ? h : w, oh = (rot == 90 || rot == 270) ? w : h;
+  if (out_stride < ow) return set_err(FI_EINVAL, "out_stride too small");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t gbytes = (size_t)w * h * 2, obytes = (size_t)out_stride * oh;
+  const size_t o_st = (gbytes + 255) / 256 * 256, o_desc = o_st + (sizeof(MonoState) + 255) / 256 * 256,
+               o_w = o_desc + 256, o_out = o_w + 256, total = o_out + obytes;
+  uint8_t *d = nullptr;
+  HIP_TRY(hipMalloc(&d, total));
+  MonoDesc md{};
+  md.g = (const uint16_t *)d;
+  md.w = w;
+  md.h = h;
+  md.rot = rot;
+  md.dst = d + o_out;
+  md.dst_stride = out_stride;
+  md.st = (MonoState *)(d + o_st);
+  volatile double qr1 = 65535.0 + 1.0, span = 16 - 1.0;
+  const double step = exp(log((double)qr1) / (double)span);
+  double weight = 1.0, wts[16];
+  for (int k = 0; k < 16; k++) {
+    wts[16 - k - 1] = 1.0 / weight;
+    weight *= step;
+  }
+  int rc = FI_OK;
+  if (hipMemcpy(d, gray, gbytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d + o_desc, &md, sizeof(md), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d + o_w, wts, sizeof(wts), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(d + o_out, 0, obytes) != hipSuccess) {
+    rc = set_err(FI_EDEVICE, "fi_debug_monochrome: upload failed");
+  } else {
+    launch_mono(c->stream, (const MonoDesc *)(d + o_desc), 1, (const double *)(d + o_w));
+    if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess ||
+        hipMemcpy(out, d + o_out, obytes, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = set_err(FI_EDEVICE, "fi_debug_monochrome: kernel failed");
+  }
+  (void)hipFree(d);
+  return rc;
+}
+
 const char *fi_last_error(void) { return g_err.c_str(); }
 
 int fi_device_count(int32_t *count) {

@@ -229,6 +229,25 @@ struct ApplyDesc {
   int32_t *out_wh;  // [2] written by the kernel
 };
 
+// -monochrome (fi_mono.hip): per-image quantize state
+// written by k_mono_stats, read by k_mono_dither
+struct MonoState {
+  int32_t bilevel;         // 1: the gray image is already black/white (no quantize)
+  int32_t black, white;    // NormalizeImage stretch points
+  int32_t ncol;            // colormap entries (<= 2)
+  uint16_t mean[8];        // cluster means (the dither's colormap)
+  uint16_t bil[8];         // thresholded bilevel colours (0 / 65535)
+  uint8_t cand[256];       // per 8-bit value: colours of its closest-colour search subtree (bit i = colour i)
+};
+struct MonoDesc {
+  const uint16_t *g;       // Q16 gray of the extent window (row stride w), written by the resample epilogue
+  int32_t w, h, rot;
+  int32_t pad;
+  uint8_t *dst;            // final 8-bit output, rotated (IntegralRotateImage after -monochrome)
+  int64_t dst_stride;
+  MonoState *st;
+};
+
 struct CropScore {  // per crop (batch-global index)
   double detail, saturation, skin, total;
   double bound;

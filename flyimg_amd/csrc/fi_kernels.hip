@@ -72,7 +72,11 @@ __device__ __forceinline__ void store_pixel(const ResizeDesc &D, int x, int y, u
     dy = D.ew - 1 - x;
   }
   uint8_t *o = D.dst + (int64_t)dy * D.dst_stride;
-  if (D.gray) {
+  if (D.gray == 2) {
+    // -monochrome input: the Q16 gray value itself (u16 scratch, fi_mono.hip; rot = 0)
+    const double gv = 0.212656 * (double)r + 0.715158 * (double)g + 0.072186 * (double)b;
+    reinterpret_cast<uint16_t *>(o)[dx] = (uint16_t)clamp_q16d(gv);
+  } else if (D.gray) {
     // -colorspace Gray: Rec709Luma on gamma-encoded Q16, ClampToQuantum
     const double gv = 0.212656 * (double)r + 0.715158 * (double)g + 0.072186 * (double)b;
     o[dx] = q16_to_u8(clamp_q16d(gv));

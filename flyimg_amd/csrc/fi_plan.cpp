@@ -92,7 +92,6 @@ int plan_im(const fi_image &img, ImPlan *p) {
   if ((int64_t)img.src_stride < (int64_t)img.src_w * 3) return fail(FI_EINVAL, "src_stride < 3*src_w");
   const uint32_t f = img.flags;
   if ((f & FI_OP_THUMBNAIL) && (f & FI_OP_RESIZE)) return fail(FI_EINVAL, "both -thumbnail and -resize");
-  if (f & FI_OP_MONOCHROME) return fail(FI_EUNSUPPORTED, "-monochrome is not implemented on the GPU path yet");
   const bool has_geom = img.target_w > 0 || img.target_h > 0;
   p->tw = p->W;
   p->th = p->H;
@@ -134,7 +133,9 @@ int plan_im(const fi_image &img, ImPlan *p) {
     p->ew = ew;
     p->eh = eh;
   }
-  p->gray = (f & FI_OP_GRAY) != 0;
+  // -monochrome (ImageProcessor.php:90-92) converts to GRAY first (SetImageType Bilevel)
+  p->mono = (f & FI_OP_MONOCHROME) != 0;
+  p->gray = (f & FI_OP_GRAY) != 0 || p->mono;
   p->rot = 0;
   if (f & FI_OP_ROTATE) {
     if (img.rotate % 90) return fail(FI_EUNSUPPORTED, "only -rotate by multiples of 90 (IntegralRotateImage)");

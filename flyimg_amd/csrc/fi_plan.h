@@ -28,6 +28,7 @@ struct ImPlan {
   double xf = 1, yf = 1;
   int ex0 = 0, ey0 = 0, ew = 0, eh = 0;  // extent window in the resized image
   bool gray = false;
+  bool mono = false;        // -monochrome: Q16 gray of the extent window -> fi_mono.hip -> rotate
   int rot = 0;
   int out_w = 0, out_h = 0, out_c = 3;   // after rotate
 };

@@ -240,6 +240,17 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
   auto store_block = [&](int b) {
     const int rows_here = min(16, D.eh - 16 * b);
     const int nb = nx * oc;
+    if (D.gray == 2) {
+      // -monochrome input: Q16 gray (u16 scratch, rot = 0) for fi_mono.hip
+      for (int it = tid; it < rows_here * nx; it += kVmThreads) {
+        const int yl = it / nx, x = it - yl * nx;
+        const uint16_t *o = otile + yl * kVmOtilePitch + 3 * x;
+        const double gv = 0.212656 * (double)o[0] + 0.715158 * (double)o[1] + 0.072186 * (double)o[2];
+        const uint32_t q = !(gv > 0.0) ? 0u : (gv >= 65535.0 ? 65535u : (uint32_t)(gv + 0.5));
+        reinterpret_cast<uint16_t *>(D.dst + (int64_t)(16 * b + yl) * D.dst_stride)[S.x0 + x] = (uint16_t)q;
+      }
+      return;
+    }
     if (fast8) {
       // items = (row, destination dword): interior dwords copied from the
       // shifted 8-bit tile as one dword, the partial first/last dword byte by byte

@@ -178,6 +178,15 @@ class Context:
         L.check(self._lib.fi_kernel_stats(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)))
         return ms.value, n.value, b.value
 
+    def monochrome_q16(self, gray: np.ndarray, rot: int = 0) -> np.ndarray:
+        """Test hook: the -monochrome kernels on a Q16 gray image (fi_debug_monochrome)."""
+        g = np.ascontiguousarray(gray, dtype=np.uint16)
+        h, w = g.shape
+        oh, ow = (w, h) if rot in (90, 270) else (h, w)
+        out = np.zeros((oh, ow), np.uint8)
+        L.check(self._lib.fi_debug_monochrome(self.h, g.ctypes.data, w, h, rot, out.ctypes.data, ow))
+        return out
+
 
 def device_count() -> int:
     n = ctypes.c_int32()

@@ -57,7 +57,7 @@ extern "C" {
 #define FI_GEOM_SHRINK_ONLY (1u << 3)  /* '>' geometry flag (generateSimpleSize :159)     */
 #define FI_OP_EXTENT (1u << 4)         /* -gravity G -extent WxH (c_1, :144-145)          */
 #define FI_OP_GRAY (1u << 5)           /* -colorspace Gray (clsp_Gray, :88)               */
-#define FI_OP_MONOCHROME (1u << 6)     /* -monochrome (mnchr_1, :90-92)                   */
+#define FI_OP_MONOCHROME (1u << 6)     /* -monochrome (mnchr_1, :90-92); implies Gray      */
 #define FI_OP_ROTATE (1u << 7)         /* -rotate <deg>, multiples of 90 (r_90, :306)     */
 #define FI_OP_SMARTCROP (1u << 8)      /* compute smartcrop.py's box on the result (smc_1) */
 #define FI_OP_SMARTCROP_APPLY (1u << 9) /* and crop to it (SmartCropProcessor.php:30-34)   */
@@ -212,6 +212,13 @@ int fi_rccl_init(fi_ctx *ctx, int32_t rank, int32_t world, const uint8_t id[128]
 /* Every rank sends `count` records (same count on every rank); rank 0
  * receives world*count records in rank order. */
 int fi_rccl_gather_records(fi_ctx *ctx, const fi_record *send, int32_t count, fi_record *recv);
+
+/* Test hook (not a reference interface): the -monochrome kernels on a
+ * caller-supplied Q16 gray image (host buffers), w x h row-major, rotated by
+ * rot (0/90/180/270) into out (0/255 bytes).  Lets the parity tests feed the
+ * oracle's or_im_monochrome the identical input. */
+int fi_debug_monochrome(fi_ctx *ctx, const uint16_t *gray, int32_t w, int32_t h, int32_t rot, uint8_t *out,
+                        int32_t out_stride);
 
 #ifdef __cplusplus
 }

@@ -104,6 +104,12 @@ def lib():
             P(ScCrop), i, P(i), P(i), P(i), P(ctypes.c_double), u8p, u8p,
         ]
         L.or_sc_max_crops.argtypes = [i, i, i]
+        u16p = P(ctypes.c_uint16)
+        L.or_im_monochrome.argtypes = [u16p, i, i, u8p]
+        L.or_hilbert_d2xy.argtypes = [i, ctypes.c_long, P(i), P(i)]
+        L.or_hilbert_d2xy.restype = None
+        L.or_mono_curve_level.argtypes = [i, i]
+        L.or_mono_quant_info.argtypes = [P(ctypes.c_uint64), P(i), u16p, u16p]
         assert L.or_sizeof_crop() == ctypes.sizeof(ScCrop)
         assert L.or_sizeof_params() == ctypes.sizeof(ScParams)
         _lib = L
@@ -144,10 +150,45 @@ def im_gravity_offset(W, H, ew, eh, gravity=5):
 
 
 FLAG_THUMBNAIL, FLAG_FILL, FLAG_SHRINK, FLAG_EXTENT, FLAG_GRAY, FLAG_ROTATE = 1, 2, 4, 8, 16, 32
+FLAG_MONO = 64  # -monochrome (B7); implies gray
+
+
+def im_monochrome(gray_q16: np.ndarray) -> np.ndarray:
+    """-monochrome of a Q16 gray image (B7 restatement, parity unpinned) -> 0/255 u8."""
+    g = np.ascontiguousarray(gray_q16, dtype=np.uint16)
+    h, w = g.shape
+    out = np.zeros((h, w), np.uint8)
+    rc = lib().or_im_monochrome(g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), w, h, _u8(out))
+    if rc:
+        raise ValueError(f"or_im_monochrome rc={rc}")
+    return out
+
+
+def hilbert_d2xy(level: int, d: int):
+    x, y = ctypes.c_int(), ctypes.c_int()
+    lib().or_hilbert_d2xy(level, d, ctypes.byref(x), ctypes.byref(y))
+    return x.value, y.value
+
+
+def mono_curve_level(w: int, h: int) -> int:
+    return lib().or_mono_curve_level(w, h)
+
+
+def mono_quant_info(hist: np.ndarray):
+    """(ncol, cluster means, bilevel colours) of a stretched Q16 histogram."""
+    H = np.ascontiguousarray(hist, dtype=np.uint64)
+    assert H.size == 65536
+    n = ctypes.c_int()
+    m = np.zeros(2, np.uint16)
+    b = np.zeros(2, np.uint16)
+    P = ctypes.POINTER
+    lib().or_mono_quant_info(H.ctypes.data_as(P(ctypes.c_uint64)), ctypes.byref(n),
+                             m.ctypes.data_as(P(ctypes.c_uint16)), b.ctypes.data_as(P(ctypes.c_uint16)))
+    return n.value, m[: min(n.value, 2)].tolist(), b[: min(n.value, 2)].tolist()
 
 
 def im_convert(src: np.ndarray, rw=0, rh=0, flags=FLAG_THUMBNAIL, gravity=5, rotate=0) -> np.ndarray:
-    """convert <src> <resize op> [-gravity g -extent WxH] [-colorspace Gray] [-rotate r]."""
+    """convert <src> <resize op> [-gravity g -extent WxH] [-colorspace Gray] [-monochrome] [-rotate r]."""
     src = np.ascontiguousarray(src, dtype=np.uint8)
     H, W = src.shape[:2]
     cap = max(W * H * 3, 1) * 64 + (rw or 1) * (rh or 1) * 3 * 4

@@ -89,9 +89,19 @@ def test_baseline_configs_plan():
 def test_unsupported_ops_fail_loudly():
     with pytest.raises(ExecFailedException):
         ImageProcessor(OptionsBag("w_200,r_-45"), 400, 300).to_op()
-    op = Op(100, 0, L.FI_OP_THUMBNAIL | L.FI_OP_MONOCHROME)
+    op = Op(100, 0, L.FI_OP_THUMBNAIL, rotate=45)
+    op.flags |= L.FI_OP_ROTATE
     with pytest.raises(L.FiError):
         plan(400, 300, op)
+
+
+def test_monochrome_plans_one_channel():
+    """mnchr_1 (ImageProcessor.php:90-92): -monochrome converts to GRAY, so the
+    output has one channel; rotation applies after it."""
+    from flyimg_amd.processor import ImageProcessor, OptionsBag
+
+    assert plan(400, 300, ImageProcessor(OptionsBag("w_100,mnchr_1"), 400, 300).to_op()) == (100, 75, 1)
+    assert plan(400, 300, ImageProcessor(OptionsBag("w_100,h_50,c_1,r_90,mnchr_1"), 400, 300).to_op()) == (50, 100, 1)
 
 
 def _norm_decls(text):

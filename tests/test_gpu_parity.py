@@ -326,3 +326,75 @@ def test_pipelined_submit_matches_synchronous(ctx):
     finally:
         ctx.free(pool)
         ctx.free(dst)
+
+
+# ---------------------------------------------------------------------------
+# -monochrome (B7): fi_mono.hip vs oracle/fi_oracle.c or_im_monochrome
+# ---------------------------------------------------------------------------
+def _mono_inputs():
+    rng = np.random.default_rng(4242)
+    out = []
+    yy, xx = np.mgrid[0:181, 0:257]
+    out.append(("smooth_181x257", np.clip(30000 + 25000 * np.sin(xx / 9.0) * np.cos(yy / 13.0)
+                                          + rng.integers(-2000, 2000, xx.shape), 0, 65535)))
+    out.append(("random_64x64", rng.integers(0, 65536, (64, 64))))
+    out.append(("narrow_range_100x37", rng.integers(21000, 26000, (100, 37))))
+    out.append(("skewed_1x300", np.minimum(65535, (rng.random((1, 300)) ** 3 * 70000).astype(np.int64))))
+    out.append(("tall_513x3", rng.integers(0, 65536, (513, 3))))
+    out.append(("bilevel_40x50", np.where(rng.random((40, 50)) > 0.4, 65535, 0)))
+    out.append(("uniform_33x33", np.full((33, 33), 40000)))
+    out.append(("two_values_20x20", np.where(rng.random((20, 20)) > 0.5, 50000, 10000)))
+    src = synth_rgb(400, 400, 99).astype(np.float64) * 257.0
+    gq = np.floor(0.212656 * src[..., 0] + 0.715158 * src[..., 1] + 0.072186 * src[..., 2] + 0.5)
+    out.append(("synth_gray_400x400", gq))
+    return [(n, np.clip(g, 0, 65535).astype(np.uint16)) for n, g in out]
+
+
+@pytest.mark.parametrize("name,g", _mono_inputs(), ids=[c[0] for c in _mono_inputs()])
+@pytest.mark.parametrize("rot", [0, 90])
+def test_monochrome_kernels_bit_exact(ctx, name, g, rot):
+    """Same Q16 input -> identical 0/255 output (stats, tree, dither, rotation)."""
+    ref = orc.im_monochrome(g)
+    if rot == 90:
+        ref = np.rot90(ref, -1)
+    gpu = ctx.monochrome_q16(g, rot)
+    assert gpu.shape == ref.shape
+    assert np.array_equal(gpu, ref), f"{name}: {(gpu != ref).sum()} of {gpu.size} pixels differ"
+
+
+MONO_CASES = [
+    # identity geometry: the Q16 gray is exactly 257 * pixel on both sides -> bit-exact end to end
+    ("identity_extent_rot90", 300, 200, 250, 200,
+     F.FI_OP_THUMBNAIL | F.FI_GEOM_FILL | F.FI_OP_EXTENT | F.FI_OP_MONOCHROME | F.FI_OP_ROTATE, 90),
+    ("identity_gray_mono", 160, 120, 160, 0, F.FI_OP_THUMBNAIL | F.FI_OP_GRAY | F.FI_OP_MONOCHROME, 0),
+]
+
+
+@pytest.mark.parametrize("case", MONO_CASES, ids=[c[0] for c in MONO_CASES])
+def test_monochrome_pipeline_identity_bit_exact(rctx, case):
+    name, W, H, tw, th, flags, rot = case
+    src = synth_rgb(W, H, 500 + W)
+    outs, recs, rc = rctx.process([src], [Op(tw, th, flags, L.GRAVITY["Center"], rot)])
+    assert rc == 0 and recs[0].status == 0, L.lib().fi_last_error()
+    ref = orc.im_convert(src, tw, th, _oracle_flags(flags) | orc.FLAG_MONO, rotate=rot)
+    assert outs[0].shape == ref.shape
+    assert np.array_equal(outs[0], ref), f"{name}: {(outs[0] != ref).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("W,H,opts", [(1920, 1080, "w_500,mnchr_1"),
+                                      (6000, 4000, "w_400,h_400,c_1,r_90,mnchr_1")])
+def test_monochrome_pipeline_resized(rctx, W, H, opts):
+    """Resized: the GPU's Q16 gray is within the resample tolerance of the
+    oracle's, and the error diffusion is chaotic in its input, so the check is
+    the operator's invariants: 0/255 only, the oracle's geometry, and the white
+    fraction of the oracle's output on the same source within 1 %."""
+    from flyimg_amd.processor import ImageProcessor, OptionsBag
+
+    op = ImageProcessor(OptionsBag(opts), W, H).to_op()
+    src = synth_rgb(W, H, 31)
+    outs, recs, rc = rctx.process([src], [op])
+    assert rc == 0 and recs[0].status == 0, L.lib().fi_last_error()
+    ref = orc.im_convert(src, op.target_w, op.target_h, _oracle_flags(op.flags) | orc.FLAG_MONO, rotate=op.rotate)
+    assert outs[0].shape == ref.shape
+    assert set(np.unique(outs[0])) <= {0, 255}
+    assert abs(outs[0].mean() - ref.mean()) / 255 < 0.01
