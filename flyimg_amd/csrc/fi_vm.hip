@@ -96,8 +96,9 @@ __device__ uint64_t g_vm_stamps[kVmStampSlots * (kVmStampN + 1)];
 
 // MODE (profiling ablations, FI_VM_VARIANT; wrong pixels): 0 production,
 // 1 loads + LDS writes only, 2 no horizontal pass / epilogue, 3 no stores,
-// 4 no horizontal MFMA (planes + stores kept), 9 production + per-phase
-// s_memtime sums (tools/vm_timing.py).
+// 4 no horizontal pass (planes + stores kept), 5 as 4 without stores, 6 as 4
+// without planes (stores kept), 9 production + per-phase s_memtime sums
+// (tools/vm_timing.py).
 // Launch bound: 8-wave workgroups, two per CU -> 4 waves per SIMD (<= 128 VGPRs).
 template <int MODE>
 __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict__ descs,
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
     }
     if (tid < 388) *reinterpret_cast<i32x4 *>(apl + 16 * tid) = aq;
     stamp(2);
-    if ((MODE == 0 || MODE == 4 || MODE == 9) && pend >= 0) {
+    if ((MODE == 0 || MODE == 4 || MODE == 6 || MODE == 9) && pend >= 0) {
       store_block(pend);
       pend = -1;
     }
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
 #pragma unroll
         for (int j = 0; j < kVmTiles; j++) {
           const uint32_t o = (vcolp[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-          if (o == 0xFFFFu) continue;
+          if (o == 0xFFFFu || MODE == 6) continue;
           uint32_t q[4];
 #pragma unroll
           for (int i = 0; i < 4; i++)  // ClampToQuantum: +0.5 truncated; the conversions saturate
@@ -397,10 +398,10 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
           *reinterpret_cast<uint32_t *>(vpl + o + 3 * plane) = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
         }
         stamp(8);
-        __syncthreads();
+        if (MODE != 6) __syncthreads();
         stamp(9);
         // ---- horizontal: items (16-px output block, channel) over the waves
-        if (MODE != 4) {
+        if (MODE != 4 && MODE != 5 && MODE != 6) {
 #pragma unroll
           for (int k = 0; k < 2; k++) {
             const int it = wv + kVmWaves * k;
@@ -466,7 +467,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
     }
     mc = mn;
   }
-  if ((MODE == 0 || MODE == 4 || MODE == 9) && pend >= 0) {
+  if ((MODE == 0 || MODE == 4 || MODE == 6 || MODE == 9) && pend >= 0) {
     __syncthreads();
     store_block(pend);
   }
@@ -503,6 +504,10 @@ int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTi
     hipLaunchKernelGGL((k_rs_vm<3>), dim3(ntiles), dim3(kVmThreads), lds, s, descs, strips, tiles, ai);
   else if (v == 4)
     hipLaunchKernelGGL((k_rs_vm<4>), dim3(ntiles), dim3(kVmThreads), lds, s, descs, strips, tiles, ai);
+  else if (v == 5)
+    hipLaunchKernelGGL((k_rs_vm<5>), dim3(ntiles), dim3(kVmThreads), lds, s, descs, strips, tiles, ai);
+  else if (v == 6)
+    hipLaunchKernelGGL((k_rs_vm<6>), dim3(ntiles), dim3(kVmThreads), lds, s, descs, strips, tiles, ai);
   else if (v == 9)
     hipLaunchKernelGGL((k_rs_vm<9>), dim3(ntiles), dim3(kVmThreads), lds, s, descs, strips, tiles, ai);
   else
