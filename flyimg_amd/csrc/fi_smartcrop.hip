@@ -120,44 +120,77 @@ __global__ __launch_bounds__(kPrepThreads) void k_sc_hmfma(const ScDesc *__restr
   const int aw = D.aw, hrows = D.hrows, yoff = D.ybox_first;
   const int apitch = (aw * 3 + 15) & ~15;
   const int nch = sC == 3 ? 3 : 1;
-  // ---- stage rows [r0, r0 + R) as planes [c][row][P] of (p - 128); zero pad
-  const int ng = P >> 2;  // 4-pixel groups per plane row
+  // ---- stage rows [r0, r0 + R) as planes [c][row][P] of (p - 128); zero pad.
+  // One item = 16 pixels of a row: three 16-byte loads (dword-aligned rows),
+  // deinterleaved into one 16-byte LDS store per plane; row tails pad with 128.
+  typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+  typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+  const int ng = P >> 4;  // 16-pixel groups per plane row
   const bool a4 = (((uintptr_t)src | (uintptr_t)sstride) & 3) == 0;
-  for (int it = tid; it < R * ng; it += kPrepThreads) {
-    const int rr = it / ng, g = it - rr * ng;
-    uint32_t w0 = 0, w1 = 0, w2 = 0;
-    if (r0 + rr < hrows && 4 * g < sW) {
+  // batches of 4 items per thread: all 12 loads of a batch are issued before
+  // the first is consumed (one HBM round trip per batch, not per item)
+  for (int base = 0; base < R * ng; base += 4 * kPrepThreads) {
+    u32x4a q[4][3];
+    bool fast[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int it = base + u * kPrepThreads + tid;
+      const int rr = it / ng, g = it - rr * ng;
       const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride;
-      if (sC == 3) {
-        uint8_t b[12];
-        if (a4 && 4 * g + 4 <= sW) {
-          const uint32_t *q = reinterpret_cast<const uint32_t *>(s + 12 * g);
-          const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+      fast[u] = it < R * ng && r0 + rr < hrows && sC == 3 && a4 && 16 * g + 16 <= sW;
+      if (fast[u]) {
 #pragma unroll
-          for (int k = 0; k < 4; k++) {
-            b[k] = (uint8_t)(d0 >> (8 * k));
-            b[4 + k] = (uint8_t)(d1 >> (8 * k));
-            b[8 + k] = (uint8_t)(d2 >> (8 * k));
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 12; k++) b[k] = (4 * g + k / 3 < sW) ? s[12 * g + k] : (uint8_t)128;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          w0 |= (uint32_t)(b[3 * i] ^ 0x80) << (8 * i);
-          w1 |= (uint32_t)(b[3 * i + 1] ^ 0x80) << (8 * i);
-          w2 |= (uint32_t)(b[3 * i + 2] ^ 0x80) << (8 * i);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; i++) w0 |= (uint32_t)((4 * g + i < sW ? s[4 * g + i] : (uint8_t)128) ^ 0x80) << (8 * i);
+        for (int k = 0; k < 3; k++) q[u][k] = *reinterpret_cast<const u32x4a *>(s + 48 * g + 16 * k);
       }
     }
-    reinterpret_cast<uint32_t *>(lds8 + (0 * R + rr) * P)[g] = w0;
-    if (nch == 3) {
-      reinterpret_cast<uint32_t *>(lds8 + (1 * R + rr) * P)[g] = w1;
-      reinterpret_cast<uint32_t *>(lds8 + (2 * R + rr) * P)[g] = w2;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int it = base + u * kPrepThreads + tid;
+      if (it >= R * ng) break;
+      const int rr = it / ng, g = it - rr * ng;
+      const bool rowok = r0 + rr < hrows;
+      const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride;
+      u32x4s w0, w1, w2;
+      if (fast[u]) {
+        // deinterleave 16 RGB pixels: plane dword k takes bytes 12k + {0,3,6,9}
+        // (+1 / +2 for G / B) of the three source dwords 3k .. 3k + 2
+        const uint32_t d[12] = {q[u][0].x, q[u][0].y, q[u][0].z, q[u][0].w, q[u][1].x, q[u][1].y,
+                                q[u][1].z, q[u][1].w, q[u][2].x, q[u][2].y, q[u][2].z, q[u][2].w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t a0 = d[3 * k], a1 = d[3 * k + 1], a2 = d[3 * k + 2];
+          w0[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00060300u), 0x05020100u) ^ 0x80808080u;
+          w1[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00070401u), 0x06020100u) ^ 0x80808080u;
+          w2[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00000502u), 0x07040100u) ^ 0x80808080u;
+        }
+      } else {
+        for (int k = 0; k < 4; k++) {
+          uint32_t a = 0, b = 0, c = 0;
+          for (int j = 0; j < 4; j++) {
+            const int x = 16 * g + 4 * k + j;
+            const bool ok = rowok && x < sW;
+            uint32_t vr, vg, vb;
+            if (sC == 3) {
+              vr = ok ? s[3 * x] : 128u;
+              vg = ok ? s[3 * x + 1] : 128u;
+              vb = ok ? s[3 * x + 2] : 128u;
+            } else {
+              vr = vg = vb = ok ? s[x] : 128u;
+            }
+            a |= vr << (8 * j);
+            b |= vg << (8 * j);
+            c |= vb << (8 * j);
+          }
+          w0[k] = a ^ 0x80808080u;
+          w1[k] = b ^ 0x80808080u;
+          w2[k] = c ^ 0x80808080u;
+        }
+      }
+      *reinterpret_cast<u32x4s *>(lds8 + (0 * R + rr) * P + 16 * g) = w0;
+      if (nch == 3) {
+        *reinterpret_cast<u32x4s *>(lds8 + (1 * R + rr) * P + 16 * g) = w1;
+        *reinterpret_cast<u32x4s *>(lds8 + (2 * R + rr) * P + 16 * g) = w2;
+      }
     }
   }
   __syncthreads();
@@ -615,8 +648,27 @@ __global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict
   const int64_t total = (int64_t)rowb * oh;
   if (total <= 0) return;
   const uint8_t *src0 = A.src + (int64_t)c.ry * A.src_stride + (int64_t)c.rx * A.C;
+  // (row, byte) of output offset o: float reciprocal + exact correction (no
+  // 64-bit division; total = rowb * oh < 2^31 for any thumbnail)
+  const float inv_rowb = 1.0f / (float)rowb;
+  auto rowcol = [&](int64_t o, int *y_, int *x_) {
+    const int oo = (int)o;
+    int y = (int)((float)oo * inv_rowb);
+    int x = oo - y * rowb;
+    while (x < 0) {
+      y--;
+      x += rowb;
+    }
+    while (x >= rowb) {
+      y++;
+      x -= rowb;
+    }
+    *y_ = y;
+    *x_ = x;
+  };
   auto src_of = [&](int64_t o) {
-    const int y = (int)(o / rowb), x = (int)(o - (int64_t)y * rowb);
+    int y, x;
+    rowcol(o, &y, &x);
     return src0 + (int64_t)y * A.src_stride + x;
   };
   const int head = (int)((16 - ((uintptr_t)A.dst & 15)) & 15);
@@ -629,7 +681,8 @@ __global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict
   }
   for (int64_t k = (int64_t)blockIdx.x * 256 + tid; k < nchunk; k += (int64_t)gridDim.x * 256) {
     const int64_t o = head + 16 * k;
-    const int y = (int)(o / rowb), x = (int)(o - (int64_t)y * rowb);
+    int y, x;
+    rowcol(o, &y, &x);
     uint4 out;
     if (x + 16 <= rowb) {
       const uint8_t *s = src0 + (int64_t)y * A.src_stride + x;
@@ -642,8 +695,15 @@ __global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict
       out.w = ap_align(w4, w3, sh);
     } else {
       uint8_t b[16];
+      int yy = y, xx = x;
 #pragma unroll
-      for (int j = 0; j < 16; j++) b[j] = *src_of(o + j);
+      for (int j = 0; j < 16; j++) {  // straddles a row end
+        b[j] = src0[(int64_t)yy * A.src_stride + xx];
+        if (++xx == rowb) {
+          xx = 0;
+          yy++;
+        }
+      }
       out.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
       out.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
       out.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
