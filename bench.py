@@ -35,7 +35,34 @@ WORKLOADS = {
     "cfg3": (3840, 2160, 4096, "w_512,h_512,c_1", "configs[2]: batch of 4096 3840x2160 RGB -> 512x512 Lanczos thumbnails c_1"),
     "cfg5": (6000, 4000, 1024, "w_400,h_400,c_1,r_90,clsp_Gray,smc_1", "configs[4]: 6000x4000 batch -> w_400,h_400,c_1,r_90,clsp_Gray,smc_1"),
     "cfg1": (3000, 2000, 1024, "w_300,h_250,c_1", "configs[0] geometry on the GPU: 3000x2000 -> w_300,h_250,c_1"),
+    # cfg4 is a mixed list, not one geometry (see cfg4_list / run_cfg4)
+    "cfg4": (0, 0, 65536, "mixed", "configs[3]: 65536 mixed-size images (0.5-24 MP), multiple output sizes, "
+                                    "sharded across GPUs"),
 }
+
+CFG4_OPS = ["w_300,h_250,c_1", "w_500,smc_1", "w_512,h_512,c_1", "h_300", "w_400,h_400,c_1"]
+CFG4_ASPECTS = [4 / 3, 3 / 2, 16 / 9, 1.0, 2 / 3, 9 / 16]
+CFG4_MP_CLASSES = 64
+
+
+def cfg4_list(n=65536, seed=20250112):
+    """megapixels log-uniform in [0.5, 24] (64 log-spaced
+    classes, like the finite set of camera resolutions a service sees), aspect
+    from {4:3, 3:2, 16:9, 1:1, 2:3, 9:16}, ops cycling through the cfg1 / cfg2 /
+    cfg3 ops, h_300 and w_400,h_400,c_1.  Returns [(W, H, op_index)]."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    mps = np.exp(np.linspace(np.log(0.5), np.log(24.0), CFG4_MP_CLASSES))
+    out = []
+    ks = rng.integers(0, CFG4_MP_CLASSES, n)
+    asp = rng.integers(0, len(CFG4_ASPECTS), n)
+    for i in range(n):
+        a = CFG4_ASPECTS[int(asp[i])]
+        W = max(16, int(round((float(mps[ks[i]]) * 1e6 * a) ** 0.5)))
+        H = max(16, int(round(W / a)))
+        out.append((W, H, i % len(CFG4_OPS)))
+    return out
 
 
 KERNEL_OF_PATH = {
@@ -111,6 +138,8 @@ def main():
     if world != args.gpus and rank == 0:
         log(f"note: WORLD_SIZE={world} vs --gpus {args.gpus}; using WORLD_SIZE")
     comm = make_comm()
+    if args.workload == "cfg4":
+        return run_cfg4(args, rank, world, local_rank, comm)
     W, H, nimg, options, cfg_text = WORKLOADS[args.workload]
     if args.images:
         nimg = args.images
@@ -245,6 +274,172 @@ def main():
         print(json.dumps(result), flush=True)
     ctx.free(pool)
     ctx.free(dst)
+    comm.close()
+    ctx.close()
+
+
+def run_cfg4(args, rank, world, local_rank, comm):
+    """cfg4: the 65536-image mixed list, LPT-sharded by input bytes across the
+    ranks (strong scaling: the total is fixed), each rank running its shard as
+    pipelined batches of 1024.  One step = every rank's whole shard.  Sources:
+    one synthetic image per (size class) in a device pool (~7 GB), shared by the
+    descriptors of that class."""
+    import numpy as np
+
+    from flyimg_amd import _lib as L
+    from flyimg_amd.parallel import RecordGather, shard_lpt
+    from flyimg_amd.processor import ImageProcessor, OptionsBag
+    from flyimg_amd.runtime import Context
+    from flyimg_amd.runtime import plan as fi_plan
+
+    n_total = args.images or 65536
+    items = cfg4_list(n_total)
+    shard = shard_lpt([float(W) * H for W, H, _ in items], world)[rank]
+    ctx = Context(local_rank)
+    gather = RecordGather(comm, ctx)
+    sizes = sorted({(W, H) for W, H, _ in items})
+    stride_of = {wh: (wh[0] * 3 + 15) // 16 * 16 for wh in sizes}
+    off_of, total = {}, 0
+    for wh in sizes:
+        off_of[wh] = total
+        total += stride_of[wh] * wh[1]
+    pool = ctx.malloc(total)
+    t0 = time.perf_counter()
+    for k, wh in enumerate(sizes):
+        ctx.fill_synthetic(pool + off_of[wh], wh[0], wh[1], stride_of[wh], 0x5EED + 7919 * k)
+    log(f"rank {rank}: cfg4 shard {len(shard)} of {n_total} images, pool of {len(sizes)} size classes "
+        f"({total / 1e9:.2f} GB) in {time.perf_counter() - t0:.1f} s")
+    ops = {}
+    for i in shard:
+        W, H, k = items[i]
+        if (W, H, k) not in ops:
+            op = ImageProcessor(OptionsBag(CFG4_OPS[k]), W, H).to_op()
+            ops[(W, H, k)] = (op, fi_plan(W, H, op))
+    B = 1024
+    batches = [shard[j:j + B] for j in range(0, len(shard), B)]
+    cap = max(sum(int(np.prod(ops[items[i]][1])) for i in b) for b in batches) if batches else 1
+    dst = [ctx.malloc(cap), ctx.malloc(cap)]
+    arrs = [(L.FiImage * B)() for _ in range(2)]
+
+    def fill(arr, b, slot):
+        o = 0
+        for j, i in enumerate(b):
+            W, H, k = items[i]
+            op, (ow, oh, oc) = ops[(W, H, k)]
+            a = arr[j]
+            a.src, a.src_w, a.src_h, a.src_stride, a.src_channels = pool + off_of[(W, H)], W, H, stride_of[(W, H)], 3
+            a.target_w, a.target_h, a.flags, a.gravity, a.rotate = op.target_w, op.target_h, op.flags, op.gravity, op.rotate
+            a.smartcrop_w, a.smartcrop_h = op.smartcrop_w, op.smartcrop_h
+            a.dst, a.dst_capacity = dst[slot] + o, ow * oh * oc
+            o += ow * oh * oc
+
+    bad = [0]
+
+    def step():
+        recs = []
+        for k, b in enumerate(batches):
+            fill(arrs[k % 2], b, k % 2)
+            L.check(ctx.submit_device(arrs[k % 2], len(b)))
+            if k > 0:
+                L.check(ctx.wait(1))
+                pb, pa = batches[k - 1], arrs[(k - 1) % 2]
+                bad[0] += sum(1 for j in range(len(pb)) if pa[j].status != 0)
+                recs += [(pb[j], pa[j].status, pa[j].out_w, pa[j].out_h, pa[j].crop_x, pa[j].crop_y,
+                          pa[j].crop_w, pa[j].crop_h) for j in range(len(pb))]
+        L.check(ctx.wait(0))
+        if batches:
+            pb, pa = batches[-1], arrs[(len(batches) - 1) % 2]
+            bad[0] += sum(1 for j in range(len(pb)) if pa[j].status != 0)
+            recs += [(pb[j], pa[j].status, pa[j].out_w, pa[j].out_h, pa[j].crop_x, pa[j].crop_y,
+                      pa[j].crop_w, pa[j].crop_h) for j in range(len(pb))]
+        if world > 1:
+            # uneven shards: pad to the longest so every rank sends the same count
+            n_max = max(comm.allgather_obj(len(recs)))
+            recs += [(-1, 0, 0, 0, 0, 0, 0, 0)] * (n_max - len(recs))
+            gather.gather(recs)
+
+    for _ in range(args.warmup):
+        step()
+    bad[0] = 0
+    ctx.set_timing(True)
+    ctx.reset_stats()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    t1 = time.perf_counter()
+    comm.barrier()
+    ctx.set_timing(False)
+    names = ("batch", "resize", "sc_prep", "sc_score", "crop_apply", "mono", "host_plan", "host_plan_images",
+             "host_plan_sc", "host_plan_tiles", "host_plan_vmtiles", "host_plan_blob", "host_launch", "host_wait",
+             "host_total")
+    stats = {k: ctx.stats(k) for k in names}
+    paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in KERNEL_OF_PATH}
+    allv = comm.allgather_obj({"elapsed": t1 - t0, "stats": stats, "bad": bad[0], "n": len(shard)})
+    if rank == 0:
+        T = max(v["elapsed"] for v in allv)
+        mpix = sum(W * H for W, H, _ in items) * args.steps / 1e6
+        rs_ms, rs_n, rs_bytes = stats["resize"]
+        achieved = (rs_bytes / max(rs_n, 1)) / (rs_ms / max(rs_n, 1) / 1e3) / 1e9 if rs_ms > 0 else 0.0
+        gpu_ms = stats["batch"][0] / max(args.steps, 1)
+        result = {
+            "metric": METRIC,
+            "value": round(mpix / T, 3),
+            "unit": "Mpix/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(T / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (one seeded image per size class in HBM, shared by that class's descriptors)",
+            "config": {
+                "workload": f"cfg4: {WORKLOADS['cfg4'][4]}",
+                "images_total": n_total, "size_classes": len(sizes),
+                "mean_mpix_per_image": round(mpix / args.steps / n_total, 3),
+                "ops": CFG4_OPS, "batch": B,
+                "parallelism": f"dp{world} (LPT shards by input bytes, RCCL gather of result records)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "resize stage: " + " + ".join(
+                    f"{KERNEL_OF_PATH[p]} ({n} images)" for p, n in paths.items() if n),
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "avg_launch_ms": round(rs_ms / max(rs_n, 1), 4),
+            },
+            "rank0_gpu_busy_ms_per_step": round(gpu_ms, 3),
+            "rank0_host_plan_ms_per_step": round(stats["host_plan"][0] / max(args.steps, 1), 3),
+            "stages_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4) for k, v in stats.items()},
+            "shard_images": [v["n"] for v in allv],
+            "failed_images": sum(v["bad"] for v in allv),
+        }
+        if not args.no_cpu_baseline:
+            try:
+                # the oracle on the first images of the list (bounded sample)
+                cb = None
+                for W, H, k in items[:8]:
+                    r = cpu_baseline(W, H, CFG4_OPS[k], budget_s=2.0, max_images=1)
+                    if cb is None:
+                        cb = {"mpix": 0.0, "s": 0.0, "n": 0}
+                    cb["mpix"] += W * H / 1e6
+                    cb["s"] += W * H / 1e6 / r["value"]
+                    cb["n"] += 1
+                result["cpu_baseline"] = {"value": round(cb["mpix"] / cb["s"], 4), "unit": "Mpix/s", "cores": 1,
+                                          "kind": "port",
+                                          "sample": f"first {cb['n']} images of the cfg4 list through "
+                                                    f"oracle/fi_oracle.c, single thread, {cb['s']:.1f} s"}
+            except Exception as e:  # noqa: BLE001
+                result["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(result), flush=True)
+    ctx.free(pool)
+    for d in dst:
+        ctx.free(d)
     comm.close()
     ctx.close()
 

@@ -173,6 +173,32 @@ struct fi_ctx {
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
+  // Device-resident table heaps: every per-geometry table (tap tables, MFMA
+  // fragments, Pillow coefficients, importance tables) is uploaded once and
+  // stays at a fixed offset; a batch uploads only the tables it adds.  The
+  // heaps are append-only between resets, and a reset only ever happens
+  // between batches: work queued earlier on the (in-order) stream has read
+  // its tables before any later copy overwrites them.
+  struct Heap {
+    void *p = nullptr;
+    size_t cap = 0, used = 0;  // elements
+  };
+  Heap heap_i, heap_f, heap_d;  // int32 / float / double
+  // absolute heap offsets of placed tables, keyed by the cached host object
+  struct ScTabs {
+    int32_t hb = 0, hk = 0, hkT = 0, vb = 0, vk = 0;
+    int32_t hmB = 0, hmC = 0, hmS0 = 0, vqA = 0, vqC = 0, vqK0 = 0;
+  };
+  std::map<const AxisTable *, DevAxis> axis_at;
+  std::map<const ScPlan *, ScTabs> sc_at;
+  std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_at;
+  std::map<const RingTable *, std::array<int32_t, 4>> ring_at;
+  std::map<const StripTab *, std::pair<int32_t, int32_t>> strip_at;
+  std::map<const MfmaV *, std::array<int32_t, 5>> mv_at;
+  std::map<const VmV *, std::array<int32_t, 8>> vv_at;
+  std::map<const MfmaH *, std::array<int32_t, 4>> mh_at;  // wsum, frag, s0, lut
+  int32_t mono_wts_at = -1;
+  bool heap_retry = false;
   bool sc_mfma = true;  // FI_DISABLE_SC_MFMA=1: VALU horizontal pass (k_sc_hrows) instead of k_sc_hmfma
 };
 
@@ -333,11 +359,99 @@ struct Exec {
   fi_ctx *c;
   Blob blob;
   Work work;
+  // tables this batch adds to the device heaps (uploaded behind the heaps'
+  // used marks bi / bf / bd, which are multiples of 16 elements)
   std::vector<int32_t> ai;
   std::vector<float> af;
   std::vector<double> ad;
+  int64_t bi = 0, bf = 0, bd = 0;
+  int32_t oi() const { return (int32_t)(bi + (int64_t)ai.size()); }
+  int32_t of() const { return (int32_t)(bf + (int64_t)af.size()); }
+  int32_t od() const { return (int32_t)(bd + (int64_t)ad.size()); }
   fi_smartcrop_params params;
 };
+
+// ---- device table heaps (fi_ctx::Heap) ------------------------------------
+constexpr size_t kHeapI = (size_t)1 << 30, kHeapF = (size_t)128 << 20, kHeapD = (size_t)128 << 20;  // elements
+constexpr size_t kAxisCacheMax = 8192, kScCacheMax = 4096, kImpCacheMax = 1024;
+
+static void heap_reset(fi_ctx *c) {
+  c->heap_i.used = c->heap_f.used = c->heap_d.used = 0;
+  c->axis_at.clear();
+  c->sc_at.clear();
+  c->imp_at.clear();
+  c->ring_at.clear();
+  c->strip_at.clear();
+  c->mv_at.clear();
+  c->vv_at.clear();
+  c->mh_at.clear();
+  c->mono_wts_at = -1;
+}
+// Before a batch places anything: evict oversized host caches (only here, so
+// no cached object a batch holds a pointer to is ever freed under it; the
+// heap placements keyed by those objects go with them), reset heaps past
+// three-quarters full, and hand the batch the heaps' used marks.
+static int heap_prepare(fi_ctx *c, Exec &E) {
+  if (c->axis_cache.size() > kAxisCacheMax || c->sc_cache.size() > kScCacheMax ||
+      c->imp_cache.size() > kImpCacheMax) {
+    c->axis_cache.clear();
+    c->ring_cache.clear();
+    c->strip_cache.clear();
+    c->mv_cache.clear();
+    c->mh_cache.clear();
+    c->vmv_cache.clear();
+    c->vmh_cache.clear();
+    c->sc_cache.clear();
+    c->imp_cache.clear();
+    heap_reset(c);
+  }
+  struct H {
+    fi_ctx::Heap *h;
+    size_t cap, esz;
+  } hs[3] = {{&c->heap_i, kHeapI, 4}, {&c->heap_f, kHeapF, 4}, {&c->heap_d, kHeapD, 8}};
+  for (auto &x : hs) {
+    if (!x.h->p) {
+      if (hipMalloc(&x.h->p, x.cap * x.esz) != hipSuccess) {
+        x.h->p = nullptr;
+        return set_err(FI_ENOMEM, "hipMalloc(%zu) of the table heap failed on device %d", x.cap * x.esz,
+                       c->device);
+      }
+      x.h->cap = x.cap;
+      x.h->used = 0;
+    }
+  }
+  if (c->heap_i.used > c->heap_i.cap / 4 * 3 || c->heap_f.used > c->heap_f.cap / 4 * 3 ||
+      c->heap_d.used > c->heap_d.cap / 4 * 3)
+    heap_reset(c);
+  E.bi = (int64_t)c->heap_i.used;
+  E.bf = (int64_t)c->heap_f.used;
+  E.bd = (int64_t)c->heap_d.used;
+  return FI_OK;
+}
+static bool heap_fits(const fi_ctx *c, const Exec &E) {
+  return (size_t)E.bi + E.ai.size() <= c->heap_i.cap && (size_t)E.bf + E.af.size() <= c->heap_f.cap &&
+         (size_t)E.bd + E.ad.size() <= c->heap_d.cap;
+}
+// Enqueue the copies of the batch's new tables (already uploaded in the blob
+// at ab + *_off) behind the heaps' used marks; advance the marks (16-element
+// aligned, so 16-byte aligned fragment tables stay aligned).
+static int heap_commit(fi_ctx *c, Exec &E, const uint8_t *ab, size_t ai_off, size_t af_off, size_t ad_off) {
+  if (!E.ai.empty())
+    HIP_TRY(hipMemcpyAsync((int32_t *)c->heap_i.p + E.bi, ab + ai_off, E.ai.size() * 4, hipMemcpyDeviceToDevice,
+                           c->stream));
+  if (!E.af.empty())
+    HIP_TRY(hipMemcpyAsync((float *)c->heap_f.p + E.bf, ab + af_off, E.af.size() * 4, hipMemcpyDeviceToDevice,
+                           c->stream));
+  if (!E.ad.empty())
+    HIP_TRY(hipMemcpyAsync((double *)c->heap_d.p + E.bd, ab + ad_off, E.ad.size() * 8, hipMemcpyDeviceToDevice,
+                           c->stream));
+  c->heap_i.used = ((size_t)E.bi + E.ai.size() + 15) / 16 * 16;
+  c->heap_f.used = ((size_t)E.bf + E.af.size() + 15) / 16 * 16;
+  c->heap_d.used = ((size_t)E.bd + E.ad.size() + 15) / 16 * 16;
+  if (c->timing) c->stats["heap_upload"].bytes += (double)(E.ai.size() * 4 + E.af.size() * 4 + E.ad.size() * 8);
+  return FI_OK;
+}
+
 
 static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, int in_sampled, int out_size,
                                  int o0, int o1, bool sample, int in_src, DevAxis *out,
@@ -345,40 +459,32 @@ static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, 
   auto key = std::make_tuple(filter, dbits(factor), in_sampled, out_size, o0, o1, (int)sample, in_src);
   auto it = c->axis_cache.find(key);
   if (it == c->axis_cache.end()) {
-    if (c->axis_cache.size() > 4096) {
-      c->axis_cache.clear();
-      c->ring_cache.clear();
-      c->strip_cache.clear();
-      c->mv_cache.clear();
-      c->mh_cache.clear();
-      c->vmv_cache.clear();
-      c->vmh_cache.clear();
-    }
     AxisTable t;
     build_axis(filter, factor, in_sampled, out_size, o0, o1, sample, in_src, &t);
     it = c->axis_cache.emplace(key, std::move(t)).first;
   }
   const AxisTable *t = &it->second;
-  auto pit = placed.find(t);
-  if (pit != placed.end()) {
+  (void)placed;
+  auto pit = c->axis_at.find(t);
+  if (pit != c->axis_at.end()) {
     *out = pit->second;
     return t;
   }
   DevAxis d{};
   d.n = (int32_t)t->start.size();
-  d.start = (int32_t)E.ai.size();
+  d.start = E.oi();
   E.ai.insert(E.ai.end(), t->start.begin(), t->start.end());
-  d.count = (int32_t)E.ai.size();
+  d.count = E.oi();
   E.ai.insert(E.ai.end(), t->count.begin(), t->count.end());
-  d.woff = (int32_t)E.ai.size();
-  const int32_t wbase = (int32_t)E.af.size();
+  d.woff = E.oi();
+  const int32_t wbase = E.of();
   for (int32_t w : t->woff) E.ai.push_back(w + wbase);
   E.af.insert(E.af.end(), t->w.begin(), t->w.end());
   d.maxtaps = t->maxtaps;
   d.src_lo = t->src_lo;
   d.src_hi = t->src_hi;
   d.touched = t->touched;
-  placed[t] = d;
+  c->axis_at[t] = d;
   *out = d;
   return t;
 }
@@ -443,12 +549,10 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
   const uint64_t ph = params_hash(E.params);
   // the fast pass's error bound assumes non-negative per-pixel terms
   const bool fast_ok = E.params.skin_bias >= 0 && E.params.saturation_bias >= 0;
-  struct Placed {
-    int32_t hb = 0, hk = 0, hkT = 0, vb = 0, vk = 0, crop0 = 0, ncrops = 0;
-    int32_t hmB = 0, hmC = 0, hmS0 = 0, vqA = 0, vqC = 0, vqK0 = 0;
+  struct Placed {  // per batch: the plan's crop list in this batch's crop array
+    int32_t crop0 = 0, ncrops = 0;
   };
   std::map<const ScPlan *, Placed> placed;
-  std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_placed;
   for (size_t k = 0; k < items.size(); k++) {
     const ScItem &it = items[k];
     const fi_smartcrop_options &o = it.opt;
@@ -457,7 +561,6 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     auto key = std::make_tuple(it.W, it.H, it.tw, it.th, okey);
     auto pit = c->sc_cache.find(key);
     if (pit == c->sc_cache.end()) {
-      if (c->sc_cache.size() > 4096) c->sc_cache.clear();
       ScPlan p;
       plan_sc(it.W, it.H, it.tw, it.th, o, &p);
       pit = c->sc_cache.emplace(key, std::move(p)).first;
@@ -482,35 +585,40 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     auto pp = placed.find(&P);
     if (pp == placed.end()) {
       Placed q;
-      if (P.thumb) {
-        q.hb = (int32_t)E.ai.size();
-        E.ai.insert(E.ai.end(), P.hb.begin(), P.hb.end());
-        q.hk = (int32_t)E.ai.size();
-        E.ai.insert(E.ai.end(), P.hk.begin(), P.hk.end());
-        q.hkT = (int32_t)E.ai.size();
-        E.ai.insert(E.ai.end(), P.hkT.begin(), P.hkT.end());
-        q.vb = (int32_t)E.ai.size();
-        E.ai.insert(E.ai.end(), P.vb.begin(), P.vb.end());
-        q.vk = (int32_t)E.ai.size();
-        E.ai.insert(E.ai.end(), P.vk.begin(), P.vk.end());
-        if (P.hm_ok) {
-          while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
-          q.hmB = (int32_t)E.ai.size();
-          E.ai.insert(E.ai.end(), P.hmB.begin(), P.hmB.end());
-          q.hmC = (int32_t)E.ai.size();
-          E.ai.insert(E.ai.end(), P.hmC.begin(), P.hmC.end());
-          q.hmS0 = (int32_t)E.ai.size();
-          E.ai.insert(E.ai.end(), P.hmS0.begin(), P.hmS0.end());
+      auto tp = c->sc_at.find(&P);
+      if (tp == c->sc_at.end()) {
+        fi_ctx::ScTabs t;
+        if (P.thumb) {
+          t.hb = E.oi();
+          E.ai.insert(E.ai.end(), P.hb.begin(), P.hb.end());
+          t.hk = E.oi();
+          E.ai.insert(E.ai.end(), P.hk.begin(), P.hk.end());
+          t.hkT = E.oi();
+          E.ai.insert(E.ai.end(), P.hkT.begin(), P.hkT.end());
+          t.vb = E.oi();
+          E.ai.insert(E.ai.end(), P.vb.begin(), P.vb.end());
+          t.vk = E.oi();
+          E.ai.insert(E.ai.end(), P.vk.begin(), P.vk.end());
+          if (P.hm_ok) {
+            while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
+            t.hmB = E.oi();
+            E.ai.insert(E.ai.end(), P.hmB.begin(), P.hmB.end());
+            t.hmC = E.oi();
+            E.ai.insert(E.ai.end(), P.hmC.begin(), P.hmC.end());
+            t.hmS0 = E.oi();
+            E.ai.insert(E.ai.end(), P.hmS0.begin(), P.hmS0.end());
+          }
+          if (P.vq_ok) {
+            while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
+            t.vqA = E.oi();
+            E.ai.insert(E.ai.end(), P.vqA.begin(), P.vqA.end());
+            t.vqC = E.oi();
+            E.ai.insert(E.ai.end(), P.vqC.begin(), P.vqC.end());
+            t.vqK0 = E.oi();
+            E.ai.insert(E.ai.end(), P.vqK0.begin(), P.vqK0.end());
+          }
         }
-        if (P.vq_ok) {
-          while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
-          q.vqA = (int32_t)E.ai.size();
-          E.ai.insert(E.ai.end(), P.vqA.begin(), P.vqA.end());
-          q.vqC = (int32_t)E.ai.size();
-          E.ai.insert(E.ai.end(), P.vqC.begin(), P.vqC.end());
-          q.vqK0 = (int32_t)E.ai.size();
-          E.ai.insert(E.ai.end(), P.vqK0.begin(), P.vqK0.end());
-        }
+        tp = c->sc_at.emplace(&P, t).first;
       }
       // crops + importance tables (one table per distinct window size)
       std::map<std::pair<uint64_t, uint64_t>, std::pair<int, int>> sizes;
@@ -528,19 +636,18 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
         auto ikey = std::make_tuple(sz.first.first, sz.first.second, nx, ny, ph);
         auto iit = c->imp_cache.find(ikey);
         if (iit == c->imp_cache.end()) {
-          if (c->imp_cache.size() > 1024) c->imp_cache.clear();
           std::vector<double> t;
           sc_importance_table(E.params, fw, fh, nx, ny, &t);
           iit = c->imp_cache.emplace(ikey, std::move(t)).first;
         }
         auto pk = std::make_pair(&iit->second, nx);
-        auto ip = imp_placed.find(pk);
-        if (ip == imp_placed.end()) {
+        auto ip = c->imp_at.find(pk);
+        if (ip == c->imp_at.end()) {
           double imax = 0;
           for (double v : iit->second) imax = std::max(imax, std::fabs(v));
-          const int32_t off = (int32_t)E.ad.size();
+          const int32_t off = E.od();
           E.ad.insert(E.ad.end(), iit->second.begin(), iit->second.end());
-          ip = imp_placed.emplace(pk, std::make_pair(off, imax)).first;
+          ip = c->imp_at.emplace(pk, std::make_pair(off, imax)).first;
         }
         tab_of[sz.first] = std::make_tuple(ip->second.first, nx, ip->second.second);
       }
@@ -569,6 +676,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
       pp = placed.emplace(&P, q).first;
     }
     const Placed &q = pp->second;
+    const fi_ctx::ScTabs &T = c->sc_at.at(&P);
     const bool prep = c->sc_prep && P.prep_ok;
     d.img = it.img;
     d.stride = it.stride;
@@ -587,24 +695,24 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.hrows = P.hrows;
     d.ksh = P.ksh;
     d.ksv = P.ksv;
-    d.hb = q.hb;
-    d.hk = q.hk;
-    d.hkT = q.hkT;
-    d.vb = q.vb;
-    d.vk = q.vk;
+    d.hb = T.hb;
+    d.hk = T.hk;
+    d.hkT = T.hkT;
+    d.vb = T.vb;
+    d.vk = T.vk;
     d.prep = prep ? 1 : 0;
     d.hm = prep && P.hm_ok && c->sc_mfma ? 1 : 0;
     d.hm_rows = P.hm_rows;
     d.hm_ks = P.hm_ks;
     d.hm_pitch = P.hm_pitch;
     d.hm_nb = P.hm_nb;
-    d.hmB = q.hmB;
-    d.hmC = q.hmC;
-    d.hmS0 = q.hmS0;
+    d.hmB = T.hmB;
+    d.hmC = T.hmC;
+    d.hmS0 = T.hmS0;
     d.vq = prep && P.vq_ok && c->sc_vq ? 1 : 0;
-    d.vqA = q.vqA;
-    d.vqC = q.vqC;
-    d.vqK0 = q.vqK0;
+    d.vqA = T.vqA;
+    d.vqC = T.vqC;
+    d.vqK0 = T.vqK0;
     d.prescale = P.prescale;
     d.exact_all = o.exact_all || !fast_ok;
     // workspace (offsets; converted to pointers after allocation)
@@ -774,6 +882,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   Exec E;
   E.c = c;
   fi_smartcrop_default_params(&E.params);
+  {
+    const int hrc = heap_prepare(c, E);
+    if (hrc) return hrc;
+  }
   std::vector<ImPlan> plans(n);
   std::vector<int> status(n, FI_OK);
   std::vector<std::string> errs(n);
@@ -782,11 +894,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   std::vector<ScItem> sitems;
   std::vector<int> sc_of(n, -1);
   std::map<const AxisTable *, DevAxis> placed;
-  std::map<const RingTable *, std::array<int32_t, 4>> ring_placed;
   std::vector<const RingTable *> fused_ring;
   std::vector<const AxisTable *> fused_h;
   std::vector<const std::vector<StripTab> *> fused_strips_of;
-  std::map<const StripTab *, std::pair<int32_t, int32_t>> strip_placed;
   std::vector<int> fused_img;  // indices into rd
   std::vector<int> mfma_img;   // indices into rd (mode 4)
   std::vector<const MfmaV *> mfma_v;
@@ -970,18 +1080,18 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         d.mode = 3;  // fused vertical-first
         d.fused_k = ring->K;
         d.ring_n = (int32_t)ring->rows.size();
-        auto pr = ring_placed.find(ring);
-        if (pr == ring_placed.end()) {
+        auto pr = c->ring_at.find(ring);
+        if (pr == c->ring_at.end()) {
           std::array<int32_t, 4> o;
-          o[0] = (int32_t)E.ai.size();
+          o[0] = E.oi();
           E.ai.insert(E.ai.end(), ring->rows.begin(), ring->rows.end());
-          o[1] = (int32_t)E.af.size();
+          o[1] = E.of();
           E.af.insert(E.af.end(), ring->ringw.begin(), ring->ringw.end());
-          o[2] = (int32_t)E.ai.size();
+          o[2] = E.oi();
           E.ai.insert(E.ai.end(), ring->ringy.begin(), ring->ringy.end());
-          o[3] = (int32_t)E.ai.size();
+          o[3] = E.oi();
           E.ai.insert(E.ai.end(), ring->flush.begin(), ring->flush.end());
-          pr = ring_placed.emplace(ring, o).first;
+          pr = c->ring_at.emplace(ring, o).first;
         }
         d.ring_rows = pr->second[0];
         d.ring_w = pr->second[1];
@@ -1036,6 +1146,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       (void)0;
     }
   }
+  const double t_images = now_ms();
   // smartcrop planning
   ScLaunchData SL;
   std::vector<int> sstatus(sitems.size(), FI_OK);
@@ -1087,6 +1198,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   }
   for (int i = 0; i < n; i++)
     if (sc_of[i] >= 0) SL.descs[sc_of[i]].img = out_of[i];
+  const double t_sc = now_ms();
   // ---- build launches
   std::vector<int> m0, m1, m2;
   for (size_t k = 0; k < rd.size(); k++) {
@@ -1116,13 +1228,13 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         const int y0 = (int)((int64_t)d.eh * b / B), y1 = (int)((int64_t)d.eh * (b + 1) / B);
         if (y1 <= y0) continue;
         for (const StripTab &st : strips) {
-          auto sp = strip_placed.find(&st);
-          if (sp == strip_placed.end()) {
-            const int32_t so = (int32_t)E.ai.size();
+          auto sp = c->strip_at.find(&st);
+          if (sp == c->strip_at.end()) {
+            const int32_t so = E.oi();
             E.ai.insert(E.ai.end(), st.starts.begin(), st.starts.end());
-            const int32_t wo = (int32_t)E.af.size();
+            const int32_t wo = E.of();
             E.af.insert(E.af.end(), st.wT.begin(), st.wT.end());
-            sp = strip_placed.emplace(&st, std::make_pair(so, wo)).first;
+            sp = c->strip_at.emplace(&st, std::make_pair(so, wo)).first;
           }
           FusedTile t = st.t;
           t.hstart = sp->second.first;
@@ -1151,11 +1263,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       while (E.ai.size() % 4) E.ai.push_back(0);
     };
     auto put = [&](const std::vector<int32_t> &v) {
-      const int32_t o = (int32_t)E.ai.size();
+      const int32_t o = E.oi();
       E.ai.insert(E.ai.end(), v.begin(), v.end());
       return o;
     };
-    std::map<const MfmaV *, std::array<int32_t, 5>> vplaced;
     std::map<const MfmaH *, std::pair<int32_t, int32_t>> hplaced;  // first strip, hwsum
     std::vector<std::array<int32_t, 3>> mpairs;                       // (image, strip, mfma index)
     const int nm = (int)mfma_img.size();
@@ -1163,8 +1274,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       const ResizeDesc &d = rd[mfma_img[q]];
       const MfmaV &V = *mfma_v[q];
       const MfmaH &H = *mfma_h[q];
-      auto vp = vplaced.find(&V);
-      if (vp == vplaced.end()) {
+      auto vp = c->mv_at.find(&V);
+      if (vp == c->mv_at.end()) {
         std::array<int32_t, 5> o;
         o[0] = put(V.rows);
         o[1] = put(V.ya);
@@ -1172,16 +1283,22 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         o[4] = put(V.wsum);
         align4();
         o[3] = put(V.frag);
-        vp = vplaced.emplace(&V, o).first;
+        vp = c->mv_at.emplace(&V, o).first;
       }
       auto hp = hplaced.find(&H);
       if (hp == hplaced.end()) {
         const int32_t first = (int32_t)mstrips.size();
-        const int32_t hw = put(H.wsum);
-        align4();
-        const int32_t frag = put(H.frag);
-        const int32_t s0 = put(H.s0);
-        const int32_t lut = put(H.lut);
+        auto ht = c->mh_at.find(&H);
+        if (ht == c->mh_at.end()) {
+          std::array<int32_t, 4> o;
+          o[0] = put(H.wsum);
+          align4();
+          o[1] = put(H.frag);
+          o[2] = put(H.s0);
+          o[3] = put(H.lut);
+          ht = c->mh_at.emplace(&H, o).first;
+        }
+        const int32_t hw = ht->second[0], frag = ht->second[1], s0 = ht->second[2], lut = ht->second[3];
         for (const MfmaStrip &st : H.strips) {
           MStrip m{};
           m.x0 = st.x0;
@@ -1241,6 +1358,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       }
     }
   }
+  const double t_tiles0 = now_ms();
   // streaming MFMA tiles (k_rs_vm): (image, strip, band of blocks); tables placed once per geometry
   std::vector<VDesc> vdescs;
   std::vector<MStrip> vstrips;
@@ -1251,11 +1369,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       while (E.ai.size() % 4) E.ai.push_back(0);
     };
     auto put = [&](const std::vector<int32_t> &v) {
-      const int32_t o = (int32_t)E.ai.size();
+      const int32_t o = E.oi();
       E.ai.insert(E.ai.end(), v.begin(), v.end());
       return o;
     };
-    std::map<const VmV *, std::array<int32_t, 8>> vplaced;
     std::map<const MfmaH *, std::pair<int32_t, int32_t>> hplaced;  // first strip, hwsum
     struct Work1 {
       int32_t img, first_strip, nstrips;
@@ -1267,8 +1384,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       const ResizeDesc &d = rd[vm_img[q]];
       const VmV &V = *vm_v[q];
       const MfmaH &H = *vm_h[q];
-      auto vp = vplaced.find(&V);
-      if (vp == vplaced.end()) {
+      auto vp = c->vv_at.find(&V);
+      if (vp == c->vv_at.end()) {
         std::array<int32_t, 8> o;
         std::vector<int32_t> meta;
         for (size_t k = 0; k < V.plo.size(); k++) {
@@ -1288,16 +1405,22 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         o[5] = put(V.w128);
         align4();
         o[6] = put(V.frag);
-        vp = vplaced.emplace(&V, o).first;
+        vp = c->vv_at.emplace(&V, o).first;
       }
       auto hp = hplaced.find(&H);
       if (hp == hplaced.end()) {
         const int32_t first = (int32_t)vstrips.size();
-        const int32_t hw = put(H.wsum);
-        align4();
-        const int32_t frag = put(H.frag);
-        const int32_t s0 = put(H.s0);
-        const int32_t lut = put(H.lut);
+        auto ht = c->mh_at.find(&H);
+        if (ht == c->mh_at.end()) {
+          std::array<int32_t, 4> o;
+          o[0] = put(H.wsum);
+          align4();
+          o[1] = put(H.frag);
+          o[2] = put(H.s0);
+          o[3] = put(H.lut);
+          ht = c->mh_at.emplace(&H, o).first;
+        }
+        const int32_t hw = ht->second[0], frag = ht->second[1], s0 = ht->second[2], lut = ht->second[3];
         for (const MfmaStrip &st : H.strips) {
           MStrip m{};
           m.x0 = st.x0;
@@ -1374,6 +1497,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       for (int x = 0; x < 8; x++)
         if (i < q8[x].size()) vtiles.push_back(q8[x][i]);
   }
+  const double t_tiles = now_ms();
   Blob &B = E.blob;
   const size_t all_rd_off = B.addv(rd);
   const size_t mdesc_off = B.addv(mdescs), mstrip_off = B.addv(mstrips), mtile_off = B.addv(mtiles);
@@ -1411,10 +1535,12 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   const size_t apply_off = B.addv(apply);
   const size_t mono_off = B.addv(mdesc_mono);
   size_t mono_wts = 0;
-  if (!mono.empty()) {
+  if (!mono.empty() && c->mono_wts_at >= 0) mono_wts = (size_t)c->mono_wts_at;
+  if (!mono.empty() && c->mono_wts_at < 0) {
     // the Riemersma error-queue weights (quantize.c), computed with libm at run
     // time exactly as oracle/fi_oracle.c does
-    mono_wts = E.ad.size();
+    mono_wts = (size_t)E.od();
+    c->mono_wts_at = (int32_t)mono_wts;
     volatile double qr1 = 65535.0 + 1.0, span = 16 - 1.0;
     const double step = exp(log((double)qr1) / (double)span);
     double weight = 1.0, wts[16];
@@ -1425,6 +1551,15 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     E.ad.insert(E.ad.end(), wts, wts + 16);
   }
   const size_t ai_off = B.addv(E.ai), af_off = B.addv(E.af), ad_off = B.addv(E.ad);
+  if (!heap_fits(c, E)) {
+    // the batch's new tables overflow the heaps: start them empty and plan again
+    if (c->heap_retry) return set_err(FI_ENOMEM, "batch tables exceed the device table heap");
+    heap_reset(c);
+    c->heap_retry = true;
+    const int rrc = run_batch(c, imgs, n, async);
+    c->heap_retry = false;
+    return rrc;
+  }
   // ---- upload (pinned slot: the previous batch may still be running)
   const int slot = c->next_slot;
   rc = wait_slot(c, slot);
@@ -1442,11 +1577,18 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   HIP_TRY(hipMemcpyAsync(c->arena.p, S.blob, B.b.size(), hipMemcpyHostToDevice, c->stream));
   const double t_planned = now_ms();
   host_stat(c, "host_plan", t_planned - t_start);
+  host_stat(c, "host_plan_images", t_images - t_start);
+  host_stat(c, "host_plan_sc", t_sc - t_images);
+  host_stat(c, "host_plan_tiles", t_tiles - t_sc);
+  host_stat(c, "host_plan_vmtiles", t_tiles - t_tiles0);
+  host_stat(c, "host_plan_blob", t_planned - t_tiles);
   if (c->timing) c->stats["host_plan"].bytes += (double)B.b.size();
   uint8_t *ab = (uint8_t *)c->arena.p;
-  const int32_t *ai = (const int32_t *)(ab + ai_off);
-  const float *af = (const float *)(ab + af_off);
-  const double *ad = (const double *)(ab + ad_off);
+  rc = heap_commit(c, E, ab, ai_off, af_off, ad_off);
+  if (rc) return rc;
+  const int32_t *ai = (const int32_t *)c->heap_i.p;
+  const float *af = (const float *)c->heap_f.p;
+  const double *ad = (const double *)c->heap_d.p;
   const ScParamsDev PD = to_dev(E.params);
   auto desc_p = [&](const Launch &L) { return ab + L.desc_off; };
   auto pre_p = [&](const Launch &L) { return (const int32_t *)(ab + L.prefix_off); };
@@ -1618,6 +1760,10 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   Exec E;
   E.c = c;
   E.params = params;
+  {
+    const int hrc = heap_prepare(c, E);
+    if (hrc) return hrc;
+  }
   std::vector<ScItem> items(1);
   items[0].img = d_img;
   items[0].stride = stride;
@@ -1648,6 +1794,7 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   ScLaunches SX;
   add_sc_launches(c, B, SL, st, &SX);
   const size_t ai_off = B.addv(E.ai), ad_off = B.addv(E.ad);
+  if (!heap_fits(c, E)) return set_err(FI_ENOMEM, "smartcrop tables exceed the device table heap");
   rc = ensure(c, &c->arena, B.b.size() + 256);
   if (rc) return rc;
   rc = ensure_pinned(c, B.b.size() + 256);
@@ -1655,7 +1802,9 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   memcpy(c->pinned, B.b.data(), B.b.size());
   HIP_TRY(hipMemcpyAsync(c->arena.p, c->pinned, B.b.size(), hipMemcpyHostToDevice, c->stream));
   uint8_t *ab = (uint8_t *)c->arena.p;
-  rc = enqueue_sc(c, ab, SX, (const int32_t *)(ab + ai_off), (const double *)(ab + ad_off),
+  rc = heap_commit(c, E, ab, ai_off, ai_off, ad_off);
+  if (rc) return rc;
+  rc = enqueue_sc(c, ab, SX, (const int32_t *)c->heap_i.p, (const double *)c->heap_d.p,
                   (CropScore *)(wb + scores_off), (ScResult *)(wb + results_off), to_dev(params));
   if (rc) return rc;
   scores->resize(SL.nscores);
