@@ -191,7 +191,10 @@ def im_convert(src: np.ndarray, rw=0, rh=0, flags=FLAG_THUMBNAIL, gravity=5, rot
     """convert <src> <resize op> [-gravity g -extent WxH] [-colorspace Gray] [-monochrome] [-rotate r]."""
     src = np.ascontiguousarray(src, dtype=np.uint8)
     H, W = src.shape[:2]
-    cap = max(W * H * 3, 1) * 64 + (rw or 1) * (rh or 1) * 3 * 4
+    tw, th = W, H
+    if rw or rh:
+        tw, th = im_meta_geometry(W, H, rw, rh, bool(flags & FLAG_FILL), bool(flags & FLAG_SHRINK))
+    cap = 3 * (max(tw, rw or 0) * max(th, rh or 0) + 16)  # output bound (an int32 on the C side)
     out = np.zeros(cap, np.uint8)
     ow, oh, oc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     rc = lib().or_im_convert(_u8(src), W, H, W * 3, rw, rh, flags, gravity, rotate, _u8(out), cap,
