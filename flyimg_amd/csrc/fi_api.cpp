@@ -55,6 +55,10 @@ __global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
 size_t mfma_lds_bytes(int nblocks);
 int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const MTile *tiles, int ntiles,
                 const int32_t *ai, size_t lds);
+// tiled horizontal-first pass 1 (fi_kernels.hip)
+constexpr int kHTileRows = 8;
+int launch_rs_h_tile(hipStream_t s, const ResizeDesc *descs, const int32_t *prefix, int n, int tiles,
+                     const int32_t *ai, const float *af, int pitch);
 // -monochrome (fi_mono.hip)
 size_t mono_lds_bytes();
 int launch_mono(hipStream_t s, const MonoDesc *descs, int n, const double *wts);
@@ -902,6 +906,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   std::vector<const MfmaV *> mfma_v;
   std::vector<const MfmaH *> mfma_h;
   std::vector<int> vm_img;     // indices into rd (mode 5)
+  int h_tile_pitch = 0;        // k_rs_h_tile: max staged row bytes over the mode-2 images
   std::vector<const VmV *> vm_v;
   std::vector<const MfmaH *> vm_h;
   // per image resized-buffer workspace offsets (for smartcrop-apply)
@@ -1116,6 +1121,12 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         d.mid_rows = d.v.src_hi - d.v.src_lo;
         d.mid_cols = P.ew;
         d.mid_stride = (3 * P.ew + 7) / 8 * 8;
+        // k_rs_h_tile LDS row pitch: the source bytes of a 256-column chunk's windows
+        for (int x0 = 0; x0 < P.ew; x0 += 256) {
+          const int x1 = std::min(P.ew, x0 + 256);
+          const int lo = ht->start[x0], hi = ht->start[x1 - 1] + ht->count[x1 - 1];
+          h_tile_pitch = std::max(h_tile_pitch, (3 * (hi - lo) + 8 + 15) / 16 * 16);
+        }
       }
       if (d.mode != 3 && d.mode != 4 && d.mode != 5) {
         d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
@@ -1507,7 +1518,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
   Launch L0 = add_launch(B, rd, m0, eh_tiles);
   Launch L1a = add_launch(B, rd, m1, eh_tiles);
-  Launch L2a = add_launch(B, rd, m2, mid_tiles);
+  const bool h_tiled = (size_t)kHTileRows * h_tile_pitch <= 64 * 1024;
+  Launch L2a = h_tiled ? add_launch(B, rd, m2, [](const ResizeDesc &d) {
+    return ((d.mid_rows + kHTileRows - 1) / kHTileRows) * ((d.ew + 255) / 256);
+  }) : add_launch(B, rd, m2, mid_tiles);
   Launch L2b = add_launch(B, rd, m2, eh_tiles);
   ScLaunches SX;
   add_sc_launches(c, B, SL, sstatus, &SX);
@@ -1623,8 +1637,12 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
                            (const ResizeDesc *)desc_p(L1a), pre_p(L1a), L1a.n, ai, af);
       }
       if (L2a.tiles) {
-        hipLaunchKernelGGL(k_rs_h_u8, dim3(L2a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L2a),
-                           pre_p(L2a), L2a.n, ai, af);
+        if (h_tiled)
+          launch_rs_h_tile(c->stream, (const ResizeDesc *)desc_p(L2a), pre_p(L2a), L2a.n, L2a.tiles, ai, af,
+                           h_tile_pitch);
+        else
+          hipLaunchKernelGGL(k_rs_h_u8, dim3(L2a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L2a),
+                             pre_p(L2a), L2a.n, ai, af);
         hipLaunchKernelGGL(k_rs_v_final, dim3(L2b.tiles), dim3(256), 0, c->stream,
                            (const ResizeDesc *)desc_p(L2b), pre_p(L2b), L2b.n, ai, af);
       }

@@ -180,6 +180,89 @@ __global__ __launch_bounds__(256) void k_rs_h_u8(const ResizeDesc *__restrict__ 
   }
 }
 
+// H-first, pass 1 (tiled): one workgroup = (image, 8 mid rows, 256 output
+// columns).  The source bytes the 256 columns' windows touch are staged in
+// LDS for the 8 rows with coalesced dword loads; each thread then reads every
+// weight once for 8 rows (the per-row kernel above re-fetched the weights and
+// gathered the source bytes from global memory row by row).  Same fp32
+// operation order per output as k_rs_h_u8, so the same Q16 values.
+constexpr int kHTRows = 8;
+__global__ __launch_bounds__(256) void k_rs_h_tile(const ResizeDesc *__restrict__ descs,
+                                                   const int32_t *__restrict__ prefix, int nimg,
+                                                   const int32_t *__restrict__ ai, const float *__restrict__ af,
+                                                   int pitch) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t hl[];  // [kHTRows][pitch]
+  const int t = blockIdx.x;
+  const int i = find_image(prefix, nimg, t);
+  const ResizeDesc &D = descs[i];
+  const int ncc = (D.ew + 255) >> 8, lt = t - prefix[i];
+  const int rb = lt / ncc, cc = lt - rb * ncc;
+  const int r0 = rb * kHTRows, nr = min(kHTRows, D.mid_rows - r0);
+  const int x0 = cc * 256, x1 = min(D.ew, x0 + 256);
+  const int s_lo = ai[D.h.start + x0];
+  const int s_hi = ai[D.h.start + x1 - 1] + ai[D.h.count + x1 - 1];
+  const int tid = threadIdx.x;
+  int shr[kHTRows];
+#pragma unroll
+  for (int r = 0; r < kHTRows; r++) {
+    const uint8_t *row = D.src + (int64_t)(D.mid_r0 + r0 + min(r, nr - 1)) * D.src_stride;
+    shr[r] = (int)(((uintptr_t)row + 3 * (uintptr_t)s_lo) & 3u);
+  }
+  {
+    // dwords wholly inside the window's bytes, then the tail bytes one by one
+    // (never a byte past the window: the source may end right after it)
+    const int ndw = (3 * (s_hi - s_lo) + 3 + 3) >> 2;
+    for (int it = tid; it < nr * ndw; it += 256) {
+      const int r = it / ndw, k = it - r * ndw;
+      const uint8_t *row = D.src + (int64_t)(D.mid_r0 + r0 + r) * D.src_stride;
+      const uintptr_t a0 = ((uintptr_t)row + 3 * (uintptr_t)s_lo) & ~(uintptr_t)3;
+      const uintptr_t end = (uintptr_t)row + 3 * (uintptr_t)s_hi;
+      uint32_t v;
+      if (a0 + 4 * (uintptr_t)k + 4 <= end) {
+        v = reinterpret_cast<const uint32_t *>(a0)[k];
+      } else {
+        v = 0;
+        for (int b = 0; b < 4; b++) {
+          const uintptr_t a = a0 + 4 * (uintptr_t)k + b;
+          if (a >= (uintptr_t)row + 3 * (uintptr_t)s_lo && a < end) v |= (uint32_t)(*(const uint8_t *)a) << (8 * b);
+        }
+      }
+      reinterpret_cast<uint32_t *>(hl + r * pitch)[k] = v;
+    }
+  }
+  __syncthreads();
+  const int x = x0 + tid;
+  if (x >= x1) return;
+  const int s = ai[D.h.start + x], n = ai[D.h.count + x];
+  const float *w = af + ai[D.h.woff + x];
+  float acc[kHTRows][3];
+#pragma unroll
+  for (int r = 0; r < kHTRows; r++) acc[r][0] = acc[r][1] = acc[r][2] = 0.f;
+  for (int j = 0; j < n; j++) {
+    const float wj = w[j];
+    const int o = 3 * (s + j - s_lo);
+#pragma unroll
+    for (int r = 0; r < kHTRows; r++) {
+      const uint8_t *p = hl + r * pitch + shr[r] + o;
+      acc[r][0] += wj * (float)p[0];
+      acc[r][1] += wj * (float)p[1];
+      acc[r][2] += wj * (float)p[2];
+    }
+  }
+  for (int r = 0; r < nr; r++) {
+    uint16_t *out = D.mid + (int64_t)(r0 + r) * D.mid_stride;
+    out[3 * x + 0] = (uint16_t)clamp_q16(acc[r][0] * 257.0f);
+    out[3 * x + 1] = (uint16_t)clamp_q16(acc[r][1] * 257.0f);
+    out[3 * x + 2] = (uint16_t)clamp_q16(acc[r][2] * 257.0f);
+  }
+}
+int launch_rs_h_tile(hipStream_t s, const ResizeDesc *descs, const int32_t *prefix, int n, int tiles,
+                     const int32_t *ai, const float *af, int pitch) {
+  if (tiles <= 0) return 0;
+  hipLaunchKernelGGL(k_rs_h_tile, dim3(tiles), dim3(256), (size_t)kHTRows * pitch, s, descs, prefix, n, ai, af, pitch);
+  return 0;
+}
+
 // H-first, pass 2: out[y][x] = Q16(sum_j w[y][j] * mid[start_y + j - r0][3x + c]) + epilogue
 __global__ __launch_bounds__(256) void k_rs_v_final(const ResizeDesc *__restrict__ descs,
                                                     const int32_t *__restrict__ prefix, int nimg,
