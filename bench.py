@@ -155,7 +155,9 @@ def main():
     ow, oh, oc = fi_plan(W, H, op)
     dst_cap = ow * oh * oc
     pool = ctx.malloc(src_bytes * nimg)
-    dst = ctx.malloc(dst_cap * nimg)
+    # one output set per in-flight batch: batch k+1 resamples while batch k's
+    # smart-crop stage still reads its resized outputs
+    dsts = [ctx.malloc(dst_cap * nimg) for _ in range(2)]
     t0 = time.perf_counter()
     for i in range(nimg):
         ctx.fill_synthetic(pool + i * src_bytes, W, H, src_stride, 0x5EED + rank * nimg + i)
@@ -164,7 +166,7 @@ def main():
     # runs (fi_submit_batch_device); batch k's records are finalized and
     # gathered once k+1 is queued.
     arrs = [(L.FiImage * nimg)() for _ in range(2)]
-    for arr in arrs:
+    for arr, dst in zip(arrs, dsts):
         for i in range(nimg):
             a = arr[i]
             a.src, a.src_w, a.src_h, a.src_stride, a.src_channels = pool + i * src_bytes, W, H, src_stride, 3
@@ -273,7 +275,8 @@ def main():
                 result["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(result), flush=True)
     ctx.free(pool)
-    ctx.free(dst)
+    for d in dsts:
+        ctx.free(d)
     comm.close()
     ctx.close()
 

@@ -141,8 +141,14 @@ struct Slot {
   size_t blob_cap = 0;
   void *res = nullptr;
   size_t res_cap = 0;
-  hipEvent_t done = nullptr;  // recorded after the batch's last readback
+  hipEvent_t done = nullptr;  // recorded (on sc_stream) after the batch's last readback
+  hipEvent_t rs_done = nullptr;  // resample stage of the batch done (main stream)
   bool busy = false;
+  // device buffers of the in-flight batch: the uploaded blob (descriptors) and
+  // the workspace (intermediates, smartcrop scratch, scores, results).  Per
+  // slot, because batch k+1's upload and resample run while batch k's
+  // smartcrop stage still reads its own.
+  DevBuf arena, work;
 };
 constexpr int kSlots = 2;
 struct fi_ctx {
@@ -150,7 +156,8 @@ struct fi_ctx {
   Slot slots[kSlots];
   int next_slot = 0;
   std::vector<PendingBatch> inflight;  // submission order
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;     // upload, resample, mono
+  hipStream_t sc_stream = nullptr;  // smartcrop stage + crop apply + readback of a batch (waits for its resample)
   std::mutex mu;
   DevBuf arena, work, io;
   void *pinned = nullptr;
@@ -206,9 +213,13 @@ struct fi_ctx {
   bool sc_mfma = true;  // FI_DISABLE_SC_MFMA=1: VALU horizontal pass (k_sc_hrows) instead of k_sc_hmfma
 };
 
+static void sync_streams(fi_ctx *c) {
+  (void)hipStreamSynchronize(c->stream);
+  if (c->sc_stream != c->stream) (void)hipStreamSynchronize(c->sc_stream);
+}
 static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
   if (b->cap >= bytes) return FI_OK;
-  (void)hipStreamSynchronize(c->stream);  // in-flight batches may still read it
+  sync_streams(c);  // in-flight batches may still read it
   if (b->p) (void)hipFree(b->p);
   b->p = nullptr;
   b->cap = 0;
@@ -255,21 +266,24 @@ static hipEvent_t get_event(fi_ctx *c) {
   (void)hipEventCreate(&e);
   return e;
 }
-struct Timer {
+struct Timer {  // HIP-event range: starts on stream sa, ends on stream sb
   fi_ctx *c;
   TimedRange r;
   bool on;
-  Timer(fi_ctx *c_, const char *name, double bytes) : c(c_), on(c_->timing) {
+  hipStream_t sb;
+  Timer(fi_ctx *c_, const char *name, double bytes) : Timer(c_, name, bytes, c_->stream, c_->stream) {}
+  Timer(fi_ctx *c_, const char *name, double bytes, hipStream_t sa, hipStream_t sb_)
+      : c(c_), on(c_->timing), sb(sb_) {
     if (!on) return;
     r.name = name;
     r.bytes = bytes;
     r.a = get_event(c);
     r.b = get_event(c);
-    (void)hipEventRecord(r.a, c->stream);
+    (void)hipEventRecord(r.a, sa);
   }
   ~Timer() {
     if (!on) return;
-    (void)hipEventRecord(r.b, c->stream);
+    (void)hipEventRecord(r.b, sb);
     c->pending.push_back(r);
   }
 };
@@ -380,6 +394,8 @@ constexpr size_t kHeapI = (size_t)1 << 30, kHeapF = (size_t)128 << 20, kHeapD = 
 constexpr size_t kAxisCacheMax = 8192, kScCacheMax = 4096, kImpCacheMax = 1024;
 
 static void heap_reset(fi_ctx *c) {
+  // work queued on either stream may still read tables the next batch overwrites
+  sync_streams(c);
   c->heap_i.used = c->heap_f.used = c->heap_d.used = 0;
   c->axis_at.clear();
   c->sc_at.clear();
@@ -835,34 +851,34 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->nsg = (int)sg.size();
   X->crops_off = B.addv(SL.crops);
 }
-static int enqueue_sc(fi_ctx *c, uint8_t *ab, const ScLaunches &X, const int32_t *ai, const double *ad,
-                      CropScore *scores, ScResult *results, const ScParamsDev &PD) {
+static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &X, const int32_t *ai,
+                      const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &PD) {
   auto desc = [&](const Launch &L) { return (const ScDesc *)(ab + L.desc_off); };
   auto pre = [&](const Launch &L) { return (const int32_t *)(ab + L.prefix_off); };
   {
-    Timer t(c, "sc_prep", 0);
+    Timer t(c, "sc_prep", 0, st, st);
     if (X.red.tiles)
-      hipLaunchKernelGGL(k_sc_reduce, dim3(X.red.tiles), dim3(256), 0, c->stream, desc(X.red), pre(X.red), X.red.n);
-    if (launch_sc_h(c->stream, true, (const ScDesc *)(ab + X.hm_off), X.nhm, X.hm_chunks, X.hm_lds, ai) != 0 ||
-        launch_sc_h(c->stream, false, (const ScDesc *)(ab + X.hv_off), X.nhv, X.h_chunks, X.h_lds, ai) != 0 ||
-        launch_sc_v(c->stream, (const ScDesc *)(ab + X.prep_off), X.nprep, X.v_chunks, X.v_lds, ai, PD) != 0 ||
-        launch_sc_vq(c->stream, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0)
+      hipLaunchKernelGGL(k_sc_reduce, dim3(X.red.tiles), dim3(256), 0, st, desc(X.red), pre(X.red), X.red.n);
+    if (launch_sc_h(st, true, (const ScDesc *)(ab + X.hm_off), X.nhm, X.hm_chunks, X.hm_lds, ai) != 0 ||
+        launch_sc_h(st, false, (const ScDesc *)(ab + X.hv_off), X.nhv, X.h_chunks, X.h_lds, ai) != 0 ||
+        launch_sc_v(st, (const ScDesc *)(ab + X.prep_off), X.nprep, X.v_chunks, X.v_lds, ai, PD) != 0 ||
+        launch_sc_vq(st, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0)
       return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d)", X.hm_lds, X.h_lds, X.v_lds);
     if (X.hp.tiles)
-      hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, c->stream, desc(X.hp), pre(X.hp), X.hp.n, ai);
+      hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, st, desc(X.hp), pre(X.hp), X.hp.n, ai);
     if (X.vp.tiles)
-      hipLaunchKernelGGL(k_sc_vpass, dim3(X.vp.tiles), dim3(256), 0, c->stream, desc(X.vp), pre(X.vp), X.vp.n, ai);
+      hipLaunchKernelGGL(k_sc_vpass, dim3(X.vp.tiles), dim3(256), 0, st, desc(X.vp), pre(X.vp), X.vp.n, ai);
     if (X.maps.tiles)
-      hipLaunchKernelGGL(k_sc_maps, dim3(X.maps.tiles), dim3(256), 0, c->stream, desc(X.maps), pre(X.maps),
+      hipLaunchKernelGGL(k_sc_maps, dim3(X.maps.tiles), dim3(256), 0, st, desc(X.maps), pre(X.maps),
                          X.maps.n, PD);
   }
   {
-    Timer t(c, "sc_score", 0);
+    Timer t(c, "sc_score", 0, st, st);
     const DevCrop *crops = (const DevCrop *)(ab + X.crops_off);
-    if (launch_sc_score(c->stream, true, (const ScDesc *)(ab + X.sl_off), X.nsl, X.sl_px, crops, ad, scores,
+    if (launch_sc_score(st, true, (const ScDesc *)(ab + X.sl_off), X.nsl, X.sl_px, crops, ad, scores,
                         results, PD) != 0)
       return set_err(FI_EDEVICE, "k_sc_score2 launch rejected (%d px)", X.sl_px);
-    (void)launch_sc_score(c->stream, false, (const ScDesc *)(ab + X.sg_off), X.nsg, 0, crops, ad, scores, results,
+    (void)launch_sc_score(st, false, (const ScDesc *)(ab + X.sg_off), X.nsg, 0, crops, ad, scores, results,
                           PD);
   }
   HIP_TRY(hipGetLastError());
@@ -1172,9 +1188,15 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   const size_t results_off = E.work.take(sizeof(ScResult) * std::max<size_t>(sitems.size(), 1));
   const size_t scores_off = E.work.take(sizeof(CropScore) * std::max(SL.nscores, 1));
   const size_t outwh_off = E.work.take(sizeof(int32_t) * 2 * std::max(n, 1));
-  int rc = ensure(c, &c->work, E.work.size + 256);
+  // the batch's slot: pinned staging + device blob/workspace (the batch that
+  // used it last must be done before anything here is overwritten)
+  const int slot = c->next_slot;
+  int rc = wait_slot(c, slot);
   if (rc) return rc;
-  uint8_t *wb = (uint8_t *)c->work.p;
+  Slot &S = c->slots[slot];
+  rc = ensure(c, &S.work, E.work.size + 256);
+  if (rc) return rc;
+  uint8_t *wb = (uint8_t *)S.work.p;
   // resolve tagged workspace offsets
   for (int i = 0; i < n; i++) {
     if (rd_of[i] < 0) continue;
@@ -1575,11 +1597,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     return rrc;
   }
   // ---- upload (pinned slot: the previous batch may still be running)
-  const int slot = c->next_slot;
-  rc = wait_slot(c, slot);
-  if (rc) return rc;
-  Slot &S = c->slots[slot];
-  rc = ensure(c, &c->arena, B.b.size() + 256);
+  rc = ensure(c, &S.arena, B.b.size() + 256);
   if (rc) return rc;
   rc = ensure_pinned_buf(&S.blob, &S.blob_cap, B.b.size() + 256);
   if (rc) return rc;
@@ -1588,7 +1606,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   rc = ensure_pinned_buf(&S.res, &S.res_cap, res_bytes + outwh_bytes + 64);
   if (rc) return rc;
   memcpy(S.blob, B.b.data(), B.b.size());
-  HIP_TRY(hipMemcpyAsync(c->arena.p, S.blob, B.b.size(), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(S.arena.p, S.blob, B.b.size(), hipMemcpyHostToDevice, c->stream));
   const double t_planned = now_ms();
   host_stat(c, "host_plan", t_planned - t_start);
   host_stat(c, "host_plan_images", t_images - t_start);
@@ -1597,7 +1615,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   host_stat(c, "host_plan_vmtiles", t_tiles - t_tiles0);
   host_stat(c, "host_plan_blob", t_planned - t_tiles);
   if (c->timing) c->stats["host_plan"].bytes += (double)B.b.size();
-  uint8_t *ab = (uint8_t *)c->arena.p;
+  uint8_t *ab = (uint8_t *)S.arena.p;
   rc = heap_commit(c, E, ab, ai_off, af_off, ad_off);
   if (rc) return rc;
   const int32_t *ai = (const int32_t *)c->heap_i.p;
@@ -1608,7 +1626,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   auto pre_p = [&](const Launch &L) { return (const int32_t *)(ab + L.prefix_off); };
   // ---- resample kernels
   {
-    Timer tb(c, "batch", 0);
+    Timer tb(c, "batch", 0, c->stream, c->sc_stream);
     {
       Timer t(c, "resize", resize_bytes);
       if (L0.tiles)
@@ -1652,12 +1670,18 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       (void)launch_mono(c->stream, (const MonoDesc *)(ab + mono_off), (int)mono.size(), ad + mono_wts);
     }
     HIP_TRY(hipGetLastError());
+    // the smartcrop stage, crop apply and readback go on sc_stream behind this
+    // batch's resample, so they overlap the next batch's upload and resample
+    if (!S.rs_done) HIP_TRY(hipEventCreateWithFlags(&S.rs_done, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(S.rs_done, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->sc_stream, S.rs_done, 0));
     if (any_sc) {
-      rc = enqueue_sc(c, ab, SX, ai, ad, (CropScore *)(wb + scores_off), (ScResult *)(wb + results_off), PD);
+      rc = enqueue_sc(c, c->sc_stream, ab, SX, ai, ad, (CropScore *)(wb + scores_off),
+                      (ScResult *)(wb + results_off), PD);
       if (rc) return rc;
       if (!apply.empty()) {
-        Timer t(c, "crop_apply", 0);
-        (void)launch_crop_apply(c->stream, (const ApplyDesc *)(ab + apply_off), (int)apply.size(),
+        Timer t(c, "crop_apply", 0, c->sc_stream, c->sc_stream);
+        (void)launch_crop_apply(c->sc_stream, (const ApplyDesc *)(ab + apply_off), (int)apply.size(),
                                 (const DevCrop *)(ab + SX.crops_off), (const ScResult *)(wb + results_off));
       }
       HIP_TRY(hipGetLastError());
@@ -1666,11 +1690,11 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   // ---- results: per-image records into the slot's pinned readback
   uint8_t *rp = (uint8_t *)S.res;
   if (!sitems.empty())
-    HIP_TRY(hipMemcpyAsync(rp, wb + results_off, res_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(rp, wb + results_off, res_bytes, hipMemcpyDeviceToHost, c->sc_stream));
   if (!apply.empty())
-    HIP_TRY(hipMemcpyAsync(rp + res_bytes, wb + outwh_off, outwh_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(rp + res_bytes, wb + outwh_off, outwh_bytes, hipMemcpyDeviceToHost, c->sc_stream));
   if (!S.done) HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(S.done, c->stream));
+  HIP_TRY(hipEventRecord(S.done, c->sc_stream));
   S.busy = true;
   c->next_slot = (slot + 1) % kSlots;
   PendingBatch pb;
@@ -1822,7 +1846,7 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   uint8_t *ab = (uint8_t *)c->arena.p;
   rc = heap_commit(c, E, ab, ai_off, ai_off, ad_off);
   if (rc) return rc;
-  rc = enqueue_sc(c, ab, SX, (const int32_t *)c->heap_i.p, (const double *)c->heap_d.p,
+  rc = enqueue_sc(c, c->stream, ab, SX, (const int32_t *)c->heap_i.p, (const double *)c->heap_d.p,
                   (CropScore *)(wb + scores_off), (ScResult *)(wb + results_off), to_dev(params));
   if (rc) return rc;
   scores->resize(SL.nscores);
@@ -1950,10 +1974,19 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_MFMA")) c->sc_mfma = !(e[0] == '1');
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  // FI_SC_STREAM=1: the smartcrop stage of batch k on its own stream, beside
+  // batch k+1's resample.  Off by default: k_rs_vm fills every CU (LDS), so
+  // the overlap only stretches both (cfg2: step 3.79 vs 3.81 ms, sc_score
+  // 0.39 -> 2.06 ms, resize 2.47 -> 2.83 ms).
+  bool sc_stream = false;
+  if (const char *e = getenv("FI_SC_STREAM")) sc_stream = e[0] == '1';
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      (sc_stream && hipStreamCreateWithFlags(&c->sc_stream, hipStreamNonBlocking) != hipSuccess)) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return set_err(FI_EDEVICE, "hipStreamCreate failed");
   }
+  if (!sc_stream) c->sc_stream = c->stream;
   *out = c;
   return FI_OK;
 }
@@ -1962,7 +1995,7 @@ void fi_destroy(fi_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)drain(c);
-  (void)hipStreamSynchronize(c->stream);
+  sync_streams(c);
   if (c->comm) ncclCommDestroy(c->comm);
   for (DevBuf *b : {&c->arena, &c->work, &c->io})
     if (b->p) (void)hipFree(b->p);
@@ -1971,9 +2004,13 @@ void fi_destroy(fi_ctx *c) {
     if (sl.blob) (void)hipHostFree(sl.blob);
     if (sl.res) (void)hipHostFree(sl.res);
     if (sl.done) (void)hipEventDestroy(sl.done);
+    if (sl.rs_done) (void)hipEventDestroy(sl.rs_done);
+    for (DevBuf *b : {&sl.arena, &sl.work})
+      if (b->p) (void)hipFree(b->p);
   }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
+  if (c->sc_stream != c->stream) (void)hipStreamDestroy(c->sc_stream);
   delete c;
 }
 

@@ -160,7 +160,10 @@ int fi_process_batch_device(fi_ctx *ctx, fi_image *imgs, int32_t n);
 /* Asynchronous form of fi_process_batch_device for pipelined serving: plans,
  * uploads and launches the batch, then returns; `imgs` must stay valid until
  * fi_wait().  Batch k+1 is planned on the host while batch k runs on the GPU
- * (two pinned staging slots; a third submit waits for the oldest batch).
+ * (two pinned staging slots; a third submit waits for the oldest batch), and
+ * batch k's smart-crop stage runs on a second stream concurrently with batch
+ * k+1's resample -- so the dst buffers of two in-flight batches must not
+ * overlap (sources may be shared).
  * fi_wait(ctx, keep) finalizes submitted batches in order -- fills their
  * result fields -- until at most `keep` remain in flight (0 = drain all) and
  * returns the first error. */
