@@ -212,10 +212,49 @@ class ImageProcessor:
         return op
 
 
+class ExtractProcessor:
+    """ExtractProcessor.php:21-40: ``convert <src> -crop WxH+X+Y <src>`` with
+    W = p2x - p1x, H = p2y - p1y, run before ImageProcessor
+    (ImageHandler.php:163-165), which then identifies the cropped file
+    (ImageMetaInfo::info() is lazy, ImageMetaInfo.php:125-134).
+
+    IM CropImage intersects the rectangle with the image.  No pixel work: the
+    extracted source is a view (pointer + stride + dims) of the decoded one,
+    which is what an fi_image source already is."""
+
+    @staticmethod
+    def rectangle(options: OptionsBag, src_w: int, src_h: int):
+        """(x, y, w, h) of the extracted region, clipped to the image."""
+        keys = ("extract-top-x", "extract-top-y", "extract-bottom-x", "extract-bottom-y")
+        vals = [options.extract_key(k) for k in keys]
+        try:
+            x0, y0, x1, y1 = (int(str(v)) for v in vals)
+        except ValueError:
+            # PHP 8: arithmetic on a non-numeric string is a TypeError
+            raise ExecFailedException(f"extract coordinates must be integers, got {vals}") from None
+        gw, gh = x1 - x0, y1 - y0
+        if gw <= 0 or gh <= 0 or x0 < 0 or y0 < 0:
+            raise ExecFailedException(f"-crop {gw}x{gh}+{x0}+{y0}: not a positive rectangle")
+        if x0 >= src_w or y0 >= src_h:
+            raise ExecFailedException(f"-crop {gw}x{gh}+{x0}+{y0}: geometry does not contain image")
+        return x0, y0, min(gw, src_w - x0), min(gh, src_h - y0)
+
+    @staticmethod
+    def extract(options: OptionsBag, image):
+        """The extracted view of a decoded HWC image, or the image itself when
+        ``e`` is not set."""
+        if _empty(options.extract_key("extract")):
+            return image
+        x, y, w, h = ExtractProcessor.rectangle(options, image.shape[1], image.shape[0])
+        return image[y:y + h, x:x + w]
+
+
 def process_new_image(ctx, options: str, image):
-    """ImageHandler::processNewImage for the GPU path: ImageProcessor ->
-    SmartCropProcessor on one decoded RGB8 image.  Returns (pixels, record)."""
+    """ImageHandler::processNewImage for the GPU path: ExtractProcessor ->
+    ImageProcessor -> SmartCropProcessor on one decoded RGB8 image.  Returns
+    (pixels, record)."""
     bag = OptionsBag(options)
+    image = ExtractProcessor.extract(bag, image)
     h, w = image.shape[:2]
     op = ImageProcessor(bag, w, h).to_op()
     outs, recs, rc = ctx.process([image], [op])

@@ -155,6 +155,21 @@ def test_smartcrop_fast_path_top_crop(sctx, case):
         assert abs(t.total - float.fromhex(g[7])) <= 1e-9 * max(1.0, abs(t.total))
 
 
+@pytest.mark.parametrize("case", SC["cases"], ids=[c["name"] for c in SC["cases"]])
+def test_smartcrop_fast_bounds_contain_exact(sctx, case):
+    """Bound-and-verify path: the fast f64 total of every crop lies within
+    1e-9 (relative) of smartcrop.py's sequential f64 total (its rigorous
+    bound is ~1e-11); re-scored crops carry it bit for bit."""
+    r = sctx.smartcrop_ex(G.case_input(case), 100, 100, options=_opts(False))
+    assert len(r["crops"]) == len(case["crops"])
+    for c, g in zip(r["crops"], case["crops"]):
+        exact = float.fromhex(g[7])
+        if c.exact:
+            assert c.total.hex() == g[7]
+        else:
+            assert abs(c.total - exact) <= 1e-9 * max(1.0, abs(exact)), (c.total, exact)
+
+
 def test_smartcrop_reference_fixture(sctx):
     ctx = sctx
     """SmartCropProcessorTest.php:16-24: smart_crop.jpg -> 674x674+0+0."""
@@ -398,3 +413,43 @@ def test_monochrome_pipeline_resized(rctx, W, H, opts):
     assert outs[0].shape == ref.shape
     assert set(np.unique(outs[0])) <= {0, 255}
     assert abs(outs[0].mean() - ref.mean()) / 255 < 0.01
+
+
+# ---------------------------------------------------------------------------
+# ExtractProcessor (e_1): the reference fixture pair (ExtractProcessorTest.php)
+def test_extract_reference_fixture(ctx):
+    """extract-original.jpg + e_1,p1x_100,p1y_100,p2x_300,p2y_300 through the
+    GPU path equals the 200x200 crop of the decoded source exactly, and the
+    reference's own result (IM + JPEG q90 re-encode) within JPEG noise --
+    closer than any crop shifted by one pixel."""
+    import os
+
+    from PIL import Image
+
+    from flyimg_amd.processor import process_new_image
+
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    src = np.asarray(Image.open(os.path.join(here, "extract-original.jpg")).convert("RGB"))
+    ref = np.asarray(Image.open(os.path.join(here, "extract-result.jpg")).convert("RGB")).astype(np.int32)
+    out, rec = process_new_image(ctx, "e_1,p1x_100,p1y_100,p2x_300,p2y_300,o_jpg,rf_1", src)
+    assert out.shape == (200, 200, 3) and rec.status == 0
+    assert np.array_equal(out, src[100:300, 100:300])
+    d = np.abs(out.astype(np.int32) - ref).mean()
+    assert d < 2.5, d
+    for dx, dy in ((1, 0), (-1, 0), (0, 1), (0, -1)):
+        sh = src[100 + dy:300 + dy, 100 + dx:300 + dx].astype(np.int32)
+        assert d < np.abs(sh - ref).mean()
+
+
+def test_extract_then_resize_matches_oracle(ctx):
+    """e_1 + w_120,h_90,c_1 on a synthetic image: the extracted view (not
+    16-byte aligned) through the GPU path within +-1 LSB of the oracle on the
+    same cropped pixels."""
+    from flyimg_amd.processor import process_new_image
+
+    src = synth_rgb(640, 480, 77)
+    out, rec = process_new_image(ctx, "e_1,p1x_33,p1y_21,p2x_533,p2y_421,w_120,h_90,c_1", src)
+    crop = np.ascontiguousarray(src[21:421, 33:533])
+    ref = orc.im_convert(crop, 120, 90, orc.FLAG_THUMBNAIL | orc.FLAG_FILL | orc.FLAG_EXTENT)
+    assert out.shape == ref.shape == (90, 120, 3)
+    assert np.abs(out.astype(np.int16) - ref.astype(np.int16)).max() <= 1
