@@ -57,6 +57,8 @@ int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const M
                 const int32_t *ai, size_t lds);
 // tiled horizontal-first pass 1 (fi_kernels.hip)
 constexpr int kHTileRows = 8;
+int launch_rs4(hipStream_t s, int mode, const ResizeDesc *d1, const int32_t *p1, int n1, int tiles1,
+               const ResizeDesc *d2, const int32_t *p2, int n2, int tiles2, const int32_t *ai, const double *ad);
 int launch_rs_h_tile(hipStream_t s, const ResizeDesc *descs, const int32_t *prefix, int n, int tiles,
                      const int32_t *ai, const float *af, int pitch);
 // -monochrome (fi_mono.hip)
@@ -201,6 +203,7 @@ struct fi_ctx {
     int32_t hmB = 0, hmC = 0, hmS0 = 0, vqA = 0, vqC = 0, vqK0 = 0;
   };
   std::map<const AxisTable *, DevAxis> axis_at;
+  std::map<const AxisTable *, int32_t> axis_wd_at;  // f64 weights (RGBA path) in heap_d
   std::map<const ScPlan *, ScTabs> sc_at;
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_at;
   std::map<const RingTable *, std::array<int32_t, 4>> ring_at;
@@ -398,6 +401,7 @@ static void heap_reset(fi_ctx *c) {
   sync_streams(c);
   c->heap_i.used = c->heap_f.used = c->heap_d.used = 0;
   c->axis_at.clear();
+  c->axis_wd_at.clear();
   c->sc_at.clear();
   c->imp_at.clear();
   c->ring_at.clear();
@@ -504,11 +508,24 @@ static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, 
   d.src_lo = t->src_lo;
   d.src_hi = t->src_hi;
   d.touched = t->touched;
+  d.wbase = wbase;
+  d.wd = -1;
   c->axis_at[t] = d;
   *out = d;
   return t;
 }
 
+
+// The f64 weights of an axis (RGBA path), placed in the double heap once.
+static void add_axis_f64(fi_ctx *c, Exec &E, const AxisTable *t, DevAxis *d) {
+  auto it = c->axis_wd_at.find(t);
+  if (it == c->axis_wd_at.end()) {
+    const int32_t off = E.od();
+    E.ad.insert(E.ad.end(), t->wd.begin(), t->wd.end());
+    it = c->axis_wd_at.emplace(t, off).first;
+  }
+  d->wd = it->second;
+}
 
 // Column strips of the fused kernel (fi_fused.hip): <= kFusedStripBytes
 // source bytes (256 streaming lanes x 8 B), <= 768 output columns, horizontal
@@ -965,7 +982,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     ResizeDesc d{};
     d.src = im.src;
     d.src_stride = im.src_stride;
-    d.C = 3;
+    d.C = P.C;
+    const bool rgb = P.C == 3;
     d.ew = P.ew;
     d.eh = P.eh;
     d.ex0 = P.ex0;
@@ -999,7 +1017,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     int64_t src_bytes = 0;
     if (!P.resize) {
       d.mode = 0;
-      src_bytes = (int64_t)P.ew * P.eh * 3;
+      src_bytes = (int64_t)P.ew * P.eh * P.C;
     } else {
       const AxisTable *vt =
           add_axis(c, E, P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &d.v, placed);
@@ -1009,7 +1027,12 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       const MfmaH *mh = nullptr;
       const VmV *vv = nullptr;
       const MfmaH *vh = nullptr;
-      if (!P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
+      if (!rgb) {
+        // matte (RGBA) images: the alpha-weighted f64 generic passes (k_rs4_*)
+        add_axis_f64(c, E, vt, &d.v);
+        add_axis_f64(c, E, ht, &d.h);
+      }
+      if (rgb && !P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0) {
         auto vit = c->vmv_cache.find(vt);
         if (vit == c->vmv_cache.end()) {
@@ -1042,7 +1065,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           vh = &hit->second;
         }
       }
-      if (!vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
+      if (rgb && !vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0) {
         auto vit = c->mv_cache.find(vt);
         if (vit == c->mv_cache.end()) {
@@ -1062,7 +1085,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         }
       }
       const RingTable *ring = nullptr;
-      if (!vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
+      if (rgb && !vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0 && d.h.maxtaps <= 64) {
         auto rit = c->ring_cache.find(vt);
         if (rit == c->ring_cache.end()) {
@@ -1123,6 +1146,18 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         fused_strips_of.push_back(strips);
         fused_img.push_back((int)rd.size());
         src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
+      } else if (!rgb && !P.hfirst) {
+        d.mode = 1;  // RGBA: mid = [eh][source columns src_lo..src_hi) x 4 Q16
+        d.mid_c0 = d.h.src_lo;
+        d.mid_cols = d.h.src_hi - d.h.src_lo;
+        d.mid_rows = P.eh;
+        d.mid_stride = 4 * (int64_t)d.mid_cols;
+      } else if (!rgb) {
+        d.mode = 2;  // RGBA: mid = [source rows src_lo..src_hi][ew] x 4 Q16
+        d.mid_r0 = d.v.src_lo;
+        d.mid_rows = d.v.src_hi - d.v.src_lo;
+        d.mid_cols = P.ew;
+        d.mid_stride = 4 * (int64_t)P.ew;
       } else if (!P.hfirst) {
         d.mode = 1;
         const int64_t b_lo = (int64_t)3 * d.h.src_lo / 8 * 8;
@@ -1146,7 +1181,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       }
       if (d.mode != 3 && d.mode != 4 && d.mode != 5) {
         d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
-        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
+        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * P.C;
       }
     }
     resize_bytes += (double)src_bytes + (double)need;
@@ -1233,10 +1268,13 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     if (sc_of[i] >= 0) SL.descs[sc_of[i]].img = out_of[i];
   const double t_sc = now_ms();
   // ---- build launches
-  std::vector<int> m0, m1, m2;
+  std::vector<int> m0, m1, m2, q0, q1, q2;  // q*: RGBA (matte) images of modes 0 / 1 / 2
   for (size_t k = 0; k < rd.size(); k++) {
     if (rd[k].mode >= 3) continue;
-    (rd[k].mode == 0 ? m0 : rd[k].mode == 1 ? m1 : m2).push_back((int)k);
+    if (rd[k].C == 4)
+      (rd[k].mode == 0 ? q0 : rd[k].mode == 1 ? q1 : q2).push_back((int)k);
+    else
+      (rd[k].mode == 0 ? m0 : rd[k].mode == 1 ? m1 : m2).push_back((int)k);
   }
   // fused tiles: (image, column strip, row band); grouped by ring size K
   struct FusedGroup {
@@ -1545,6 +1583,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     return ((d.mid_rows + kHTileRows - 1) / kHTileRows) * ((d.ew + 255) / 256);
   }) : add_launch(B, rd, m2, mid_tiles);
   Launch L2b = add_launch(B, rd, m2, eh_tiles);
+  Launch Q0 = add_launch(B, rd, q0, eh_tiles), Q1a = add_launch(B, rd, q1, eh_tiles),
+         Q2a = add_launch(B, rd, q2, mid_tiles), Q2b = add_launch(B, rd, q2, eh_tiles);
   ScLaunches SX;
   add_sc_launches(c, B, SL, sstatus, &SX);
   const bool any_sc = SX.nsl + SX.nsg > 0;
@@ -1647,6 +1687,13 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         if (launch_fused(c->stream, g.first, (const ResizeDesc *)(ab + all_rd_off), (const FusedTile *)(ab + G.off),
                          (int)G.tiles.size(), ai, af, pitch, G.max_taps, G.max_nbytes) != 0)
           return set_err(FI_EDEVICE, "fused resample launch rejected (K=%d, LDS budget)", g.first);
+      }
+      if (Q0.tiles || Q1a.tiles || Q2a.tiles) {
+        const ResizeDesc *dq0 = (const ResizeDesc *)desc_p(Q0), *dq1 = (const ResizeDesc *)desc_p(Q1a),
+                         *dq2a = (const ResizeDesc *)desc_p(Q2a), *dq2b = (const ResizeDesc *)desc_p(Q2b);
+        launch_rs4(c->stream, 0, dq0, pre_p(Q0), Q0.n, Q0.tiles, nullptr, nullptr, 0, 0, ai, ad);
+        launch_rs4(c->stream, 1, dq1, pre_p(Q1a), Q1a.n, Q1a.tiles, dq1, pre_p(Q1a), Q1a.n, Q1a.tiles, ai, ad);
+        launch_rs4(c->stream, 2, dq2a, pre_p(Q2a), Q2a.n, Q2a.tiles, dq2b, pre_p(Q2b), Q2b.n, Q2b.tiles, ai, ad);
       }
       if (L1a.tiles) {
         hipLaunchKernelGGL(k_rs_v_u8, dim3(L1a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L1a),
@@ -2078,7 +2125,8 @@ int fi_process_batch(fi_ctx *c, fi_image *imgs, int32_t n) {
     fi_image p = imgs[i];
     ImPlan pl;
     plan_im(p, &pl);
-    const int64_t sstride = ((int64_t)imgs[i].src_w * 3 + 15) / 16 * 16;
+    const int C = imgs[i].src_channels == 4 ? 4 : 3;
+    const int64_t sstride = ((int64_t)imgs[i].src_w * C + 15) / 16 * 16;
     soff[i] = total;
     total += (size_t)std::max<int64_t>(sstride * imgs[i].src_h, 0);
     total = (total + 255) / 256 * 256;
@@ -2091,12 +2139,14 @@ int fi_process_batch(fi_ctx *c, fi_image *imgs, int32_t n) {
   if (rc) return rc;
   uint8_t *io = (uint8_t *)c->io.p;
   for (int i = 0; i < n; i++) {
-    if (!imgs[i].src || imgs[i].src_w <= 0 || imgs[i].src_h <= 0 || imgs[i].src_channels != 3) {
+    const int C = imgs[i].src_channels;
+    if (!imgs[i].src || imgs[i].src_w <= 0 || imgs[i].src_h <= 0 || (C != 3 && C != 4) ||
+        imgs[i].src_stride < imgs[i].src_w * C) {
       dev[i].src = nullptr;
       continue;
     }
     HIP_TRY(hipMemcpy2DAsync(io + soff[i], dev[i].src_stride, imgs[i].src, imgs[i].src_stride,
-                             (size_t)imgs[i].src_w * 3, imgs[i].src_h, hipMemcpyHostToDevice, c->stream));
+                             (size_t)imgs[i].src_w * C, imgs[i].src_h, hipMemcpyHostToDevice, c->stream));
     dev[i].src = io + soff[i];
     dev[i].dst = imgs[i].dst ? io + doff[i] : nullptr;
   }

@@ -31,6 +31,9 @@ struct DevAxis {
   int32_t src_lo;   // min over start
   int32_t src_hi;   // max over start+count (exclusive)
   int32_t touched;  // source indices with a non-zero merged weight
+  int32_t wbase;    // af offset the woff entries are relative to
+  int32_t wd;       // ad offset of the f64 weights (RGBA path; -1 = not placed):
+                    // weight (o, j) = ad[wd + ai[woff + o] - wbase + j]
 };
 
 // Per-image descriptor of the resample path (generic two-pass kernels and
@@ -38,7 +41,7 @@ struct DevAxis {
 struct ResizeDesc {
   const uint8_t *src;
   int64_t src_stride;  // bytes
-  int32_t C;           // 3
+  int32_t C;           // 3, or 4 (RGBA: IM's matte path, fi_kernels.hip k_rs4_*)
   int32_t mode;        // 0 = copy/epilogue only, 1 = V then H, 2 = H then V
   DevAxis v;           // output rows  (extent window) <- source rows
   DevAxis h;           // output cols  (extent window) <- source cols

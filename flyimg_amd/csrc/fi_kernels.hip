@@ -300,6 +300,160 @@ __global__ __launch_bounds__(256) void k_rs_copy(const ResizeDesc *__restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// RGBA sources: ImageMagick's matte resample (IM 6 resize.c HorizontalFilter /
+// VerticalFilter, the image->matte branch), f64 as IM's MagickRealType, f64
+// tap weights (DevAxis::wd).  Q16 intermediate RGBA with the alpha channel
+// (IM keeps opacity = QuantumRange - alpha: converted at each pass).  Generic
+// two-pass structure as above, one workgroup per output / intermediate row.
+// ---------------------------------------------------------------------------
+struct Px4 {
+  uint32_t c[4];
+};
+// One output of a matte pass: tap j at p + j * step (Q16 RGBA, or 8-bit RGBA
+// scaled by 257 when U8).
+template <bool U8, class T>
+__device__ __forceinline__ Px4 matte_taps(const T *p, int64_t step, const double *w, int n) {
+  const double qs = 1.0 / 65535.0;  // QuantumScale
+  double r = 0.0, g = 0.0, b = 0.0, op = 0.0, gamma = 0.0;
+  for (int j = 0; j < n; j++) {
+    const T *q = p + (int64_t)j * step;
+    const double k = U8 ? 257.0 : 1.0;
+    const double A = k * (double)q[3];
+    const double alpha = w[j] * qs * A;
+    r += alpha * (k * (double)q[0]);
+    g += alpha * (k * (double)q[1]);
+    b += alpha * (k * (double)q[2]);
+    op += w[j] * (65535.0 - A);
+    gamma += alpha;
+  }
+  // PerceptibleReciprocal
+  const double sg = gamma < 0.0 ? -1.0 : 1.0;
+  gamma = (sg * gamma) >= 1.0e-12 ? 1.0 / gamma : sg / 1.0e-12;
+  Px4 o;
+  o.c[0] = clamp_q16d(gamma * r);
+  o.c[1] = clamp_q16d(gamma * g);
+  o.c[2] = clamp_q16d(gamma * b);
+  o.c[3] = 65535u - clamp_q16d(op);
+  return o;
+}
+__device__ __forceinline__ const double *axis_wd(const DevAxis &a, const int32_t *ai, const double *ad, int o) {
+  return ad + a.wd + (ai[a.woff + o] - a.wbase);
+}
+// Epilogue of a matte image: extent pixel (x, y) -> RGBA8 or gray + alpha, rotated.
+__device__ __forceinline__ void store_pixel4(const ResizeDesc &D, int x, int y, const Px4 &v) {
+  int dx = x, dy = y;
+  if (D.rot == 90) {
+    dx = D.eh - 1 - y;
+    dy = x;
+  } else if (D.rot == 180) {
+    dx = D.ew - 1 - x;
+    dy = D.eh - 1 - y;
+  } else if (D.rot == 270) {
+    dx = y;
+    dy = D.ew - 1 - x;
+  }
+  uint8_t *o = D.dst + (int64_t)dy * D.dst_stride;
+  if (D.gray) {
+    const double gv = 0.212656 * (double)v.c[0] + 0.715158 * (double)v.c[1] + 0.072186 * (double)v.c[2];
+    o[dx * 2 + 0] = q16_to_u8(clamp_q16d(gv));
+    o[dx * 2 + 1] = q16_to_u8(v.c[3]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; c++) o[dx * 4 + c] = q16_to_u8(v.c[c]);
+  }
+}
+// V-first pass 1: mid[y][e] (source column mid_c0 + e) over the rows of output row y
+__global__ __launch_bounds__(256) void k_rs4_v_mid(const ResizeDesc *__restrict__ descs,
+                                                   const int32_t *__restrict__ prefix, int nimg,
+                                                   const int32_t *__restrict__ ai, const double *__restrict__ ad) {
+  const int t = blockIdx.x;
+  const int i = find_image(prefix, nimg, t);
+  const ResizeDesc &D = descs[i];
+  const int y = t - prefix[i];
+  const int s = ai[D.v.start + y], n = ai[D.v.count + y];
+  const double *w = axis_wd(D.v, ai, ad, y);
+  uint16_t *out = D.mid + (int64_t)y * D.mid_stride;
+  for (int e = threadIdx.x; e < D.mid_cols; e += 256) {
+    const Px4 v = matte_taps<true>(D.src + (int64_t)s * D.src_stride + 4 * ((int64_t)D.mid_c0 + e), D.src_stride, w, n);
+#pragma unroll
+    for (int c = 0; c < 4; c++) out[4 * e + c] = (uint16_t)v.c[c];
+  }
+}
+// V-first pass 2: output row y from mid row y over the columns
+__global__ __launch_bounds__(256) void k_rs4_h_final(const ResizeDesc *__restrict__ descs,
+                                                     const int32_t *__restrict__ prefix, int nimg,
+                                                     const int32_t *__restrict__ ai, const double *__restrict__ ad) {
+  const int t = blockIdx.x;
+  const int i = find_image(prefix, nimg, t);
+  const ResizeDesc &D = descs[i];
+  const int y = t - prefix[i];
+  const uint16_t *row = D.mid + (int64_t)y * D.mid_stride;
+  for (int x = threadIdx.x; x < D.ew; x += 256) {
+    const int s = ai[D.h.start + x], n = ai[D.h.count + x];
+    store_pixel4(D, x, y, matte_taps<false>(row + 4 * ((int64_t)s - D.mid_c0), 4, axis_wd(D.h, ai, ad, x), n));
+  }
+}
+// H-first pass 1: mid row rr (source row mid_r0 + rr) over the columns
+__global__ __launch_bounds__(256) void k_rs4_h_mid(const ResizeDesc *__restrict__ descs,
+                                                   const int32_t *__restrict__ prefix, int nimg,
+                                                   const int32_t *__restrict__ ai, const double *__restrict__ ad) {
+  const int t = blockIdx.x;
+  const int i = find_image(prefix, nimg, t);
+  const ResizeDesc &D = descs[i];
+  const int rr = t - prefix[i];
+  const uint8_t *row = D.src + (int64_t)(D.mid_r0 + rr) * D.src_stride;
+  uint16_t *out = D.mid + (int64_t)rr * D.mid_stride;
+  for (int x = threadIdx.x; x < D.ew; x += 256) {
+    const int s = ai[D.h.start + x], n = ai[D.h.count + x];
+    const Px4 v = matte_taps<true>(row + 4 * (int64_t)s, 4, axis_wd(D.h, ai, ad, x), n);
+#pragma unroll
+    for (int c = 0; c < 4; c++) out[4 * x + c] = (uint16_t)v.c[c];
+  }
+}
+// H-first pass 2: output row y over the mid rows
+__global__ __launch_bounds__(256) void k_rs4_v_final(const ResizeDesc *__restrict__ descs,
+                                                     const int32_t *__restrict__ prefix, int nimg,
+                                                     const int32_t *__restrict__ ai, const double *__restrict__ ad) {
+  const int t = blockIdx.x;
+  const int i = find_image(prefix, nimg, t);
+  const ResizeDesc &D = descs[i];
+  const int y = t - prefix[i];
+  const int s = ai[D.v.start + y], n = ai[D.v.count + y];
+  const double *w = axis_wd(D.v, ai, ad, y);
+  const uint16_t *col0 = D.mid + (int64_t)(s - D.mid_r0) * D.mid_stride;
+  for (int x = threadIdx.x; x < D.ew; x += 256)
+    store_pixel4(D, x, y, matte_taps<false>(col0 + 4 * x, D.mid_stride, w, n));
+}
+// No resample (ResizeImage clone): extent crop + gray + rotate of a matte image
+__global__ __launch_bounds__(256) void k_rs4_copy(const ResizeDesc *__restrict__ descs,
+                                                  const int32_t *__restrict__ prefix, int nimg) {
+  const int t = blockIdx.x;
+  const int i = find_image(prefix, nimg, t);
+  const ResizeDesc &D = descs[i];
+  const int y = t - prefix[i];
+  const uint8_t *row = D.src + (int64_t)(D.ey0 + y) * D.src_stride + 4 * (int64_t)D.ex0;
+  for (int x = threadIdx.x; x < D.ew; x += 256) {
+    Px4 v;
+#pragma unroll
+    for (int c = 0; c < 4; c++) v.c[c] = 257u * row[4 * x + c];
+    store_pixel4(D, x, y, v);
+  }
+}
+int launch_rs4(hipStream_t s, int mode, const ResizeDesc *d1, const int32_t *p1, int n1, int tiles1,
+               const ResizeDesc *d2, const int32_t *p2, int n2, int tiles2, const int32_t *ai, const double *ad) {
+  if (mode == 0) {
+    if (tiles1 > 0) hipLaunchKernelGGL(k_rs4_copy, dim3(tiles1), dim3(256), 0, s, d1, p1, n1);
+  } else if (mode == 1) {
+    if (tiles1 > 0) hipLaunchKernelGGL(k_rs4_v_mid, dim3(tiles1), dim3(256), 0, s, d1, p1, n1, ai, ad);
+    if (tiles2 > 0) hipLaunchKernelGGL(k_rs4_h_final, dim3(tiles2), dim3(256), 0, s, d2, p2, n2, ai, ad);
+  } else {
+    if (tiles1 > 0) hipLaunchKernelGGL(k_rs4_h_mid, dim3(tiles1), dim3(256), 0, s, d1, p1, n1, ai, ad);
+    if (tiles2 > 0) hipLaunchKernelGGL(k_rs4_v_final, dim3(tiles2), dim3(256), 0, s, d2, p2, n2, ai, ad);
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // smartcrop prescale: Pillow reduce + LANCZOS resample (exact integer math)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void load_rgb(const uint8_t *img, int64_t stride, int C, int x, int y,

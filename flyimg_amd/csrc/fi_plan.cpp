@@ -88,8 +88,12 @@ int plan_im(const fi_image &img, ImPlan *p) {
     return code;
   };
   if (img.src_w <= 0 || img.src_h <= 0) return fail(FI_EINVAL, "source dimensions must be positive");
-  if (img.src_channels != 3) return fail(FI_EUNSUPPORTED, "only RGB8 sources (src_channels=3) are supported");
-  if ((int64_t)img.src_stride < (int64_t)img.src_w * 3) return fail(FI_EINVAL, "src_stride < 3*src_w");
+  // RGB8, or RGBA8 (straight alpha, a PNG with an alpha channel: IM's matte
+  // image -- Mitchell filter, alpha-weighted resample)
+  if (img.src_channels != 3 && img.src_channels != 4)
+    return fail(FI_EUNSUPPORTED, "only RGB8 / RGBA8 sources (src_channels 3 or 4) are supported");
+  if ((int64_t)img.src_stride < (int64_t)img.src_w * img.src_channels) return fail(FI_EINVAL, "src_stride < C*src_w");
+  const bool matte = img.src_channels == 4;
   const uint32_t f = img.flags;
   if ((f & FI_OP_THUMBNAIL) && (f & FI_OP_RESIZE)) return fail(FI_EINVAL, "both -thumbnail and -resize");
   const bool has_geom = img.target_w > 0 || img.target_h > 0;
@@ -115,7 +119,9 @@ int plan_im(const fi_image &img, ImPlan *p) {
   if (p->resize) {
     p->xf = (double)p->tw / (double)p->sw;
     p->yf = (double)p->th / (double)p->sh;
-    p->filter = ((p->xf * p->yf) > 1.0) ? kFilterMitchell : kFilterLanczos;
+    // ResizeImage with the default filter: Mitchell for matte (alpha) images
+    // and enlargements, Lanczos otherwise
+    p->filter = (matte || (p->xf * p->yf) > 1.0) ? kFilterMitchell : kFilterLanczos;
     p->hfirst = p->xf > p->yf;
   }
   p->ex0 = p->ey0 = 0;
@@ -141,7 +147,10 @@ int plan_im(const fi_image &img, ImPlan *p) {
     if (img.rotate % 90) return fail(FI_EUNSUPPORTED, "only -rotate by multiples of 90 (IntegralRotateImage)");
     p->rot = ((img.rotate % 360) + 360) % 360;
   }
-  p->out_c = p->gray ? 1 : 3;
+  if (matte && p->mono) return fail(FI_EUNSUPPORTED, "-monochrome of an RGBA source is not on the GPU path");
+  if (matte && (f & FI_OP_SMARTCROP))
+    return fail(FI_EUNSUPPORTED, "smartcrop of an RGBA image: smartcrop.py fails on RGBA (split(), smartcrop.py:17)");
+  p->out_c = matte ? (p->gray ? 2 : 4) : (p->gray ? 1 : 3);
   const bool swap = p->rot == 90 || p->rot == 270;
   p->out_w = swap ? p->eh : p->ew;
   p->out_h = swap ? p->ew : p->eh;
@@ -240,7 +249,10 @@ void build_axis(int filter, double factor, int in_sampled, int out_size, int o0,
     t->start.push_back((int32_t)m0);
     t->count.push_back(cnt);
     t->woff.push_back((int32_t)t->w.size());
-    for (int i = 0; i < cnt; i++) t->w.push_back((float)merged[i]);
+    for (int i = 0; i < cnt; i++) {
+      t->w.push_back((float)merged[i]);
+      t->wd.push_back(merged[i]);
+    }
     t->maxtaps = std::max(t->maxtaps, cnt);
     t->src_lo = std::min<int32_t>(t->src_lo, (int32_t)m0);
     t->src_hi = std::max<int32_t>(t->src_hi, (int32_t)(m0 + cnt));

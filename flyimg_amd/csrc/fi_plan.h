@@ -38,6 +38,7 @@ int plan_im(const fi_image &img, ImPlan *p);
 struct AxisTable {
   std::vector<int32_t> start, count, woff;
   std::vector<float> w;
+  std::vector<double> wd;  // the same weights in f64 (the RGBA path accumulates in f64 as IM does)
   int32_t maxtaps = 0, src_lo = 0, src_hi = 0, touched = 0;
 };
 // Ring table of the fused vertical-first kernel (fi_fused.hip): the list of

@@ -77,10 +77,12 @@ extern "C" {
  * "filled by library" fields.  For fi_process_batch the pointers are host
  * pointers; for fi_process_batch_device they are device pointers. */
 typedef struct fi_image {
-  const uint8_t *src;      /* HWC RGB8 (src_channels 3)                       */
+  const uint8_t *src;      /* HWC RGB8, or RGBA8 (straight alpha)             */
   int32_t src_w, src_h;    /* pixels                                          */
   int32_t src_stride;      /* bytes per row                                   */
-  int32_t src_channels;    /* 3                                               */
+  int32_t src_channels;    /* 3, or 4: an IM matte image (PNG with alpha) --   *
+                            * Mitchell, alpha-weighted passes (resize.c), out *
+                            * RGBA8 or gray+alpha (2); no smartcrop / mono    */
   int32_t target_w;        /* geometry W (0 = absent, getDimensions :240-259) */
   int32_t target_h;        /* geometry H (0 = absent)                         */
   uint32_t flags;          /* FI_OP_* | FI_GEOM_*                             */

@@ -85,6 +85,7 @@ def lib():
         L.or_im_meta_geometry.argtypes = [i, i, i, i, i, i, P(i), P(i)]
         L.or_im_resize_u8_to_q16.argtypes = [u8p, i, i, i, i, i, i, i, i, P(ctypes.c_uint16)]
         L.or_im_convert.argtypes = [u8p, i, i, i, i, i, ctypes.c_uint, i, i, u8p, i, P(i), P(i), P(i)]
+        L.or_im_convert_c.argtypes = [u8p, i, i, i, i, i, i, ctypes.c_uint, i, i, u8p, i, P(i), P(i), P(i)]
         L.or_im_gravity_offset.argtypes = [i, i, i, i, i, P(i), P(i)]
         L.or_im_gravity_offset.restype = None
         L.or_im_sample_index.argtypes = [ctypes.c_long] * 3
@@ -188,17 +189,20 @@ def mono_quant_info(hist: np.ndarray):
 
 
 def im_convert(src: np.ndarray, rw=0, rh=0, flags=FLAG_THUMBNAIL, gravity=5, rotate=0) -> np.ndarray:
-    """convert <src> <resize op> [-gravity g -extent WxH] [-colorspace Gray] [-monochrome] [-rotate r]."""
+    """convert <src> <resize op> [-gravity g -extent WxH] [-colorspace Gray] [-monochrome] [-rotate r].
+    RGBA sources (H x W x 4) take IM's matte path: Mitchell, alpha-weighted passes,
+    RGBA out (gray + alpha after -colorspace Gray)."""
     src = np.ascontiguousarray(src, dtype=np.uint8)
     H, W = src.shape[:2]
+    C = src.shape[2] if src.ndim == 3 else 1  # 3 = RGB, 4 = RGBA (IM matte image)
     tw, th = W, H
     if rw or rh:
         tw, th = im_meta_geometry(W, H, rw, rh, bool(flags & FLAG_FILL), bool(flags & FLAG_SHRINK))
-    cap = 3 * (max(tw, rw or 0) * max(th, rh or 0) + 16)  # output bound (an int32 on the C side)
+    cap = 4 * (max(tw, rw or 0) * max(th, rh or 0) + 16)  # output bound (an int32 on the C side)
     out = np.zeros(cap, np.uint8)
     ow, oh, oc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    rc = lib().or_im_convert(_u8(src), W, H, W * 3, rw, rh, flags, gravity, rotate, _u8(out), cap,
-                             ctypes.byref(ow), ctypes.byref(oh), ctypes.byref(oc))
+    rc = lib().or_im_convert_c(_u8(src), W, H, C, W * C, rw, rh, flags, gravity, rotate, _u8(out), cap,
+                               ctypes.byref(ow), ctypes.byref(oh), ctypes.byref(oc))
     if rc:
         raise ValueError(f"or_im_convert rc={rc}")
     o = out[: ow.value * oh.value * oc.value].reshape(oh.value, ow.value, oc.value)

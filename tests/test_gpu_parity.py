@@ -453,3 +453,78 @@ def test_extract_then_resize_matches_oracle(ctx):
     ref = orc.im_convert(crop, 120, 90, orc.FLAG_THUMBNAIL | orc.FLAG_FILL | orc.FLAG_EXTENT)
     assert out.shape == ref.shape == (90, 120, 3)
     assert np.abs(out.astype(np.int16) - ref.astype(np.int16)).max() <= 1
+
+
+# ---------------------------------------------------------------------------
+# RGBA (IM matte) sources: Mitchell, alpha-weighted passes (resize.c matte
+# branch), RGBA or gray+alpha out -- k_rs4_* vs the oracle's im_matte_pixel
+def _rgba(W, H, seed):
+    rng = np.random.default_rng(seed)
+    a = np.empty((H, W, 4), np.uint8)
+    a[..., :3] = synth_rgb(W, H, seed)
+    yy, xx = np.mgrid[0:H, 0:W]
+    alpha = np.clip(255.0 * (0.5 + 0.7 * np.sin(xx / 37.0) * np.cos(yy / 23.0)), 0, 255)
+    alpha[: H // 5] = 0                     # fully transparent band
+    alpha[-H // 6:] = 255                   # opaque band
+    alpha[H // 3: H // 3 + 7] = rng.integers(0, 256, (7, W))  # ragged alpha
+    a[..., 3] = alpha.astype(np.uint8)
+    return a
+
+
+RGBA_CASES = [
+    # (W, H, rw, rh, flags, rotate)
+    (1600, 1200, 200, 0, orc.FLAG_THUMBNAIL | orc.FLAG_SHRINK, 0),                          # sample pre-step, V first
+    (900, 300, 120, 0, orc.FLAG_THUMBNAIL | orc.FLAG_SHRINK, 0),                            # H first
+    (640, 480, 150, 150, orc.FLAG_THUMBNAIL | orc.FLAG_FILL | orc.FLAG_EXTENT, 0),          # extent
+    (640, 480, 160, 0, orc.FLAG_THUMBNAIL | orc.FLAG_GRAY | orc.FLAG_ROTATE, 90),           # gray + alpha, rot
+    (300, 200, 300, 0, orc.FLAG_THUMBNAIL | orc.FLAG_SHRINK, 0),                            # 1:1 clone
+    (120, 90, 300, 0, 0, 0),                                                                # -resize enlarge
+]
+
+
+@pytest.mark.parametrize("case", RGBA_CASES, ids=[f"{c[0]}x{c[1]}-{c[2]}x{c[3]}-f{c[4]}" for c in RGBA_CASES])
+def test_rgba_resize_within_one_lsb_of_oracle(ctx, case):
+    W, H, rw, rh, flags, rot = case
+    src = _rgba(W, H, W + H)
+    ref = orc.im_convert(src, rw, rh, flags, 5, rot)
+    F = L
+    f = (F.FI_OP_THUMBNAIL if flags & orc.FLAG_THUMBNAIL else F.FI_OP_RESIZE)
+    f |= F.FI_GEOM_FILL if flags & orc.FLAG_FILL else 0
+    f |= F.FI_GEOM_SHRINK_ONLY if flags & orc.FLAG_SHRINK else 0
+    f |= F.FI_OP_EXTENT if flags & orc.FLAG_EXTENT else 0
+    f |= F.FI_OP_GRAY if flags & orc.FLAG_GRAY else 0
+    f |= F.FI_OP_ROTATE if flags & orc.FLAG_ROTATE else 0
+    outs, recs, rc = ctx.process([src], [Op(rw, rh, f, L.GRAVITY["Center"], rot)])
+    L.check(rc)
+    out = outs[0]
+    assert out.shape == ref.shape and out.shape[-1] == (2 if flags & orc.FLAG_GRAY else 4)
+    d = np.abs(out.astype(np.int16) - ref.astype(np.int16))
+    assert d.max() <= 1, d.max()
+    assert (d == 0).mean() >= 0.98
+
+
+def test_rgba_reference_fixture(ctx):
+    """The reference's square-opaque-200.png (an RGBA PNG: IM reads it as a
+    matte image) -> w_100: within +-1 LSB of the oracle, alpha stays opaque."""
+    import os
+
+    from PIL import Image
+
+    from flyimg_amd.processor import process_new_image
+
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    im = Image.open(os.path.join(here, "square-opaque-200.png"))
+    assert im.mode == "RGBA"
+    src = np.ascontiguousarray(np.asarray(im))
+    out, rec = process_new_image(ctx, "w_100", src)
+    ref = orc.im_convert(src, 100, 0, orc.FLAG_THUMBNAIL | orc.FLAG_SHRINK)
+    assert out.shape == ref.shape == (100, 100, 4)
+    assert np.abs(out.astype(np.int16) - ref.astype(np.int16)).max() <= 1
+    assert (out[..., 3] == 255).all()
+
+
+def test_rgba_rejects_smartcrop_and_monochrome(ctx):
+    src = _rgba(320, 240, 5)
+    for f in (L.FI_OP_THUMBNAIL | L.FI_OP_SMARTCROP, L.FI_OP_THUMBNAIL | L.FI_OP_MONOCHROME):
+        outs, recs, rc = ctx.process([src], [Op(100, 0, f, L.GRAVITY["Center"], 0, 100, 100)])
+        assert recs[0].status == L.FI_EUNSUPPORTED
