@@ -143,7 +143,7 @@ def main():
     W, H, nimg, options, cfg_text = WORKLOADS[args.workload]
     if args.images:
         nimg = args.images
-    ctx = Context(local_rank)
+    ctx = Context(int(os.environ.get("FI_BENCH_DEVICE", local_rank)))  # override: rehearsal of N ranks on one GPU
     gather = RecordGather(comm, ctx)
 
     # ---- device-resident synthetic pool (distinct seed per global image) ----
@@ -234,7 +234,7 @@ def main():
                 "workload": f"{args.workload}: {cfg_text}",
                 "images_per_gpu": nimg, "src": f"{W}x{H} RGB8", "options": options,
                 "out": f"{ow}x{oh}x{oc} before smart-crop apply",
-                "parallelism": f"dp{world} (images sharded per GPU, RCCL gather of 32-B result records)"
+                "parallelism": f"dp{world} (images sharded per GPU, {gather.backend} gather of 32-B result records)"
                                if world > 1 else "dp1",
                 "record_gather": gather.backend,
                 "arithmetic": "resample fp32 on u8 (Q16 intermediate as ImageMagick); smartcrop prescale int32 "
@@ -298,7 +298,7 @@ def run_cfg4(args, rank, world, local_rank, comm):
     n_total = args.images or 65536
     items = cfg4_list(n_total)
     shard = shard_lpt([float(W) * H for W, H, _ in items], world)[rank]
-    ctx = Context(local_rank)
+    ctx = Context(int(os.environ.get("FI_BENCH_DEVICE", local_rank)))  # override: rehearsal of N ranks on one GPU
     gather = RecordGather(comm, ctx)
     sizes = sorted({(W, H) for W, H, _ in items})
     stride_of = {wh: (wh[0] * 3 + 15) // 16 * 16 for wh in sizes}

@@ -87,9 +87,16 @@ class FileComm:
         return self._get(tag, 0)
 
     def close(self):
+        # the other ranks may still be reading rank 0's barrier file: each
+        # acknowledges after its barrier, and rank 0 removes the directory
+        # only once every acknowledgement is in
         self.barrier()
-        if self.rank == 0:
-            shutil.rmtree(self.dir, ignore_errors=True)
+        if self.rank != 0:
+            self._put("bye", self.rank, b"1")
+            return
+        for r in range(1, self.world):
+            self._get("bye", r)
+        shutil.rmtree(self.dir, ignore_errors=True)
 
 
 def make_comm():
@@ -131,17 +138,22 @@ class RecordGather:
         if comm.world == 1:
             self.backend = "local"
             return
-        if ctx is not None:
+        if ctx is not None and os.environ.get("FI_RECORD_GATHER", "rccl") == "rccl":
             import ctypes
 
             from . import _lib as L
 
             uid = ctypes.create_string_buffer(128)
+            ok = 1
             if comm.rank == 0:
-                L.check(L.lib().fi_rccl_get_unique_id(uid))
-            data = comm.bcast_bytes(uid.raw if comm.rank == 0 else None)
-            L.check(L.lib().fi_rccl_init(ctx.h, comm.rank, comm.world, data))
-            self.backend = "rccl"
+                ok = int(L.lib().fi_rccl_get_unique_id(uid) == 0)
+            data = comm.bcast_bytes((uid.raw if ok else b"") if comm.rank == 0 else None)
+            if len(data) == 128:
+                ok = int(L.lib().fi_rccl_init(ctx.h, comm.rank, comm.world, data) == 0)
+            else:
+                ok = 0
+            # every rank takes the same backend: RCCL only if it came up everywhere
+            self.backend = "rccl" if all(comm.allgather_obj(ok)) else "comm"
         else:
             self.backend = "comm"
 

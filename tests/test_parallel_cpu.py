@@ -157,3 +157,23 @@ def test_file_comm_timeout_is_loud():
         with pytest.raises(TimeoutError):
             c.allgather_obj(1)
         assert time.time() - t0 < 5
+
+
+def _close_rank(rank, world, root, q):
+    try:
+        for it in range(25):
+            comm = FileComm(rank, world, run_id=f"close{it}", root=root, timeout=10)
+            comm.barrier()
+            comm.close()  # rank 0 must not remove the directory under a reader
+        q.put((rank, None, None, None, None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, None, None, repr(e)))
+
+
+def test_file_comm_close_waits_for_every_rank(tmp_path):
+    """Regression: rank 0 used to delete the rendezvous directory right after
+    its closing barrier, while another rank could still be polling for rank
+    0's barrier file -- that rank then hung until its timeout."""
+    out = _run(_close_rank, 4, str(tmp_path))
+    for r in range(4):
+        assert out[r][4] is None, out[r][4]
