@@ -56,11 +56,12 @@ size_t mfma_lds_bytes(int nblocks);
 int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const MTile *tiles, int ntiles,
                 const int32_t *ai, size_t lds);
 // tiled horizontal-first pass 1 (fi_kernels.hip)
-constexpr int kHTileRows = 8;
+constexpr int kHTileRows = 16;  // fi_kernels.hip kHTRows
+size_t rs_h_tile_lds(int pitch, int taps);
 int launch_rs4(hipStream_t s, int mode, const ResizeDesc *d1, const int32_t *p1, int n1, int tiles1,
                const ResizeDesc *d2, const int32_t *p2, int n2, int tiles2, const int32_t *ai, const double *ad);
 int launch_rs_h_tile(hipStream_t s, const ResizeDesc *descs, const int32_t *prefix, int n, int tiles,
-                     const int32_t *ai, const float *af, int pitch);
+                     const int32_t *ai, const float *af, int pitch, int taps);
 // -monochrome (fi_mono.hip)
 size_t mono_lds_bytes();
 int launch_mono(hipStream_t s, const MonoDesc *descs, int n, const double *wts);
@@ -940,6 +941,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   std::vector<const MfmaH *> mfma_h;
   std::vector<int> vm_img;     // indices into rd (mode 5)
   int h_tile_pitch = 0;        // k_rs_h_tile: max staged row bytes over the mode-2 images
+  int h_tile_taps = 0;         // k_rs_h_tile: max horizontal window over the mode-2 images
   std::vector<const VmV *> vm_v;
   std::vector<const MfmaH *> vm_h;
   // per image resized-buffer workspace offsets (for smartcrop-apply)
@@ -1177,6 +1179,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           const int x1 = std::min(P.ew, x0 + 256);
           const int lo = ht->start[x0], hi = ht->start[x1 - 1] + ht->count[x1 - 1];
           h_tile_pitch = std::max(h_tile_pitch, (3 * (hi - lo) + 8 + 15) / 16 * 16);
+          h_tile_taps = std::max(h_tile_taps, (int)d.h.maxtaps);
         }
       }
       if (d.mode != 3 && d.mode != 4 && d.mode != 5) {
@@ -1578,7 +1581,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
   Launch L0 = add_launch(B, rd, m0, eh_tiles);
   Launch L1a = add_launch(B, rd, m1, eh_tiles);
-  const bool h_tiled = (size_t)kHTileRows * h_tile_pitch <= 64 * 1024;
+  const bool h_tiled = rs_h_tile_lds(h_tile_pitch, h_tile_taps) <= 64 * 1024;
   Launch L2a = h_tiled ? add_launch(B, rd, m2, [](const ResizeDesc &d) {
     return ((d.mid_rows + kHTileRows - 1) / kHTileRows) * ((d.ew + 255) / 256);
   }) : add_launch(B, rd, m2, mid_tiles);
@@ -1704,7 +1707,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       if (L2a.tiles) {
         if (h_tiled)
           launch_rs_h_tile(c->stream, (const ResizeDesc *)desc_p(L2a), pre_p(L2a), L2a.n, L2a.tiles, ai, af,
-                           h_tile_pitch);
+                           h_tile_pitch, h_tile_taps);
         else
           hipLaunchKernelGGL(k_rs_h_u8, dim3(L2a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L2a),
                              pre_p(L2a), L2a.n, ai, af);

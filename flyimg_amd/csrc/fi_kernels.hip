@@ -110,16 +110,32 @@ __global__ __launch_bounds__(256) void k_rs_v_u8(const ResizeDesc *__restrict__ 
 #pragma unroll
     for (int k = 0; k < 8; k++) acc[k] = 0.0f;
     const bool full = e + 8 <= nel;
-    for (int j = 0; j < n; j++) {
-      const uint8_t *p = D.src + (int64_t)(s + j) * D.src_stride + b_lo + e;
-      const float wj = w[j];
-      if (full && ((((uintptr_t)p) & 7) == 0)) {
-        const uint2 v = *reinterpret_cast<const uint2 *>(p);
+    const uint8_t *p0 = D.src + (int64_t)s * D.src_stride + b_lo + e;
+    if (full && ((((uintptr_t)p0 | (uintptr_t)D.src_stride) & 7) == 0)) {
+      for (int j0 = 0; j0 < n; j0 += 8) {
+        // 8 rows' loads in flight, then accumulated in tap order (same fp32 ops)
+        uint2 v[8];
+        float wq[8];
 #pragma unroll
-        for (int k = 0; k < 4; k++) acc[k] += wj * (float)((v.x >> (8 * k)) & 255u);
+        for (int u = 0; u < 8; u++) {
+          const int j = min(j0 + u, n - 1);
+          v[u] = *reinterpret_cast<const uint2 *>(p0 + (int64_t)j * D.src_stride);
+          wq[u] = w[j];
+        }
 #pragma unroll
-        for (int k = 0; k < 4; k++) acc[4 + k] += wj * (float)((v.y >> (8 * k)) & 255u);
-      } else {
+        for (int u = 0; u < 8; u++) {
+          if (j0 + u < n) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) acc[k] += wq[u] * (float)((v[u].x >> (8 * k)) & 255u);
+#pragma unroll
+            for (int k = 0; k < 4; k++) acc[4 + k] += wq[u] * (float)((v[u].y >> (8 * k)) & 255u);
+          }
+        }
+      }
+    } else {
+      for (int j = 0; j < n; j++) {
+        const uint8_t *p = p0 + (int64_t)j * D.src_stride;
+        const float wj = w[j];
         for (int k = 0; k < 8 && e + k < nel; k++) acc[k] += wj * (float)p[k];
       }
     }
@@ -142,11 +158,26 @@ __global__ __launch_bounds__(256) void k_rs_h_final(const ResizeDesc *__restrict
     const float *w = af + ai[D.h.woff + x];
     const uint16_t *p = row + (int64_t)3 * s - D.mid_c0;
     float r = 0.f, g = 0.f, b = 0.f;
-    for (int j = 0; j < n; j++) {
-      const float wj = w[j];
-      r += wj * (float)p[3 * j + 0];
-      g += wj * (float)p[3 * j + 1];
-      b += wj * (float)p[3 * j + 2];
+    for (int j0 = 0; j0 < n; j0 += 8) {
+      // 8 taps' loads in flight, then accumulated in tap order (same fp32 ops)
+      uint16_t q[8][3];
+      float wq[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int j = min(j0 + u, n - 1);
+        q[u][0] = p[3 * j + 0];
+        q[u][1] = p[3 * j + 1];
+        q[u][2] = p[3 * j + 2];
+        wq[u] = w[j];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (j0 + u < n) {
+          r += wq[u] * (float)q[u][0];
+          g += wq[u] * (float)q[u][1];
+          b += wq[u] * (float)q[u][2];
+        }
+      }
     }
     store_pixel(D, x, y, clamp_q16(r), clamp_q16(g), clamp_q16(b));
   }
@@ -180,18 +211,20 @@ __global__ __launch_bounds__(256) void k_rs_h_u8(const ResizeDesc *__restrict__ 
   }
 }
 
-// H-first, pass 1 (tiled): one workgroup = (image, 8 mid rows, 256 output
-// columns).  The source bytes the 256 columns' windows touch are staged in
-// LDS for the 8 rows with coalesced dword loads; each thread then reads every
-// weight once for 8 rows (the per-row kernel above re-fetched the weights and
-// gathered the source bytes from global memory row by row).  Same fp32
-// operation order per output as k_rs_h_u8, so the same Q16 values.
-constexpr int kHTRows = 8;
+// H-first, pass 1 (tiled): one workgroup = (image, kHTRows mid rows, 256
+// output columns).  The source bytes the 256 columns' windows touch are staged
+// in LDS for the rows with coalesced dword loads, and the columns' weights
+// transposed [tap][column] (zero padded to the axis' longest window, so the
+// tap loop is uniform; a zero weight adds +0.0 and changes nothing).  Each
+// thread then reads a tap's weight once for all rows and a pixel's three
+// bytes with one two-dword LDS read + v_alignbyte.  Same fp32 operation
+// order per output as k_rs_h_u8, so the same Q16 values.
+constexpr int kHTRows = 16;
 __global__ __launch_bounds__(256) void k_rs_h_tile(const ResizeDesc *__restrict__ descs,
                                                    const int32_t *__restrict__ prefix, int nimg,
                                                    const int32_t *__restrict__ ai, const float *__restrict__ af,
                                                    int pitch) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t hl[];  // [kHTRows][pitch]
+  extern __shared__ __attribute__((aligned(16))) uint8_t hl[];  // [kHTRows][pitch] bytes, then wT[taps][256]
   const int t = blockIdx.x;
   const int i = find_image(prefix, nimg, t);
   const ResizeDesc &D = descs[i];
@@ -202,6 +235,24 @@ __global__ __launch_bounds__(256) void k_rs_h_tile(const ResizeDesc *__restrict_
   const int s_lo = ai[D.h.start + x0];
   const int s_hi = ai[D.h.start + x1 - 1] + ai[D.h.count + x1 - 1];
   const int tid = threadIdx.x;
+  const int x = x0 + tid;
+  const bool valid = x < x1;
+  const int taps = D.h.maxtaps;
+  float *wT = reinterpret_cast<float *>(hl + kHTRows * pitch);
+  int s = s_lo, n = 0;
+  if (valid) {
+    s = ai[D.h.start + x];
+    n = ai[D.h.count + x];
+    const float *w = af + ai[D.h.woff + x];
+    for (int j0 = 0; j0 < taps; j0 += 8) {  // 8 weight loads in flight, then the LDS stores
+      float t8[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) t8[u] = j0 + u < n ? w[j0 + u] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (j0 + u < taps) wT[(j0 + u) * 256 + tid] = t8[u];
+    }
+  }
   int shr[kHTRows];
 #pragma unroll
   for (int r = 0; r < kHTRows; r++) {
@@ -210,56 +261,79 @@ __global__ __launch_bounds__(256) void k_rs_h_tile(const ResizeDesc *__restrict_
   }
   {
     // dwords wholly inside the window's bytes, then the tail bytes one by one
-    // (never a byte past the window: the source may end right after it)
+    // (never a byte past the window: the source may end right after it).
+    // Batches of 16 loads per thread are in flight before the first LDS
+    // store (a load-store pair per iteration put one HBM round trip per
+    // staged dword on the critical path).
     const int ndw = (3 * (s_hi - s_lo) + 3 + 3) >> 2;
-    for (int it = tid; it < nr * ndw; it += 256) {
-      const int r = it / ndw, k = it - r * ndw;
-      const uint8_t *row = D.src + (int64_t)(D.mid_r0 + r0 + r) * D.src_stride;
-      const uintptr_t a0 = ((uintptr_t)row + 3 * (uintptr_t)s_lo) & ~(uintptr_t)3;
-      const uintptr_t end = (uintptr_t)row + 3 * (uintptr_t)s_hi;
-      uint32_t v;
-      if (a0 + 4 * (uintptr_t)k + 4 <= end) {
-        v = reinterpret_cast<const uint32_t *>(a0)[k];
-      } else {
-        v = 0;
-        for (int b = 0; b < 4; b++) {
-          const uintptr_t a = a0 + 4 * (uintptr_t)k + b;
-          if (a >= (uintptr_t)row + 3 * (uintptr_t)s_lo && a < end) v |= (uint32_t)(*(const uint8_t *)a) << (8 * b);
+    const int total = nr * ndw;
+    constexpr int kB = 16;
+    for (int base = 0; base < total; base += 256 * kB) {
+      uint32_t v[kB];
+#pragma unroll
+      for (int u = 0; u < kB; u++) {
+        const int it = base + u * 256 + tid;
+        v[u] = 0;
+        if (it < total) {
+          const int r = it / ndw, k = it - r * ndw;
+          const uint8_t *row = D.src + (int64_t)(D.mid_r0 + r0 + r) * D.src_stride;
+          const uintptr_t a0 = ((uintptr_t)row + 3 * (uintptr_t)s_lo) & ~(uintptr_t)3;
+          const uintptr_t end = (uintptr_t)row + 3 * (uintptr_t)s_hi;
+          if (a0 + 4 * (uintptr_t)k + 4 <= end) {
+            v[u] = reinterpret_cast<const uint32_t *>(a0)[k];
+          } else {
+            for (int b = 0; b < 4; b++) {
+              const uintptr_t a = a0 + 4 * (uintptr_t)k + b;
+              if (a >= (uintptr_t)row + 3 * (uintptr_t)s_lo && a < end) v[u] |= (uint32_t)(*(const uint8_t *)a) << (8 * b);
+            }
+          }
         }
       }
-      reinterpret_cast<uint32_t *>(hl + r * pitch)[k] = v;
+#pragma unroll
+      for (int u = 0; u < kB; u++) {
+        const int it = base + u * 256 + tid;
+        if (it < total) {
+          const int r = it / ndw, k = it - r * ndw;
+          reinterpret_cast<uint32_t *>(hl + r * pitch)[k] = v[u];
+        }
+      }
     }
   }
   __syncthreads();
-  const int x = x0 + tid;
-  if (x >= x1) return;
-  const int s = ai[D.h.start + x], n = ai[D.h.count + x];
-  const float *w = af + ai[D.h.woff + x];
+  if (!valid) return;
   float acc[kHTRows][3];
 #pragma unroll
   for (int r = 0; r < kHTRows; r++) acc[r][0] = acc[r][1] = acc[r][2] = 0.f;
-  for (int j = 0; j < n; j++) {
-    const float wj = w[j];
-    const int o = 3 * (s + j - s_lo);
+  const int ob = 3 * (s - s_lo);
+  for (int j = 0; j < taps; j++) {
+    const float wj = wT[j * 256 + tid];
 #pragma unroll
     for (int r = 0; r < kHTRows; r++) {
-      const uint8_t *p = hl + r * pitch + shr[r] + o;
-      acc[r][0] += wj * (float)p[0];
-      acc[r][1] += wj * (float)p[1];
-      acc[r][2] += wj * (float)p[2];
+      const int o = r * pitch + shr[r] + ob + 3 * j;
+      // bytes o .. o + 2 of the staged row from the two dwords around them
+      const uint32_t *dw = reinterpret_cast<const uint32_t *>(hl + (o & ~3));
+      const uint32_t v = __builtin_amdgcn_alignbyte(dw[1], dw[0], (uint32_t)(o & 3));
+      acc[r][0] += wj * (float)(v & 255u);
+      acc[r][1] += wj * (float)((v >> 8) & 255u);
+      acc[r][2] += wj * (float)((v >> 16) & 255u);
     }
   }
-  for (int r = 0; r < nr; r++) {
-    uint16_t *out = D.mid + (int64_t)(r0 + r) * D.mid_stride;
-    out[3 * x + 0] = (uint16_t)clamp_q16(acc[r][0] * 257.0f);
-    out[3 * x + 1] = (uint16_t)clamp_q16(acc[r][1] * 257.0f);
-    out[3 * x + 2] = (uint16_t)clamp_q16(acc[r][2] * 257.0f);
+#pragma unroll
+  for (int r = 0; r < kHTRows; r++) {  // unrolled: acc stays in registers (a dynamic index spills it to scratch)
+    if (r < nr) {
+      uint16_t *out = D.mid + (int64_t)(r0 + r) * D.mid_stride;
+      out[3 * x + 0] = (uint16_t)clamp_q16(acc[r][0] * 257.0f);
+      out[3 * x + 1] = (uint16_t)clamp_q16(acc[r][1] * 257.0f);
+      out[3 * x + 2] = (uint16_t)clamp_q16(acc[r][2] * 257.0f);
+    }
   }
 }
+size_t rs_h_tile_lds(int pitch, int taps) { return (size_t)kHTRows * pitch + (size_t)taps * 256 * 4 + 16; }
 int launch_rs_h_tile(hipStream_t s, const ResizeDesc *descs, const int32_t *prefix, int n, int tiles,
-                     const int32_t *ai, const float *af, int pitch) {
+                     const int32_t *ai, const float *af, int pitch, int taps) {
   if (tiles <= 0) return 0;
-  hipLaunchKernelGGL(k_rs_h_tile, dim3(tiles), dim3(256), (size_t)kHTRows * pitch, s, descs, prefix, n, ai, af, pitch);
+  hipLaunchKernelGGL(k_rs_h_tile, dim3(tiles), dim3(256), rs_h_tile_lds(pitch, taps), s, descs, prefix, n, ai, af,
+                     pitch);
   return 0;
 }
 
