@@ -32,6 +32,9 @@ FI_OP_MONOCHROME = 1 << 6
 FI_OP_ROTATE = 1 << 7
 FI_OP_SMARTCROP = 1 << 8
 FI_OP_SMARTCROP_APPLY = 1 << 9
+FI_OP_UNSHARP = 1 << 10
+FI_OP_SHARPEN = 1 << 11
+FI_OP_BLUR = 1 << 12
 
 GRAVITY = {
     "NorthWest": 1, "North": 2, "NorthEast": 3, "West": 4, "Center": 5,
@@ -54,6 +57,7 @@ class FiImage(ctypes.Structure):
         ("crop_w", ctypes.c_int32), ("crop_h", ctypes.c_int32),
         ("crop_score", ctypes.c_double),
         ("status", ctypes.c_int32), ("n_candidates", ctypes.c_int32),
+        ("unsharp", ctypes.c_double * 4), ("sharpen", ctypes.c_double * 2), ("blur", ctypes.c_double * 2),
     ]
 
 
@@ -151,6 +155,7 @@ def lib():
     L.fi_rccl_init.argtypes = [vp, i32, i32, ctypes.c_char_p]
     L.fi_rccl_gather_records.argtypes = [vp, P(FiRecord), i32, P(FiRecord)]
     L.fi_debug_monochrome.argtypes = [vp, vp, i32, i32, i32, vp, i32]
+    L.fi_debug_convolve.argtypes = [vp, vp, i32, i32, i32, vp, ctypes.c_uint32, vp]
     _lib = L
     return L
 

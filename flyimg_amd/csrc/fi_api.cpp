@@ -58,6 +58,8 @@ int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const M
 // tiled horizontal-first pass 1 (fi_kernels.hip)
 constexpr int kHTileRows = 16;  // fi_kernels.hip kHTRows
 size_t rs_h_tile_lds(int pitch, int taps);
+int launch_conv(hipStream_t s, int mode, const ConvStep *steps, const int32_t *prefix, int n, int tiles,
+                const double *ad);
 int launch_rs4(hipStream_t s, int mode, const ResizeDesc *d1, const int32_t *p1, int n1, int tiles1,
                const ResizeDesc *d2, const int32_t *p2, int n2, int tiles2, const int32_t *ai, const double *ad);
 int launch_rs_h_tile(hipStream_t s, const ResizeDesc *descs, const int32_t *prefix, int n, int tiles,
@@ -954,6 +956,11 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     size_t g_off, st_off;
   };
   std::vector<MonoItem> mono;
+  struct ConvItem {
+    int img;
+    size_t a_off, b_off;
+  };
+  std::vector<ConvItem> conv_items;
   double resize_bytes = 0;
   for (int i = 0; i < n; i++) {
     fi_image &im = imgs[i];
@@ -986,6 +993,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     d.src_stride = im.src_stride;
     d.C = P.C;
     const bool rgb = P.C == 3;
+    const bool fast_ok = rgb && !P.conv;  // the streaming / fused kernels write 8-bit only
     d.ew = P.ew;
     d.eh = P.eh;
     d.ex0 = P.ex0;
@@ -1016,6 +1024,19 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       d.gray = 2;
       d.rot = 0;
     }
+    if (P.conv) {
+      // the epilogue writes the rotated Q16 image; the convolutions ping-pong
+      // between two such buffers and the last step writes the 8-bit output
+      ConvItem ci;
+      ci.img = i;
+      const size_t qb = (size_t)P.out_w * P.out_h * P.out_c * 2;
+      ci.a_off = E.work.take(qb);
+      ci.b_off = E.work.take(qb);
+      conv_items.push_back(ci);
+      d.dst = (uint8_t *)(uintptr_t)(ci.a_off + 1);
+      d.dst_stride = (int64_t)P.out_w * P.out_c * 2;
+      d.q16out = 1;
+    }
     int64_t src_bytes = 0;
     if (!P.resize) {
       d.mode = 0;
@@ -1034,7 +1055,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         add_axis_f64(c, E, vt, &d.v);
         add_axis_f64(c, E, ht, &d.h);
       }
-      if (rgb && !P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
+      if (fast_ok && !P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0) {
         auto vit = c->vmv_cache.find(vt);
         if (vit == c->vmv_cache.end()) {
@@ -1067,7 +1088,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           vh = &hit->second;
         }
       }
-      if (rgb && !vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
+      if (fast_ok && !vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0) {
         auto vit = c->mv_cache.find(vt);
         if (vit == c->mv_cache.end()) {
@@ -1087,7 +1108,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         }
       }
       const RingTable *ring = nullptr;
-      if (rgb && !vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
+      if (fast_ok && !vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0 && d.h.maxtaps <= 64) {
         auto rit = c->ring_cache.find(vt);
         if (rit == c->ring_cache.end()) {
@@ -1242,7 +1263,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     if (d.mid) fix_ptr(d.mid, wb);
     const bool apply = (imgs[i].flags & FI_OP_SMARTCROP) && (imgs[i].flags & FI_OP_SMARTCROP_APPLY);
     if (apply) fix_ptr(out_of[i], wb);
-    if (d.gray == 2)
+    if (d.gray == 2 || d.q16out)
       fix_ptr(d.dst, wb);
     else
       d.dst = out_of[i];
@@ -1259,6 +1280,57 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     md.dst_stride = imgs[m.img].out_stride;
     md.st = (MonoState *)(wb + m.st_off);
     mdesc_mono.push_back(md);
+  }
+  // forwarded convolutions: per image, steps in IM's order (unsharp, sharpen,
+  // blur), grouped into one launch per stage
+  std::vector<ConvStep> cst[6];  // U-H, U-V+combine, S-2D, B-H, B-V, to8
+  for (const ConvItem &ci : conv_items) {
+    const ImPlan &P = plans[ci.img];
+    uint16_t *A = (uint16_t *)(wb + ci.a_off), *Bf = (uint16_t *)(wb + ci.b_off);
+    uint16_t *cur = A, *oth = Bf;
+    ConvStep base{};
+    base.W = P.out_w;
+    base.H = P.out_h;
+    base.C = P.out_c;
+    std::vector<double> kk;
+    auto table = [&](const std::vector<double> &v) {
+      const int32_t off = E.od();
+      E.ad.insert(E.ad.end(), v.begin(), v.end());
+      return off;
+    };
+    if (P.conv & 1) {
+      const int w = im_blur_kernel(P.cv[0], P.cv[1], &kk);
+      ConvStep h = base, v = base;
+      h.k = v.k = table(kk);
+      h.kw = w, h.kh = 1, h.in = cur, h.out = oth;
+      v.kw = 1, v.kh = w, v.in = oth, v.orig = cur, v.out = cur;
+      v.gain = P.cv[2];
+      v.thr = 65535.0 * P.cv[3];
+      cst[0].push_back(h);
+      cst[1].push_back(v);
+    }
+    if (P.conv & 2) {
+      const int w = im_sharpen_kernel(P.cv[4], P.cv[5], &kk);
+      ConvStep t = base;
+      t.k = table(kk);
+      t.kw = t.kh = w, t.in = cur, t.out = oth;
+      cst[2].push_back(t);
+      std::swap(cur, oth);
+    }
+    if (P.conv & 4) {
+      const int w = im_blur_kernel(P.cv[6], P.cv[7], &kk);
+      ConvStep h = base, v = base;
+      h.k = v.k = table(kk);
+      h.kw = w, h.kh = 1, h.in = cur, h.out = oth;
+      v.kw = 1, v.kh = w, v.in = oth, v.out = cur;
+      cst[3].push_back(h);
+      cst[4].push_back(v);
+    }
+    ConvStep f = base;
+    f.in = cur;
+    f.dst8 = out_of[ci.img];
+    f.dst_stride = imgs[ci.img].out_stride;
+    cst[5].push_back(f);
   }
   for (size_t k = 0; k < SL.descs.size(); k++) {
     ScDesc &d = SL.descs[k];
@@ -1613,6 +1685,12 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   }
   const size_t apply_off = B.addv(apply);
   const size_t mono_off = B.addv(mdesc_mono);
+  Launch CL[6];
+  for (int k = 0; k < 6; k++) {
+    std::vector<int> all(cst[k].size());
+    for (size_t j = 0; j < all.size(); j++) all[j] = (int)j;
+    CL[k] = add_launch(B, cst[k], all, [](const ConvStep &st) { return st.H; });
+  }
   size_t mono_wts = 0;
   if (!mono.empty() && c->mono_wts_at >= 0) mono_wts = (size_t)c->mono_wts_at;
   if (!mono.empty() && c->mono_wts_at < 0) {
@@ -1714,6 +1792,12 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         hipLaunchKernelGGL(k_rs_v_final, dim3(L2b.tiles), dim3(256), 0, c->stream,
                            (const ResizeDesc *)desc_p(L2b), pre_p(L2b), L2b.n, ai, af);
       }
+    }
+    if (!conv_items.empty()) {
+      Timer t(c, "conv", 0);
+      static const int kMode[6] = {0, 2, 3, 0, 1, 4};
+      for (int k = 0; k < 6; k++)
+        launch_conv(c->stream, kMode[k], (const ConvStep *)desc_p(CL[k]), pre_p(CL[k]), CL[k].n, CL[k].tiles, ad);
     }
     if (!mono.empty()) {
       Timer t(c, "mono", 0);
@@ -1992,6 +2076,95 @@ int fi_debug_monochrome(fi_ctx *c, const uint16_t *gray, int32_t w, int32_t h, i
         hipMemcpy(out, d + o_out, obytes, hipMemcpyDeviceToHost) != hipSuccess)
       rc = set_err(FI_EDEVICE, "fi_debug_monochrome: kernel failed");
   }
+  (void)hipFree(d);
+  return rc;
+}
+
+int fi_debug_convolve(fi_ctx *c, const uint16_t *q16, int32_t w, int32_t h, int32_t ch, const double conv[8],
+                      uint32_t ops, uint8_t *out) {
+  if (!c || !q16 || !conv || !out || w <= 0 || h <= 0 || (ch != 1 && ch != 3) || (ops & ~7u))
+    return set_err(FI_EINVAL, "bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<double> tab, kk;
+  std::vector<ConvStep> st[6];
+  const size_t qb = (size_t)w * h * ch * 2;
+  const size_t o_b = (qb + 255) / 256 * 256, o_out = 2 * o_b, o_tab = o_out + (qb / 2 + 255) / 256 * 256;
+  // host side of the steps (device pointers patched below), as run_batch builds them
+  ConvStep base{};
+  base.W = w;
+  base.H = h;
+  base.C = ch;
+  int cur = 0;  // 0 = buffer A, 1 = B
+  struct Pend {
+    int stage, in, out, orig;
+    ConvStep s;
+  };
+  std::vector<Pend> pend;
+  auto tbl = [&](const std::vector<double> &v) {
+    const int32_t off = (int32_t)tab.size();
+    tab.insert(tab.end(), v.begin(), v.end());
+    return off;
+  };
+  if (ops & 1) {
+    const int kw = im_blur_kernel(conv[0], conv[1], &kk);
+    if (kw < 0) return set_err(FI_EUNSUPPORTED, "unsharp kernel too wide");
+    ConvStep a = base, b = base;
+    a.k = b.k = tbl(kk);
+    a.kw = kw, a.kh = 1;
+    b.kw = 1, b.kh = kw, b.gain = conv[2], b.thr = 65535.0 * conv[3];
+    pend.push_back({0, cur, 1 - cur, -1, a});
+    pend.push_back({1, 1 - cur, cur, cur, b});
+  }
+  if (ops & 2) {
+    const int kw = im_sharpen_kernel(conv[4], conv[5], &kk);
+    if (kw < 0) return set_err(FI_EUNSUPPORTED, "sharpen kernel too wide");
+    ConvStep a = base;
+    a.k = tbl(kk);
+    a.kw = a.kh = kw;
+    pend.push_back({2, cur, 1 - cur, -1, a});
+    cur = 1 - cur;
+  }
+  if (ops & 4) {
+    const int kw = im_blur_kernel(conv[6], conv[7], &kk);
+    if (kw < 0) return set_err(FI_EUNSUPPORTED, "blur kernel too wide");
+    ConvStep a = base, b = base;
+    a.k = b.k = tbl(kk);
+    a.kw = kw, a.kh = 1;
+    b.kw = 1, b.kh = kw;
+    pend.push_back({3, cur, 1 - cur, -1, a});
+    pend.push_back({4, 1 - cur, cur, -1, b});
+  }
+  pend.push_back({5, cur, -1, -1, base});
+  const size_t o_desc = o_tab + (tab.size() * 8 + 255) / 256 * 256, o_pre = o_desc + pend.size() * 256;
+  const size_t total = o_pre + 256;
+  uint8_t *d = nullptr;
+  HIP_TRY(hipMalloc(&d, total));
+  uint16_t *buf[2] = {(uint16_t *)d, (uint16_t *)(d + o_b)};
+  int rc = FI_OK;
+  const int32_t pre[2] = {0, h};
+  if (hipMemcpy(d, q16, qb, hipMemcpyHostToDevice) != hipSuccess ||
+      (!tab.empty() && hipMemcpy(d + o_tab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice) != hipSuccess) ||
+      hipMemcpy(d + o_pre, pre, sizeof(pre), hipMemcpyHostToDevice) != hipSuccess)
+    rc = set_err(FI_EDEVICE, "fi_debug_convolve: upload failed");
+  static const int kMode[6] = {0, 2, 3, 0, 1, 4};
+  for (size_t j = 0; rc == FI_OK && j < pend.size(); j++) {
+    ConvStep s = pend[j].s;
+    s.in = buf[pend[j].in];
+    s.out = pend[j].out >= 0 ? buf[pend[j].out] : nullptr;
+    s.orig = pend[j].orig >= 0 ? buf[pend[j].orig] : nullptr;
+    s.dst8 = d + o_out;
+    s.dst_stride = (int64_t)w * ch;
+    uint8_t *dd = d + o_desc + 256 * j;
+    if (hipMemcpy(dd, &s, sizeof(s), hipMemcpyHostToDevice) != hipSuccess) {
+      rc = set_err(FI_EDEVICE, "fi_debug_convolve: upload failed");
+      break;
+    }
+    launch_conv(c->stream, kMode[pend[j].stage], (const ConvStep *)dd, (const int32_t *)(d + o_pre), 1, h,
+                (const double *)(d + o_tab));
+  }
+  if (rc == FI_OK && (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess ||
+                      hipMemcpy(out, d + o_out, (size_t)w * h * ch, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = set_err(FI_EDEVICE, "fi_debug_convolve: kernel failed");
   (void)hipFree(d);
   return rc;
 }

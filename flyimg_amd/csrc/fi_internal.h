@@ -55,6 +55,7 @@ struct ResizeDesc {
   uint8_t *dst;
   int64_t dst_stride;
   int32_t out_w, out_h, out_c;  // post-rotate dims
+  int32_t q16out;               // 1: the epilogue writes rotated Q16 (u16) for the convolution stage
   // fused vertical-first kernel: list of touched source rows and, per list
   // row, the weight of each of the K ring slots and the output row owning it
   int32_t fused_k;     // ring slots (0 = not fused)
@@ -75,6 +76,22 @@ struct FusedTile {
   int32_t htaps;       // horizontal taps of every column of the strip (zero padded)
   int32_t hstart;      // ai offset: first source column of each column's window [nx]
   int32_t hw;          // af offset: weights, transposed [htaps][nx]
+};
+
+// One step of the forwarded convolutions (fi_conv.hip) on one image's rotated
+// Q16 HWC buffer: mode 0 horizontal 1-D pass, 1 vertical 1-D pass, 2 vertical
+// pass + unsharp combine with `orig` (written in place), 3 2-D pass, 4 Q16 ->
+// 8-bit dst.
+struct ConvStep {
+  const uint16_t *in;
+  uint16_t *out;
+  const uint16_t *orig;  // mode 2
+  uint8_t *dst8;         // mode 4
+  int64_t dst_stride;    // mode 4, bytes
+  int32_t W, H, C;
+  int32_t kw, kh;        // kernel extent
+  int32_t k;             // ad offset of the kernel values
+  double gain, thr;      // mode 2: unsharp gain, QuantumRange * threshold
 };
 
 // smartcrop crop window in the analysed image (smartcrop.py crops()).

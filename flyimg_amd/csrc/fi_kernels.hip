@@ -72,7 +72,18 @@ __device__ __forceinline__ void store_pixel(const ResizeDesc &D, int x, int y, u
     dy = D.ew - 1 - x;
   }
   uint8_t *o = D.dst + (int64_t)dy * D.dst_stride;
-  if (D.gray == 2) {
+  if (D.q16out) {
+    // the rotated Q16 image of the forwarded convolutions (fi_conv.hip)
+    uint16_t *q = reinterpret_cast<uint16_t *>(o);
+    if (D.gray) {
+      const double gv = 0.212656 * (double)r + 0.715158 * (double)g + 0.072186 * (double)b;
+      q[dx] = (uint16_t)clamp_q16d(gv);
+    } else {
+      q[dx * 3 + 0] = (uint16_t)r;
+      q[dx * 3 + 1] = (uint16_t)g;
+      q[dx * 3 + 2] = (uint16_t)b;
+    }
+  } else if (D.gray == 2) {
     // -monochrome input: the Q16 gray value itself (u16 scratch, fi_mono.hip; rot = 0)
     const double gv = 0.212656 * (double)r + 0.715158 * (double)g + 0.072186 * (double)b;
     reinterpret_cast<uint16_t *>(o)[dx] = (uint16_t)clamp_q16d(gv);

@@ -11,6 +11,8 @@
 #include "fi_plan.h"
 
 #include <math.h>
+
+#include <cmath>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -151,10 +153,114 @@ int plan_im(const fi_image &img, ImPlan *p) {
   if (matte && (f & FI_OP_SMARTCROP))
     return fail(FI_EUNSUPPORTED, "smartcrop of an RGBA image: smartcrop.py fails on RGBA (split(), smartcrop.py:17)");
   p->out_c = matte ? (p->gray ? 2 : 4) : (p->gray ? 1 : 3);
+  p->conv = ((f & FI_OP_UNSHARP) ? 1u : 0u) | ((f & FI_OP_SHARPEN) ? 2u : 0u) | ((f & FI_OP_BLUR) ? 4u : 0u);
+  if (p->conv) {
+    if (matte || p->mono)
+      return fail(FI_EUNSUPPORTED, "-unsharp/-sharpen/-blur of an RGBA or -monochrome image are not on the GPU path");
+    for (int k = 0; k < 4; k++) p->cv[k] = img.unsharp[k];
+    p->cv[4] = img.sharpen[0];
+    p->cv[5] = img.sharpen[1];
+    p->cv[6] = img.blur[0];
+    p->cv[7] = img.blur[1];
+    for (double v : p->cv)
+      if (!std::isfinite(v) || fabs(v) > 1e6) return fail(FI_EINVAL, "convolution parameter out of range");
+    std::vector<double> kk;
+    if ((p->conv & 1) && im_blur_kernel(p->cv[0], p->cv[1], &kk) < 0)
+      return fail(FI_EUNSUPPORTED, "-unsharp kernel wider than the GPU path supports");
+    if ((p->conv & 2) && im_sharpen_kernel(p->cv[4], p->cv[5], &kk) < 0)
+      return fail(FI_EUNSUPPORTED, "-sharpen kernel wider than the GPU path supports");
+    if ((p->conv & 4) && im_blur_kernel(p->cv[6], p->cv[7], &kk) < 0)
+      return fail(FI_EUNSUPPORTED, "-blur kernel wider than the GPU path supports");
+  }
   const bool swap = p->rot == 90 || p->rot == 270;
   p->out_w = swap ? p->eh : p->ew;
   p->out_h = swap ? p->ew : p->eh;
   return FI_OK;
+}
+
+// --- forwarded convolution kernels (IM 6.9 gem.c / morphology.c / effect.c) ----
+static double conv_reciprocal(double x) {  // PerceptibleReciprocal
+  const double sign = x < 0.0 ? -1.0 : 1.0;
+  if ((sign * x) >= kImEpsilon) return 1.0 / x;
+  return sign / kImEpsilon;
+}
+static constexpr double kSq2Pi = 2.50662827463100024161235523934010416269302368164062;  // MagickSQ2PI
+static constexpr double k2Pi = 6.283185307179586476925286766559005768394338798750211641949;  // Magick2PI
+static int kernel_width_1d(double radius, double sigma) {  // GetOptimalKernelWidth1D
+  if (radius > kImEpsilon) return (int)(2.0 * ceil(radius) + 1.0);
+  const double gamma = fabs(sigma);
+  if (gamma <= kImEpsilon) return 3;
+  const double alpha = conv_reciprocal(2.0 * gamma * gamma), beta = conv_reciprocal(kSq2Pi * gamma);
+  int width;
+  for (width = 5; width < 4 * kConvMaxBlur;) {
+    double normalize = 0.0;
+    const int j = (width - 1) / 2;
+    for (int i = -j; i <= j; i++) normalize += exp(-((double)(i * i)) * alpha) * beta;
+    const double value = exp(-((double)(j * j)) * alpha) * beta / normalize;
+    if ((value < 1.0 / 65535.0) || (value < kImEpsilon)) break;
+    width += 2;
+  }
+  return width - 2;
+}
+static int kernel_width_2d(double radius, double sigma) {  // GetOptimalKernelWidth2D
+  if (radius > kImEpsilon) return (int)(2.0 * ceil(radius) + 1.0);
+  const double gamma = fabs(sigma);
+  if (gamma <= kImEpsilon) return 3;
+  const double alpha = conv_reciprocal(2.0 * gamma * gamma), beta = conv_reciprocal(k2Pi * gamma * gamma);
+  int width;
+  for (width = 5; width < 4 * kConvMaxSharpen;) {
+    double normalize = 0.0;
+    const int j = (width - 1) / 2;
+    for (int v = -j; v <= j; v++)
+      for (int u = -j; u <= j; u++) normalize += exp(-((double)(u * u + v * v)) * alpha) * beta;
+    const double value = exp(-((double)(j * j)) * alpha) * beta / normalize;
+    if ((value < 1.0 / 65535.0) || (value < kImEpsilon)) break;
+    width += 2;
+  }
+  return width - 2;
+}
+int im_blur_kernel(double radius, double sigma, std::vector<double> *k) {
+  sigma = fabs(sigma);
+  const int width = radius >= 1.0 ? (int)radius * 2 + 1 : kernel_width_1d(radius, sigma);
+  if (width < 1 || width > kConvMaxBlur) return -1;
+  k->assign(width, 0.0);
+  const int x = (width - 1) / 2;
+  if (sigma > kImEpsilon) {  // KernelRank 3: a Gaussian 3x as wide, binned
+    const int v = (width * 3 - 1) / 2;
+    const double s3 = sigma * 3.0;
+    const double alpha = 1.0 / (2.0 * s3 * s3), beta = 1.0 / (kSq2Pi * s3);
+    for (int u = -v; u <= v; u++) (*k)[(u + v) / 3] += exp(-((double)(u * u)) * alpha) * beta;
+  } else {
+    (*k)[x] = 1.0;
+  }
+  double pos = 0.0;  // ScaleKernelInfo(1.0, CorrelateNormalizeValue): 1 / positive range
+  for (double v : *k)
+    if (v > 0.0) pos += v;
+  const double scale = 1.0 / (fabs(pos) >= kImEpsilon ? pos : 1.0);
+  for (double &v : *k) v *= scale;
+  return width;
+}
+int im_sharpen_kernel(double radius, double sigma, std::vector<double> *k) {
+  const int width = kernel_width_2d(radius, sigma);
+  if (width < 1 || width > kConvMaxSharpen) return -1;
+  k->assign((size_t)width * width, 0.0);
+  const double ms = fabs(sigma) < kImEpsilon ? kImEpsilon : sigma;  // MagickSigma
+  const int j = (width - 1) / 2;
+  double normalize = 0.0;
+  int i = 0;
+  for (int v = -j; v <= j; v++)
+    for (int u = -j; u <= j; u++) {
+      (*k)[i] = -exp(-((double)u * u + v * v) / (2.0 * ms * ms)) /
+                (2.0 * 3.14159265358979323846264338327950288419716939937510 * ms * ms);
+      normalize += (*k)[i];
+      i++;
+    }
+  (*k)[i / 2] = (-2.0) * normalize;
+  normalize = 0.0;
+  for (double v : *k) normalize += v;
+  const double gamma = conv_reciprocal(normalize);
+  for (double &v : *k) v *= gamma;
+  return width;
 }
 
 // --- resize.c filters --------------------------------------------------------

@@ -31,8 +31,18 @@ struct ImPlan {
   bool mono = false;        // -monochrome: Q16 gray of the extent window -> fi_mono.hip -> rotate
   int rot = 0;
   int out_w = 0, out_h = 0, out_c = 3;   // after rotate
+  // forwarded convolutions on the rotated Q16 image (bit 0 unsharp, 1 sharpen, 2 blur)
+  unsigned conv = 0;
+  double cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // unsharp r, s, gain, thr; sharpen r, s; blur r, s
 };
 int plan_im(const fi_image &img, ImPlan *p);
+// IM 6.9 kernels of the forwarded convolutions (morphology.c BlurKernel,
+// effect.c SharpenImage): width, values (f64) -- the same arithmetic as the
+// oracle's or_im_blur_kernel / or_im_sharpen_kernel.
+int im_blur_kernel(double radius, double sigma, std::vector<double> *k);
+int im_sharpen_kernel(double radius, double sigma, std::vector<double> *k);
+constexpr int kConvMaxBlur = 1023;   // 1-D taps
+constexpr int kConvMaxSharpen = 63;  // 2-D kernel side
 
 // One resample axis in the source index domain.
 struct AxisTable {

@@ -45,6 +45,23 @@ class ExecFailedException(RuntimeError):
     """Processor.php:53-59: a failed pixel operation."""
 
 
+def im_parse_geometry(text: str):
+    """ImageMagick ParseGeometry for the -unsharp / -sharpen / -blur arguments
+    (geometry.c): ``rho[xsigma][+xi][+psi]`` -> (rho, sigma, xi, psi), None for
+    a value that is absent (mogrify then applies its defaults: sigma 1, gain 1,
+    threshold 0.05).  Separators 'x' / 'X' / ',' / '/' and signs '+' / '-'."""
+    import re
+
+    m = re.fullmatch(r"\s*([+-]?[0-9]*\.?[0-9]+(?:[eE][+-]?[0-9]+)?)?"
+                     r"(?:[xX,/]([+-]?[0-9]*\.?[0-9]+(?:[eE][+-]?[0-9]+)?))?"
+                     r"([+-][0-9]*\.?[0-9]+(?:[eE][+-]?[0-9]+)?)?"
+                     r"([+-][0-9]*\.?[0-9]+(?:[eE][+-]?[0-9]+)?)?\s*", text)
+    if not m or m.group(1) is None:
+        raise ExecFailedException(f"invalid geometry {text!r}")
+    vals = [float(x) if x is not None else None for x in m.groups()]
+    return vals[0], vals[1], vals[2], vals[3]
+
+
 def _empty(v) -> bool:
     """PHP empty(): null, '', '0', 0, false are empty."""
     return v is None or v is False or v == "" or v == "0" or v == 0
@@ -202,9 +219,21 @@ class ImageProcessor:
                 raise ExecFailedException(f"-rotate {rot} (non-integral) is not on the GPU path")
             op.flags |= L.FI_OP_ROTATE
             op.rotate = deg
-        for k in ("unsharp", "sharpen", "blur", "background"):
-            if not _empty(o.get_option(k)):
-                raise ExecFailedException(f"-{k} is not on the GPU path")
+        if not _empty(o.get_option("background")):
+            raise ExecFailedException("-background is not on the GPU path")
+        # forwarded convolutions (:303-315), applied after -rotate in this order
+        v = o.get_option("unsharp")
+        if not _empty(v):
+            g = im_parse_geometry(str(v))
+            op.flags |= L.FI_OP_UNSHARP
+            op.unsharp = (g[0], g[1] if g[1] is not None else 1.0, g[2] if g[2] is not None else 1.0,
+                          g[3] if g[3] is not None else 0.05)
+        for key, flag in (("sharpen", L.FI_OP_SHARPEN), ("blur", L.FI_OP_BLUR)):
+            v = o.get_option(key)
+            if not _empty(v):
+                g = im_parse_geometry(str(v))
+                op.flags |= flag
+                setattr(op, key, (g[0], g[1] if g[1] is not None else 1.0))
         if not _empty(o.get_option("smart-crop")):
             # SmartCropProcessor runs smartcrop.py with its CLI defaults (100x100)
             op.flags |= L.FI_OP_SMARTCROP | L.FI_OP_SMARTCROP_APPLY

@@ -27,12 +27,21 @@ class Op:
     rotate: int = 0
     smartcrop_w: int = 0
     smartcrop_h: int = 0
+    # forwarded -unsharp / -sharpen / -blur (FI_OP_UNSHARP / SHARPEN / BLUR)
+    unsharp: tuple = (0.0, 1.0, 1.0, 0.05)
+    sharpen: tuple = (0.0, 1.0)
+    blur: tuple = (0.0, 1.0)
 
 
 def _fill(img: L.FiImage, op: Op):
     img.target_w, img.target_h = op.target_w, op.target_h
     img.flags, img.gravity, img.rotate = op.flags, op.gravity, op.rotate
     img.smartcrop_w, img.smartcrop_h = op.smartcrop_w, op.smartcrop_h
+    for k in range(4):
+        img.unsharp[k] = op.unsharp[k]
+    for k in range(2):
+        img.sharpen[k] = op.sharpen[k]
+        img.blur[k] = op.blur[k]
 
 
 def plan(width: int, height: int, op: Op):
@@ -185,6 +194,17 @@ class Context:
         oh, ow = (w, h) if rot in (90, 270) else (h, w)
         out = np.zeros((oh, ow), np.uint8)
         L.check(self._lib.fi_debug_monochrome(self.h, g.ctypes.data, w, h, rot, out.ctypes.data, ow))
+        return out
+
+    def convolve_q16(self, q16: np.ndarray, conv, ops: int) -> np.ndarray:
+        """Test hook: the forwarded convolution kernels on a Q16 HWC image
+        (fi_debug_convolve); conv = unsharp[4] + sharpen[2] + blur[2]."""
+        q = np.ascontiguousarray(q16, dtype=np.uint16)
+        h, w = q.shape[:2]
+        ch = q.shape[2] if q.ndim == 3 else 1
+        cv = (ctypes.c_double * 8)(*conv)
+        out = np.zeros(q.shape, np.uint8)
+        L.check(self._lib.fi_debug_convolve(self.h, q.ctypes.data, w, h, ch, cv, ops, out.ctypes.data))
         return out
 
 

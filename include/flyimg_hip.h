@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define FI_ABI_VERSION 1
+#define FI_ABI_VERSION 2  /* 2: forwarded convolution operators (unsharp/sharpen/blur fields) */
 
 /* ---- status codes ---------------------------------------------------- */
 #define FI_OK 0
@@ -61,6 +61,10 @@ extern "C" {
 #define FI_OP_ROTATE (1u << 7)         /* -rotate <deg>, multiples of 90 (r_90, :306)     */
 #define FI_OP_SMARTCROP (1u << 8)      /* compute smartcrop.py's box on the result (smc_1) */
 #define FI_OP_SMARTCROP_APPLY (1u << 9) /* and crop to it (SmartCropProcessor.php:30-34)   */
+/* forwarded convolutions (ImageProcessor.php:303-315), after -rotate, in this order: */
+#define FI_OP_UNSHARP (1u << 10)       /* -unsharp RxS+gain+threshold (unsh_)               */
+#define FI_OP_SHARPEN (1u << 11)       /* -sharpen RxS (sh_)                                */
+#define FI_OP_BLUR (1u << 12)          /* -blur RxS (blr_)                                  */
 
 /* ImageMagick GravityType values used by -gravity (parameters.yml:99). */
 #define FI_GRAVITY_NORTHWEST 1
@@ -98,6 +102,10 @@ typedef struct fi_image {
   double crop_score;                      /* top_crop["score"]["total"]           */
   int32_t status;                         /* FI_OK or FI_E* for this image        */
   int32_t n_candidates;                   /* crops re-scored exactly (diagnostic) */
+  /* ---- inputs of the forwarded convolutions (ABI 2), IM ParseGeometry values ---- */
+  double unsharp[4];       /* radius, sigma (1), gain (1), threshold (0.05) -- FI_OP_UNSHARP */
+  double sharpen[2];       /* radius, sigma (1)                             -- FI_OP_SHARPEN */
+  double blur[2];          /* radius, sigma (1)                             -- FI_OP_BLUR    */
 } fi_image;
 
 /* SmartCrop.__init__ keyword arguments (python/smartcrop.py:41-77). */
@@ -222,6 +230,13 @@ int fi_rccl_gather_records(fi_ctx *ctx, const fi_record *send, int32_t count, fi
  * caller-supplied Q16 gray image (host buffers), w x h row-major, rotated by
  * rot (0/90/180/270) into out (0/255 bytes).  Lets the parity tests feed the
  * oracle's or_im_monochrome the identical input. */
+/* Test hook (not a reference interface): the forwarded convolution kernels
+ * (FI_OP_UNSHARP/SHARPEN/BLUR bits 0/1/2 of `ops`, conv = the fi_image
+ * unsharp[4], sharpen[2], blur[2] values) on a rotated Q16 HWC image
+ * (ch 1 or 3) -> 8-bit out (w * ch bytes per row), so tests can run the
+ * oracle's or_im_convolve_ops on the identical input. */
+int fi_debug_convolve(fi_ctx *ctx, const uint16_t *q16, int32_t w, int32_t h, int32_t ch, const double conv[8],
+                      uint32_t ops, uint8_t *out);
 int fi_debug_monochrome(fi_ctx *ctx, const uint16_t *gray, int32_t w, int32_t h, int32_t rot, uint8_t *out,
                         int32_t out_stride);
 

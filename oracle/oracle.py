@@ -86,6 +86,13 @@ def lib():
         L.or_im_resize_u8_to_q16.argtypes = [u8p, i, i, i, i, i, i, i, i, P(ctypes.c_uint16)]
         L.or_im_convert.argtypes = [u8p, i, i, i, i, i, ctypes.c_uint, i, i, u8p, i, P(i), P(i), P(i)]
         L.or_im_convert_c.argtypes = [u8p, i, i, i, i, i, i, ctypes.c_uint, i, i, u8p, i, P(i), P(i), P(i)]
+        L.or_im_convert_ex.argtypes = [u8p, i, i, i, i, i, i, ctypes.c_uint, i, i, P(ctypes.c_double), ctypes.c_uint,
+                                       u8p, i, P(i), P(i), P(i)]
+        L.or_im_convolve_ops.argtypes = [P(ctypes.c_uint16), i, i, i, P(ctypes.c_double), ctypes.c_uint]
+        L.or_im_blur_kernel.argtypes = [ctypes.c_double, ctypes.c_double, P(ctypes.c_double), i]
+        L.or_im_sharpen_kernel.argtypes = [ctypes.c_double, ctypes.c_double, P(ctypes.c_double), i]
+        L.or_im_kernel_width_1d.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.or_im_kernel_width_2d.argtypes = [ctypes.c_double, ctypes.c_double]
         L.or_im_gravity_offset.argtypes = [i, i, i, i, i, P(i), P(i)]
         L.or_im_gravity_offset.restype = None
         L.or_im_sample_index.argtypes = [ctypes.c_long] * 3
@@ -152,6 +159,7 @@ def im_gravity_offset(W, H, ew, eh, gravity=5):
 
 FLAG_THUMBNAIL, FLAG_FILL, FLAG_SHRINK, FLAG_EXTENT, FLAG_GRAY, FLAG_ROTATE = 1, 2, 4, 8, 16, 32
 FLAG_MONO = 64  # -monochrome (B7); implies gray
+CONV_UNSHARP, CONV_SHARPEN, CONV_BLUR = 1, 2, 4  # forwarded convolutions (ImageProcessor.php:303-315)
 
 
 def im_monochrome(gray_q16: np.ndarray) -> np.ndarray:
@@ -188,10 +196,13 @@ def mono_quant_info(hist: np.ndarray):
     return n.value, m[: min(n.value, 2)].tolist(), b[: min(n.value, 2)].tolist()
 
 
-def im_convert(src: np.ndarray, rw=0, rh=0, flags=FLAG_THUMBNAIL, gravity=5, rotate=0) -> np.ndarray:
+def im_convert(src: np.ndarray, rw=0, rh=0, flags=FLAG_THUMBNAIL, gravity=5, rotate=0, conv=None,
+               conv_ops=0) -> np.ndarray:
     """convert <src> <resize op> [-gravity g -extent WxH] [-colorspace Gray] [-monochrome] [-rotate r].
     RGBA sources (H x W x 4) take IM's matte path: Mitchell, alpha-weighted passes,
-    RGBA out (gray + alpha after -colorspace Gray)."""
+    RGBA out (gray + alpha after -colorspace Gray).  conv = (unsharp radius, sigma,
+    gain, threshold, sharpen radius, sigma, blur radius, sigma), conv_ops = CONV_*
+    bits: the forwarded -unsharp / -sharpen / -blur after -rotate."""
     src = np.ascontiguousarray(src, dtype=np.uint8)
     H, W = src.shape[:2]
     C = src.shape[2] if src.ndim == 3 else 1  # 3 = RGB, 4 = RGBA (IM matte image)
@@ -201,12 +212,25 @@ def im_convert(src: np.ndarray, rw=0, rh=0, flags=FLAG_THUMBNAIL, gravity=5, rot
     cap = 4 * (max(tw, rw or 0) * max(th, rh or 0) + 16)  # output bound (an int32 on the C side)
     out = np.zeros(cap, np.uint8)
     ow, oh, oc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    rc = lib().or_im_convert_c(_u8(src), W, H, C, W * C, rw, rh, flags, gravity, rotate, _u8(out), cap,
-                               ctypes.byref(ow), ctypes.byref(oh), ctypes.byref(oc))
+    cv = (ctypes.c_double * 8)(*(list(conv) + [0.0] * 8)[:8]) if conv is not None else (ctypes.c_double * 8)()
+    rc = lib().or_im_convert_ex(_u8(src), W, H, C, W * C, rw, rh, flags, gravity, rotate, cv, conv_ops, _u8(out),
+                                cap, ctypes.byref(ow), ctypes.byref(oh), ctypes.byref(oc))
     if rc:
         raise ValueError(f"or_im_convert rc={rc}")
     o = out[: ow.value * oh.value * oc.value].reshape(oh.value, ow.value, oc.value)
     return o[:, :, 0] if oc.value == 1 else o
+
+
+def im_convolve_q16(q16: np.ndarray, conv, ops: int) -> np.ndarray:
+    """or_im_convolve_ops (-unsharp / -sharpen / -blur on a Q16 HWC image) -> 8-bit."""
+    q = np.ascontiguousarray(q16, dtype=np.uint16).copy()
+    h, w = q.shape[:2]
+    ch = q.shape[2] if q.ndim == 3 else 1
+    cv = (ctypes.c_double * 8)(*conv)
+    rc = lib().or_im_convolve_ops(q.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), w, h, ch, cv, ops)
+    if rc:
+        raise ValueError(f"or_im_convolve_ops rc={rc}")
+    return (((q.astype(np.uint32) + 128) - ((q.astype(np.uint32) + 128) >> 8)) >> 8).astype(np.uint8)
 
 
 def im_resize_q16(src: np.ndarray, ow: int, oh: int, thumbnail=True) -> np.ndarray:

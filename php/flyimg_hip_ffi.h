@@ -14,6 +14,9 @@ typedef struct fi_image {
   int32_t crop_x, crop_y, crop_w, crop_h;
   double crop_score;
   int32_t status, n_candidates;
+  double unsharp[4];
+  double sharpen[2];
+  double blur[2];
 } fi_image;
 typedef struct fi_ctx fi_ctx;
 int32_t fi_abi_version(void);

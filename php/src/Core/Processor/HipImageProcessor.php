@@ -30,6 +30,9 @@ class HipImageProcessor extends ImageProcessor
     private const FI_OP_ROTATE = 1 << 7;
     private const FI_OP_SMARTCROP = 1 << 8;
     private const FI_OP_SMARTCROP_APPLY = 1 << 9;
+    private const FI_OP_UNSHARP = 1 << 10;
+    private const FI_OP_SHARPEN = 1 << 11;
+    private const FI_OP_BLUR = 1 << 12;
     private const GRAVITY = ['NorthWest' => 1, 'North' => 2, 'NorthEast' => 3, 'West' => 4, 'Center' => 5,
         'East' => 6, 'SouthWest' => 7, 'South' => 8, 'SouthEast' => 9];
 
@@ -106,7 +109,7 @@ class HipImageProcessor extends ImageProcessor
             $flags |= self::FI_OP_GRAY;
         }
         if (!empty($outputImage->extractKey('monochrome'))) {
-            $flags |= self::FI_OP_MONOCHROME;                                   // FI_EUNSUPPORTED today
+            $flags |= self::FI_OP_MONOCHROME;
         }
         $rotate = (int)$this->options->getOption('rotate');
         if ($rotate % 360 !== 0) {
@@ -114,6 +117,24 @@ class HipImageProcessor extends ImageProcessor
         }
         if (!empty($outputImage->extractKey('smart-crop'))) {                   // ImageHandler.php:125-133
             $flags |= self::FI_OP_SMARTCROP | self::FI_OP_SMARTCROP_APPLY;
+        }
+        // forwarded -unsharp / -sharpen / -blur (:303-315), after -rotate in this order;
+        // mogrify's defaults for absent geometry values: sigma 1, gain 1, threshold 0.05
+        foreach (['unsharp' => [self::FI_OP_UNSHARP, [0.0, 1.0, 1.0, 0.05]],
+                  'sharpen' => [self::FI_OP_SHARPEN, [0.0, 1.0]],
+                  'blur' => [self::FI_OP_BLUR, [0.0, 1.0]]] as $key => [$flag, $defaults]) {
+            $value = (string)$this->options->getOption($key);
+            if ($value === '') {
+                continue;
+            }
+            if (!preg_match('/^([+-]?[0-9]*\.?[0-9]+)(?:[xX,\/]([+-]?[0-9]*\.?[0-9]+))?' .
+                '([+-][0-9]*\.?[0-9]+)?([+-][0-9]*\.?[0-9]+)?$/', $value, $m)) {
+                throw new ExecFailedException("Command failed.\nThe exit code: geometry\nThe last line of output: " . $value);
+            }
+            $flags |= $flag;
+            foreach ($defaults as $k => $d) {
+                $img->{$key}[$k] = (isset($m[$k + 1]) && $m[$k + 1] !== '') ? (float)$m[$k + 1] : $d;
+            }
         }
         $img->target_w = $tw;
         $img->target_h = $th;

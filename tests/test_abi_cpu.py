@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
     for n in names:
         assert hasattr(lib, n)
-    assert lib.fi_abi_version() == 1
+    assert lib.fi_abi_version() == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -118,7 +118,7 @@ def _norm_decls(text):
         decl = re.sub(r"\s+", " ", decl).strip()
         if not decl:
             continue
-        m = re.match(r"(.*?)\s*(\**)([A-Za-z_][A-Za-z0-9_]*)((?:\s*,\s*\**[A-Za-z_][A-Za-z0-9_]*)*)$", decl)
+        m = re.match(r"(.*?)\s*(\**)([A-Za-z_][A-Za-z0-9_]*(?:\[\d+\])?)((?:\s*,\s*\**[A-Za-z_][A-Za-z0-9_]*)*)$", decl)
         base = m.group(1)
         names = [m.group(2) + m.group(3)] + [n.strip() for n in m.group(4).split(",") if n.strip()]
         fields += [(base.strip(), n) for n in names]

@@ -528,3 +528,84 @@ def test_rgba_rejects_smartcrop_and_monochrome(ctx):
     for f in (L.FI_OP_THUMBNAIL | L.FI_OP_SMARTCROP, L.FI_OP_THUMBNAIL | L.FI_OP_MONOCHROME):
         outs, recs, rc = ctx.process([src], [Op(100, 0, f, L.GRAVITY["Center"], 0, 100, 100)])
         assert recs[0].status == L.FI_EUNSUPPORTED
+
+
+# ---------------------------------------------------------------------------
+# Forwarded convolutions (-unsharp / -sharpen / -blur, ImageProcessor.php:303-315)
+CONV_CASES = [
+    # (name, conv[8], ops) -- the url-options.md examples and a combination
+    ("unsh_0x6", (0, 6, 1, 0.05, 0, 1, 0, 1), 1),
+    ("unsh_0.25x0.25+8+0.065", (0.25, 0.25, 8, 0.065, 0, 1, 0, 1), 1),
+    ("unsh_1x1+2+0", (1, 1, 2, 0.0, 0, 1, 0, 1), 1),
+    ("sh_3", (0, 1, 1, 0.05, 3, 1, 0, 1), 2),
+    ("sh_0x5", (0, 1, 1, 0.05, 0, 5, 0, 1), 2),
+    ("blr_2", (0, 1, 1, 0.05, 0, 1, 2, 1), 4),
+    ("blr_1x2", (0, 1, 1, 0.05, 0, 1, 1, 2), 4),
+    ("all", (0.5, 1, 1.5, 0.02, 1, 0.8, 0, 2), 7),
+]
+
+
+@pytest.mark.parametrize("ch", [3, 1])
+@pytest.mark.parametrize("case", CONV_CASES, ids=[c[0] for c in CONV_CASES])
+def test_convolve_kernels_bit_exact(ctx, case, ch):
+    """fi_conv.hip on a Q16 image == the oracle's or_im_convolve_ops on the
+    identical input, bit for bit (same f64 operation order)."""
+    _, conv, ops = case
+    rng = np.random.default_rng(len(case[0]) * 7 + ch)
+    q = (synth_rgb(173, 97, 11).astype(np.uint16) * 257)
+    q = np.clip(q.astype(np.int32) + rng.integers(-300, 300, q.shape), 0, 65535).astype(np.uint16)
+    if ch == 1:
+        q = np.ascontiguousarray(q[..., 1])
+    got = ctx.convolve_q16(q, conv, ops)
+    ref = orc.im_convolve_q16(q, conv, ops)
+    assert np.array_equal(got, ref)
+
+
+CONV_PIPE = [
+    ("w_300,blr_2", 0.0),
+    ("w_300,h_200,c_1,r_90,sh_3", 0.0),
+    ("w_320,clsp_Gray,unsh_0x6", 0.001),
+    ("w_300,unsh_0.25x0.25+8+0.065,sh_0x5,blr_1x2", 0.001),
+]
+
+
+@pytest.mark.parametrize("opts,outliers", CONV_PIPE, ids=[c[0] for c in CONV_PIPE])
+def test_convolve_pipeline_matches_oracle(ctx, opts, outliers):
+    """Resample -> extent -> gray -> rotate -> convolutions through the
+    GPU path vs the oracle: +-1 LSB (the resample's Q16 is within a few
+    units of IM's f64; an -unsharp threshold can flip a pixel that sits on it,
+    so those cases allow a 0.1 % tail)."""
+    from flyimg_amd.processor import ImageProcessor, OptionsBag, process_new_image
+
+    src = synth_rgb(900, 600, 5)
+    out, rec = process_new_image(ctx, opts, src)
+    op = ImageProcessor(OptionsBag(opts), 900, 600).to_op()
+    flags = 0
+    for f, o in ((L.FI_OP_THUMBNAIL, orc.FLAG_THUMBNAIL), (L.FI_GEOM_FILL, orc.FLAG_FILL),
+                 (L.FI_GEOM_SHRINK_ONLY, orc.FLAG_SHRINK), (L.FI_OP_EXTENT, orc.FLAG_EXTENT),
+                 (L.FI_OP_GRAY, orc.FLAG_GRAY), (L.FI_OP_ROTATE, orc.FLAG_ROTATE)):
+        if op.flags & f:
+            flags |= o
+    ops = (1 if op.flags & L.FI_OP_UNSHARP else 0) | (2 if op.flags & L.FI_OP_SHARPEN else 0) | \
+          (4 if op.flags & L.FI_OP_BLUR else 0)
+    ref = orc.im_convert(src, op.target_w, op.target_h, flags, op.gravity, op.rotate,
+                         conv=tuple(op.unsharp) + tuple(op.sharpen) + tuple(op.blur), conv_ops=ops)
+    assert out.shape == ref.shape
+    d = np.abs(out.astype(np.int16) - ref.astype(np.int16))
+    assert (d > 1).mean() <= outliers, (d.max(), (d > 1).mean())
+
+
+def test_convolve_then_smartcrop(ctx):
+    """smc_1 runs on the convolved output (SmartCropProcessor reads the
+    encoded result of the whole convert): the GPU box equals the oracle's
+    smartcrop on the GPU's pixels."""
+    from flyimg_amd.processor import ImageProcessor, OptionsBag
+
+    src = synth_rgb(1280, 720, 9)
+    op = ImageProcessor(OptionsBag("w_500,blr_2,smc_1"), 1280, 720).to_op()
+    no_apply = Op(op.target_w, op.target_h, op.flags & ~L.FI_OP_SMARTCROP_APPLY, op.gravity, op.rotate, 100, 100,
+                  op.unsharp, op.sharpen, op.blur)
+    outs, recs, rc = ctx.process([src], [no_apply])
+    L.check(rc)
+    t = orc.sc_crop(outs[0], 100, 100)["top_crop"]
+    assert (recs[0].crop_x, recs[0].crop_y, recs[0].crop_w, recs[0].crop_h) == (t["x"], t["y"], t["width"], t["height"])
