@@ -1,0 +1,85 @@
+"""Host codec pipeline around the GPU path:
+ImageHandler::processNewImage end to end for a batch of encoded images.
+
+  decode   Pillow (libjpeg-turbo / libpng) on a thread pool -- the decoders
+           release the GIL -- with ``-auto-orient`` (ImageProcessor.php:78)
+           applied from the EXIF orientation, then ExtractProcessor's view;
+  process  ONE fi_process_batch for the whole batch (ImageProcessor +
+           SmartCropProcessor on the MI355X);
+  encode   on the thread pool: JPEG at ``q_`` (default 90) -- flyimg pipes
+           TGA into MozJPEG's cjpeg when it is executable and otherwise lets
+           ImageMagick write the JPEG with ``-quality`` (calculateQuality,
+           ImageProcessor.php:195-217); neither ``cjpeg`` nor ``convert`` is
+           in this image, so the encoder is libjpeg-turbo at the same quality
+           (IM's own JPEG coder is libjpeg as well).  Images with alpha are
+           written as PNG.
+
+Gray (L) and palette sources are expanded to RGB / RGBA before the GPU
+(IM would keep a gray JPEG gray: the channels are equal either way).
+"""
+from __future__ import annotations
+
+import io
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import _lib as L
+from .processor import ExecFailedException, ExtractProcessor, ImageProcessor, OptionsBag, _empty
+
+
+def decode(blob: bytes) -> np.ndarray:
+    """Encoded bytes -> HWC uint8 (RGB, or RGBA when the file has alpha),
+    EXIF orientation applied (-auto-orient)."""
+    from PIL import Image, ImageOps
+
+    im = Image.open(io.BytesIO(blob))
+    im = ImageOps.exif_transpose(im)
+    alpha = im.mode in ("RGBA", "LA", "PA") or (im.mode == "P" and "transparency" in im.info)
+    im = im.convert("RGBA" if alpha else "RGB")
+    return np.asarray(im)
+
+
+def encode(pixels: np.ndarray, quality: int = 90) -> bytes:
+    from PIL import Image
+
+    buf = io.BytesIO()
+    ch = pixels.shape[2] if pixels.ndim == 3 else 1
+    if ch in (2, 4):  # alpha survives: PNG
+        Image.fromarray(pixels, "LA" if ch == 2 else "RGBA").save(buf, "PNG")
+    else:
+        Image.fromarray(pixels, "L" if ch == 1 else "RGB").save(buf, "JPEG", quality=int(quality))
+    return buf.getvalue()
+
+
+class CodecPipeline:
+    """Batches of encoded images through decode -> GPU -> encode."""
+
+    def __init__(self, ctx, threads: int = 16):
+        self.ctx = ctx
+        self.pool = ThreadPoolExecutor(max_workers=max(1, threads))
+
+    def close(self):
+        self.pool.shutdown()
+
+    def process(self, blobs: list[bytes], options: list[str]):
+        """Returns (encoded outputs, fi_image records); a failed image raises
+        ExecFailedException as Processor::execute does."""
+        pixels = list(self.pool.map(decode, blobs))
+        srcs, ops, quality = [], [], []
+        for img, opts in zip(pixels, options):
+            bag = OptionsBag(opts)
+            img = ExtractProcessor.extract(bag, img)
+            h, w = img.shape[:2]
+            q = bag.get_option("quality")
+            quality.append(int(q) if not _empty(q) else 90)
+            ops.append(ImageProcessor(bag, w, h).to_op())
+            srcs.append(np.ascontiguousarray(img))
+        outs, recs, rc = self.ctx.process(srcs, ops)
+        for i, r in enumerate(recs):
+            if r.status != L.FI_OK:
+                msg = L.lib().fi_last_error()
+                raise ExecFailedException("Command failed.\nThe exit code: %d\n%s" % (
+                    r.status, msg.decode() if msg else f"image {i}"))
+        encoded = list(self.pool.map(lambda a: encode(a[0], a[1]), zip(outs, quality)))
+        return encoded, recs

@@ -609,3 +609,60 @@ def test_convolve_then_smartcrop(ctx):
     L.check(rc)
     t = orc.sc_crop(outs[0], 100, 100)["top_crop"]
     assert (recs[0].crop_x, recs[0].crop_y, recs[0].crop_w, recs[0].crop_h) == (t["x"], t["y"], t["width"], t["height"])
+
+
+# ---------------------------------------------------------------------------
+# Host codec pipeline (flyimg_amd/codec.py): encoded in -> encoded out
+def test_codec_pipeline_end_to_end(ctx):
+    """JPEG -> decode -> GPU (w_500,smc_1) -> JPEG q90: the decoded result has
+    the record's dims and stays within JPEG noise of the oracle run on the
+    same decoded source."""
+    import io
+
+    from PIL import Image
+
+    from flyimg_amd.codec import CodecPipeline, decode, encode
+
+    src = synth_rgb(1920, 1080, 21)
+    buf = io.BytesIO()
+    Image.fromarray(src).save(buf, "JPEG", quality=95)
+    pipe = CodecPipeline(ctx, threads=4)
+    try:
+        outs, recs = pipe.process([buf.getvalue()] * 3, ["w_500,smc_1,q_90"] * 3)
+    finally:
+        pipe.close()
+    dec = decode(buf.getvalue())
+    ref = orc.im_convert(dec, 500, 0, orc.FLAG_THUMBNAIL | orc.FLAG_SHRINK)
+    t = orc.sc_crop(ref, 100, 100)["top_crop"]
+    for o, r in zip(outs, recs):
+        assert (r.crop_x, r.crop_y, r.crop_w, r.crop_h) == (t["x"], t["y"], t["width"], t["height"])
+        got = decode(o)
+        assert got.shape == (r.out_h, r.out_w, 3)
+        ow, oh = min(t["width"] + t["x"], 500 - t["x"]), min(t["height"] + t["y"], 281 - t["y"])
+        want = ref[t["y"]:t["y"] + oh, t["x"]:t["x"] + ow]
+        assert got.shape == want.shape
+        # the same JPEG q90 round trip of the oracle's pixels (within +-1 LSB of ours)
+        want_j = decode(encode(np.ascontiguousarray(want), 90))
+        assert np.abs(got.astype(np.int16) - want_j.astype(np.int16)).mean() < 0.5
+
+
+def test_codec_pipeline_auto_orient(ctx):
+    """-auto-orient (ImageProcessor.php:78): EXIF orientation 6 is applied
+    before the geometry."""
+    import io
+
+    from PIL import Image
+
+    from flyimg_amd.codec import CodecPipeline
+
+    im = Image.fromarray(synth_rgb(400, 200, 3))
+    exif = Image.Exif()
+    exif[0x0112] = 6  # rotate 90 CW on display
+    buf = io.BytesIO()
+    im.save(buf, "JPEG", quality=95, exif=exif)
+    pipe = CodecPipeline(ctx, threads=2)
+    try:
+        outs, recs = pipe.process([buf.getvalue()], ["w_100"])
+    finally:
+        pipe.close()
+    assert (recs[0].out_w, recs[0].out_h) == (100, 200)
