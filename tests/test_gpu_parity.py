@@ -666,3 +666,51 @@ def test_codec_pipeline_auto_orient(ctx):
     finally:
         pipe.close()
     assert (recs[0].out_w, recs[0].out_h) == (100, 200)
+
+
+def test_mixed_batch_every_path_one_call(ctx):
+    """One fi_process_batch with images on every route at once -- streaming
+    MFMA (RGB V-first), generic H-first, RGBA matte passes, convolutions
+    (Q16 epilogue + fi_conv.hip), smart-crop apply, extract view, -monochrome
+    -- each within +-1 LSB of the oracle (bit-exact where the route is)."""
+    from flyimg_amd.processor import ExtractProcessor, ImageProcessor, OptionsBag
+
+    cases = [
+        (synth_rgb(1920, 1080, 1), "w_500"),                       # vm
+        (synth_rgb(900, 300, 2), "w_120"),                         # H-first generic
+        (_rgba(640, 480, 3), "w_150,h_150,c_1,r_180"),             # RGBA
+        (synth_rgb(900, 600, 4), "w_300,h_200,c_1,r_270,clsp_Gray,sh_3"),  # conv, gray, rotate
+        (synth_rgb(1280, 720, 5), "w_500,blr_1x2"),                # conv
+        (synth_rgb(1600, 900, 6), "e_1,p1x_17,p1y_9,p2x_1217,p2y_809,w_400"),  # extract view
+        (synth_rgb(800, 600, 7), "w_200,mnchr_1"),                 # monochrome
+    ]
+    srcs, ops, views = [], [], []
+    for src, opts in cases:
+        bag = OptionsBag(opts)
+        v = np.ascontiguousarray(ExtractProcessor.extract(bag, src))
+        op = ImageProcessor(bag, v.shape[1], v.shape[0]).to_op()
+        srcs.append(v)
+        ops.append(op)
+    outs, recs, rc = ctx.process(srcs, ops)
+    L.check(rc)
+    for (src, opts), v, op, out in zip(cases, srcs, ops, outs):
+        flags = 0
+        for f, o in ((L.FI_OP_THUMBNAIL, orc.FLAG_THUMBNAIL), (L.FI_GEOM_FILL, orc.FLAG_FILL),
+                     (L.FI_GEOM_SHRINK_ONLY, orc.FLAG_SHRINK), (L.FI_OP_EXTENT, orc.FLAG_EXTENT),
+                     (L.FI_OP_GRAY, orc.FLAG_GRAY), (L.FI_OP_ROTATE, orc.FLAG_ROTATE),
+                     (L.FI_OP_MONOCHROME, orc.FLAG_MONO)):
+            if op.flags & f:
+                flags |= o
+        ops_c = (1 if op.flags & L.FI_OP_UNSHARP else 0) | (2 if op.flags & L.FI_OP_SHARPEN else 0) | \
+                (4 if op.flags & L.FI_OP_BLUR else 0)
+        ref = orc.im_convert(v, op.target_w, op.target_h, flags, op.gravity, op.rotate,
+                             conv=tuple(op.unsharp) + tuple(op.sharpen) + tuple(op.blur), conv_ops=ops_c)
+        assert out.shape == ref.shape, opts
+        d = np.abs(out.astype(np.int16) - ref.astype(np.int16))
+        if op.flags & L.FI_OP_MONOCHROME:
+            # the error diffusion is chaotic in its +-1 LSB input: its invariants
+            # (as test_monochrome_pipeline_resized)
+            assert set(np.unique(out)) <= {0, 255}
+            assert abs(out.mean() - ref.mean()) / 255 < 0.01, opts
+        else:
+            assert d.max() <= 1, (opts, d.max())
