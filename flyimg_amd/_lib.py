@@ -11,7 +11,7 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libflyimg_hip.so")
+LIB_PATH = os.environ.get("FI_LIB_PATH") or os.path.join(HERE, "libflyimg_hip.so")  # override: A/B of two builds
 HEADER = os.path.join(os.path.dirname(HERE), "include", "flyimg_hip.h")
 
 FI_OK = 0
