@@ -245,6 +245,36 @@ def test_resize_within_one_lsb_of_oracle(rctx, case):
     _cmp(outs[0], ref, name)
 
 
+EDGE_CASES = [
+    # (name, W, H, target_w, target_h, flags, rotate): degenerate and extreme geometries
+    ("1x1_identity", 1, 1, 1, 0, F.FI_OP_THUMBNAIL | F.FI_GEOM_SHRINK_ONLY, 0),
+    ("2x2_enlarge", 2, 2, 7, 0, F.FI_OP_THUMBNAIL, 0),
+    ("thin_row", 2000, 3, 100, 0, F.FI_OP_THUMBNAIL | F.FI_GEOM_SHRINK_ONLY, 0),
+    ("thin_col", 3, 2000, 0, 100, F.FI_OP_THUMBNAIL | F.FI_GEOM_SHRINK_ONLY, 0),
+    ("primes", 997, 709, 211, 0, F.FI_OP_THUMBNAIL | F.FI_GEOM_SHRINK_ONLY, 0),
+    ("tiny_extent", 50, 40, 7, 5, F.FI_OP_THUMBNAIL | F.FI_GEOM_FILL | F.FI_OP_EXTENT, 0),
+    ("odd_gray_rot90", 641, 479, 123, 77, F.FI_OP_THUMBNAIL | F.FI_GEOM_FILL | F.FI_OP_EXTENT | F.FI_OP_GRAY |
+     F.FI_OP_ROTATE, 90),
+    ("factor_0.01_no_sample", 6000, 400, 60, 0, F.FI_OP_THUMBNAIL | F.FI_GEOM_SHRINK_ONLY, 0),
+    ("resize_wide_taps", 4000, 300, 90, 0, F.FI_OP_RESIZE | F.FI_GEOM_SHRINK_ONLY, 0),
+]
+
+
+@pytest.mark.parametrize("case", EDGE_CASES, ids=[c[0] for c in EDGE_CASES])
+def test_resize_edge_geometries(rctx, case):
+    """Degenerate sizes (1x1, 1-pixel-high outputs, tiny extents), prime
+    dimensions and very wide tap windows (factor 0.01 without the sample
+    pre-step: ~600 taps) on every kernel path: +-1 LSB of the oracle."""
+    name, W, H, tw, th, flags, rot = case
+    src = synth_rgb(W, H, 77 + W + H)
+    outs, recs, rc = rctx.process([src], [Op(tw, th, flags, L.GRAVITY["Center"], rot)])
+    assert rc == 0 and recs[0].status == 0, L.lib().fi_last_error()
+    ref = orc.im_convert(src, tw, th, _oracle_flags(flags), rotate=rot)
+    out = outs[0]
+    assert out.shape == ref.shape, (out.shape, ref.shape)
+    assert np.abs(out.astype(np.int16) - ref.astype(np.int16)).max() <= 1
+
+
 def test_mixed_batch_one_call(rctx):
     ctx = rctx
     imgs, ops, refs = [], [], []
