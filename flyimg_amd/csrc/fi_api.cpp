@@ -74,6 +74,12 @@ int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTi
               const int32_t *ai, size_t lds);
 int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
                  const int32_t *ai, const float *af, int hw_pitch, int max_taps, int max_nbytes);
+// persistent streaming exact-integer MFMA resample (fi_vs.hip)
+size_t vs_lds_bytes(int vpitch_max);
+bool vs_strip_ok(int nocb, int ks);
+int vs_read_stamps(uint64_t *out, int slots);
+int launch_vs(hipStream_t s, int grid, const VsRec *recs, const int32_t *qbeg, int32_t *qcnt, const int32_t *ai,
+              int vpitch_max);
 }  // namespace fi
 
 using namespace fi;
@@ -187,6 +193,9 @@ struct fi_ctx {
   bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
   bool sc_vq = true;        // FI_DISABLE_SC_VQ=1: k_sc_vmaps (VALU vertical pass) instead of k_sc_vq
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
+  bool vs_rs = false;    // FI_VS_RS=1: k_rs_vs (persistent streaming MFMA resample) before k_rs_vm
+  int ncu = 256;         // compute units of the device (k_rs_vs grid)
+  std::map<const AxisTable *, VsV> vsv_cache;   // ok iff np > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
   // Device-resident table heaps: every per-geometry table (tap tables, MFMA
@@ -213,6 +222,8 @@ struct fi_ctx {
   std::map<const StripTab *, std::pair<int32_t, int32_t>> strip_at;
   std::map<const MfmaV *, std::array<int32_t, 5>> mv_at;
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
+  std::map<const VsV *, std::array<int32_t, 3>> vsv_at;  // rows, meta, afrag
+  std::map<const MfmaStrip *, int32_t> lanes_at;          // k_rs_vs lane table of a strip
   std::map<const MfmaH *, std::array<int32_t, 4>> mh_at;  // wsum, frag, s0, lut
   int32_t mono_wts_at = -1;
   bool heap_retry = false;
@@ -411,6 +422,8 @@ static void heap_reset(fi_ctx *c) {
   c->strip_at.clear();
   c->mv_at.clear();
   c->vv_at.clear();
+  c->vsv_at.clear();
+  c->lanes_at.clear();
   c->mh_at.clear();
   c->mono_wts_at = -1;
 }
@@ -427,6 +440,7 @@ static int heap_prepare(fi_ctx *c, Exec &E) {
     c->mv_cache.clear();
     c->mh_cache.clear();
     c->vmv_cache.clear();
+    c->vsv_cache.clear();
     c->vmh_cache.clear();
     c->sc_cache.clear();
     c->imp_cache.clear();
@@ -946,6 +960,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   int h_tile_taps = 0;         // k_rs_h_tile: max horizontal window over the mode-2 images
   std::vector<const VmV *> vm_v;
   std::vector<const MfmaH *> vm_h;
+  std::vector<int> vs_img;     // indices into rd (mode 6)
+  std::vector<const VsV *> vs_v;
+  std::vector<const MfmaH *> vs_h;
   // per image resized-buffer workspace offsets (for smartcrop-apply)
   std::vector<size_t> res_off(n, 0);
   // final 8-bit output of each image (dst or the apply workspace, tagged); differs
@@ -1055,20 +1072,16 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         add_axis_f64(c, E, vt, &d.v);
         add_axis_f64(c, E, ht, &d.h);
       }
-      if (fast_ok && !P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
-          (im.src_stride % 16) == 0) {
-        auto vit = c->vmv_cache.find(vt);
-        if (vit == c->vmv_cache.end()) {
-          VmV m;
-          if (!build_vm_v(*vt, &m)) m = VmV();
-          vit = c->vmv_cache.emplace(vt, std::move(m)).first;
-        }
-        // the Q16 output tile (gray / rotation) needs more LDS than the 8-bit one
-        const bool q16 = P.gray || P.rot != 0;
+      const VsV *sv = nullptr;
+      const MfmaH *sh = nullptr;
+      const bool aligned16 = ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0;
+      // the Q16 output tile (gray / rotation) needs more LDS than the 8-bit one
+      const bool q16 = P.gray || P.rot != 0;
+      auto strips_of = [&]() -> const MfmaH * {
         auto hit = c->vmh_cache.find({ht, q16});
         if (hit == c->vmh_cache.end()) {
           // strips of <= 64 px; narrower when the horizontal fragments would not
-          // leave room for two workgroups per CU
+          // leave room for two k_rs_vm workgroups per CU
           MfmaH m;
           static const int first_nx = getenv("FI_VM_MAXNX") ? atoi(getenv("FI_VM_MAXNX")) : kVmMaxNx;  // tuning
           for (int mx : {first_nx, 48, 32}) {
@@ -1083,12 +1096,42 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           }
           hit = c->vmh_cache.emplace(std::make_pair(ht, q16), std::move(m)).first;
         }
-        if (vit->second.nblk > 0 && !hit->second.strips.empty()) {
-          vv = &vit->second;
-          vh = &hit->second;
+        return hit->second.strips.empty() ? nullptr : &hit->second;
+      };
+      if (fast_ok && !P.hfirst && c->fused && c->vs_rs && !c->mfma_rs && aligned16 && (int64_t)P.H * im.src_stride < ((int64_t)1 << 31)) {
+        auto vit = c->vsv_cache.find(vt);
+        if (vit == c->vsv_cache.end()) {
+          VsV m;
+          if (!build_vs_v(*vt, &m)) m = VsV();
+          vit = c->vsv_cache.emplace(vt, std::move(m)).first;
+        }
+        const MfmaH *hh = vit->second.np > 0 ? strips_of() : nullptr;
+        int vpm = 0;
+        bool sok = hh != nullptr;
+        if (hh)
+          for (const MfmaStrip &st : hh->strips) {
+            vpm = std::max(vpm, st.vpitch);
+            sok = sok && vs_strip_ok(st.nocb, st.ks);
+          }
+        if (sok && vs_lds_bytes(vpm) <= kVsMaxLds) {
+          sv = &vit->second;
+          sh = hh;
         }
       }
-      if (fast_ok && !vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
+      if (!sv && fast_ok && !P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && aligned16) {
+        auto vit = c->vmv_cache.find(vt);
+        if (vit == c->vmv_cache.end()) {
+          VmV m;
+          if (!build_vm_v(*vt, &m)) m = VmV();
+          vit = c->vmv_cache.emplace(vt, std::move(m)).first;
+        }
+        const MfmaH *hh = strips_of();
+        if (vit->second.nblk > 0 && hh) {
+          vv = &vit->second;
+          vh = hh;
+        }
+      }
+      if (fast_ok && !sv && !vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0) {
         auto vit = c->mv_cache.find(vt);
         if (vit == c->mv_cache.end()) {
@@ -1108,7 +1151,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         }
       }
       const RingTable *ring = nullptr;
-      if (fast_ok && !vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
+      if (fast_ok && !sv && !vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0 && d.h.maxtaps <= 64) {
         auto rit = c->ring_cache.find(vt);
         if (rit == c->ring_cache.end()) {
@@ -1131,7 +1174,13 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         else
           strips = &sit->second;
       }
-      if (vv) {
+      if (sv) {
+        d.mode = 6;  // persistent streaming exact-integer MFMA, vertical first
+        vs_img.push_back((int)rd.size());
+        vs_v.push_back(sv);
+        vs_h.push_back(sh);
+        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
+      } else if (vv) {
         d.mode = 5;  // streaming exact-integer MFMA, vertical first
         vm_img.push_back((int)rd.size());
         vm_v.push_back(vv);
@@ -1203,15 +1252,15 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           h_tile_taps = std::max(h_tile_taps, (int)d.h.maxtaps);
         }
       }
-      if (d.mode != 3 && d.mode != 4 && d.mode != 5) {
+      if (d.mode < 3) {
         d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
         src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * P.C;
       }
     }
     resize_bytes += (double)src_bytes + (double)need;
     {
-      static const char *kPath[6] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_mfma",
-                                     "path_vm"};
+      static const char *kPath[7] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_mfma",
+                                     "path_vm", "path_vs"};
       c->stats[kPath[d.mode]].launches += 1;  // images per resample path (fi_kernel_stats)
     }
     rd_of[i] = (int)rd.size();
@@ -1643,11 +1692,105 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       for (int x = 0; x < 8; x++)
         if (i < q8[x].size()) vtiles.push_back(q8[x][i]);
   }
+  // persistent streaming work (k_rs_vs): one flat record per item (image, strip,
+  // band), in 8 per-XCD queues (all strips of an image in one queue)
+  std::vector<VsRec> srecs;
+  std::vector<int32_t> sqbeg(9, 0);
+  int vs_vpitch = 0;
+  {
+    auto align4 = [&]() {
+      while (E.ai.size() % 4) E.ai.push_back(0);
+    };
+    auto put = [&](const std::vector<int32_t> &v) {
+      const int32_t o = E.oi();
+      E.ai.insert(E.ai.end(), v.begin(), v.end());
+      return o;
+    };
+    std::vector<std::vector<VsRec>> q8(8);
+    int64_t nst = 0;
+    for (size_t q = 0; q < vs_img.size(); q++) nst += (int64_t)vs_h[q]->strips.size();
+    for (size_t q = 0; q < vs_img.size(); q++) {
+      const ResizeDesc &d = rd[vs_img[q]];
+      const VsV &V = *vs_v[q];
+      const MfmaH &H = *vs_h[q];
+      auto vp = c->vsv_at.find(&V);
+      if (vp == c->vsv_at.end()) {
+        std::array<int32_t, 3> o;
+        o[0] = put(V.rows);
+        align4();
+        o[1] = put(V.meta);
+        align4();
+        o[2] = put(V.afrag);
+        vp = c->vsv_at.emplace(&V, o).first;
+      }
+      auto ht = c->mh_at.find(&H);
+      if (ht == c->mh_at.end()) {
+        std::array<int32_t, 4> o;
+        o[0] = put(H.wsum);
+        align4();
+        o[1] = put(H.frag);
+        o[2] = put(H.s0);
+        o[3] = put(H.lut);
+        ht = c->mh_at.emplace(&H, o).first;
+      }
+      const int32_t frag = ht->second[1], s0 = ht->second[2];
+      VsRec base{};
+      base.src_stride = (int32_t)d.src_stride;
+      base.nrows = (int32_t)V.rows.size();
+      base.rows = vp->second[0];
+      base.afrag = vp->second[2];
+      base.ew = d.ew;
+      base.eh = d.eh;
+      base.gray = d.gray;
+      base.rot = d.rot;
+      base.dst_stride = (int32_t)d.dst_stride;
+      base.dst = d.dst;
+      // bands of blocks only when the batch is too small to fill the chip
+      int bands = nst > 0 ? (int)((2048 + nst - 1) / nst) : 1;
+      bands = std::max(1, std::min(bands, V.nblk));
+      for (int bnd = 0; bnd < bands; bnd++) {
+        const int b0 = (int)((int64_t)V.nblk * bnd / bands), b1 = (int)((int64_t)V.nblk * (bnd + 1) / bands);
+        if (b1 <= b0) continue;
+        for (const MfmaStrip &st : H.strips) {
+          auto lt = c->lanes_at.find(&st);
+          if (lt == c->lanes_at.end()) {
+            std::vector<int32_t> tab;
+            vs_lane_table(H, st, &tab);
+            align4();
+            lt = c->lanes_at.emplace(&st, put(tab)).first;
+          }
+          VsRec r = base;
+          r.src = d.src + st.b0;
+          r.nbytes = st.nbytes;
+          r.p0 = V.L[b0] / 64;
+          r.p1 = (V.R[b1 - 1] - 1) / 64 + 1;
+          r.emit0 = b0;
+          r.emit1 = b1;
+          r.lanes = lt->second;
+          r.frag = frag + (int32_t)st.frag;
+          r.s0 = s0 + (int32_t)st.s0;
+          r.ks = st.ks;
+          r.nocb = st.nocb;
+          r.vpitch = st.vpitch;
+          r.x0 = st.x0;
+          r.nx = st.x1 - st.x0;
+          q8[q % 8].push_back(r);
+          vs_vpitch = std::max(vs_vpitch, st.vpitch);
+        }
+      }
+    }
+    for (int x = 0; x < 8; x++) {
+      sqbeg[x] = (int32_t)srecs.size();
+      srecs.insert(srecs.end(), q8[x].begin(), q8[x].end());
+    }
+    sqbeg[8] = (int32_t)srecs.size();
+  }
   const double t_tiles = now_ms();
   Blob &B = E.blob;
   const size_t all_rd_off = B.addv(rd);
   const size_t mdesc_off = B.addv(mdescs), mstrip_off = B.addv(mstrips), mtile_off = B.addv(mtiles);
   const size_t vdesc_off = B.addv(vdescs), vstrip_off = B.addv(vstrips), vtile_off = B.addv(vtiles);
+  const size_t srec_off = B.addv(srecs), sqbeg_off = B.addv(sqbeg), sqcnt_off = B.addv(std::vector<int32_t>(8, 0));
   for (auto &g : fgroups) g.second.off = B.addv(g.second.tiles);
   auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
   auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
@@ -1753,6 +1896,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       if (L0.tiles)
         hipLaunchKernelGGL(k_rs_copy, dim3(L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L0),
                            pre_p(L0), L0.n);
+      if (!srecs.empty() &&
+          launch_vs(c->stream, std::min<int>(c->ncu, (int)srecs.size()), (const VsRec *)(ab + srec_off),
+                    (const int32_t *)(ab + sqbeg_off), (int32_t *)(ab + sqcnt_off), ai, vs_vpitch) != 0)
+        return set_err(FI_EDEVICE, "persistent streaming resample launch rejected (vpitch %d)", vs_vpitch);
       if (!vtiles.empty() &&
           launch_vm(c->stream, (const VDesc *)(ab + vdesc_off), (const MStrip *)(ab + vstrip_off),
                     (const VTile *)(ab + vtile_off), (int)vtiles.size(), ai, vm_lds) != 0)
@@ -2028,6 +2175,12 @@ extern "C" {
 
 int32_t fi_abi_version(void) { return FI_ABI_VERSION; }
 // profiling only (not in the public header): k_rs_vm MODE 9 phase sums, 8 u64 per workgroup
+int fi_debug_vs_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
+  if (!c || !out) return FI_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return vs_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
+}
 int fi_debug_vm_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   if (!c || !out) return FI_EINVAL;
   HIP_TRY(hipSetDevice(c->device));
@@ -2190,9 +2343,11 @@ int fi_create(fi_ctx **out, int32_t device) {
     return set_err(FI_EDEVICE, "device %d is %s; libflyimg_hip.so is built for gfx950 only", device, prop.gcnArchName);
   fi_ctx *c = new fi_ctx();
   c->device = device;
+  c->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
   if (const char *e = getenv("FI_ENABLE_MFMA_RS")) c->mfma_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
+  if (const char *e = getenv("FI_VS_RS")) c->vs_rs = e[0] == '1';
   if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
   if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');

@@ -222,6 +222,46 @@ constexpr int kVmOtileBytes = 16 * kVmOtilePitch * 2;
 constexpr int kVmOtile8Pitch = 64 * 3 + 4;     // 8-bit tile row (fast RGB path)
 constexpr int kVmOtile8Bytes = 16 * kVmOtile8Pitch;
 
+// k_rs_vs (fi_vs.hip): persistent streaming exact-integer MFMA resample,
+// vertical first.  One workgroup per CU: kVsThreads / 64 waves x (32 / waves)
+// column tiles of 16 B = 512-B strips (MStrip, shared with k_rs_vm).  Source pieces (64
+// rows x 512 B) and their A-fragment records arrive by LDS-DMA in a 3-deep
+// ring; work items come from per-XCD queues.
+constexpr int kVsThreads = 1024;
+constexpr int kVsSlots = 3;              // accumulator slots (blocks touched by one piece)
+constexpr int kVsMaxComp = 2;            // blocks completing at one piece
+constexpr int kVsRing = 3;               // A-record ring depth (pieces)
+constexpr int kVsDataRing = 2;           // source-piece ring depth: a piece's B operands go to registers first
+constexpr int kVsPieceBytes = 64 * 512;
+constexpr int kVsAFragBytes = 10 * 1024;  // per piece: 9 fragments + w128 rows
+constexpr int kVsW128 = 9 * 256;          // int32 offset of the w128 rows in the record
+constexpr int kVsMeta = kVsW128 + 48;     // int32 offset of the piece meta {bf, nb, comp, rows}
+constexpr int kVsRecRing = 8;             // LDS ring of item records
+constexpr int kVsCtlBytes = kVsRecRing * 128 + 2 * 256;  // + 2 row tables of 64 source rows
+constexpr int kVsHfBytes = 4 * 2 * 3 * 1024;  // the item's horizontal B fragments [ob][t][limb] (nocb <= 4, ks <= 2)
+constexpr int kVsPlaneOff = kVsDataRing * kVsPieceBytes + kVsRing * kVsAFragBytes + kVsCtlBytes + kVsHfBytes;
+constexpr int kVsMaxLds = 160 * 1024;
+// One work item of k_rs_vs -- (image, strip, pieces [p0, p1)), emitting blocks
+// [emit0, emit1) -- flattened with its image's and strip's fields, so the
+// kernel fetches one 128-byte record per item (no dependent descriptor loads).
+struct VsRec {
+  // issue cursor (words 0-8)
+  const uint8_t *src;   // image source + the strip's first byte
+  int32_t src_stride, nbytes;
+  int32_t nrows, rows, afrag, p0;    // touched-row list (ai offset; rows[k]); piece records (ai offset); pieces
+  int32_t p1;
+  // item entry (words 9-13)
+  int32_t lanes, frag, s0;           // lane table / strip B fragments / (w0, ks) pairs (ai offsets)
+  int32_t ks, nocb;                  // strip: k-steps, 16-px output blocks
+  // block phase and stores (words 14-25)
+  int32_t vpitch, emit0;             // plane columns; emitted blocks [emit0, emit1)
+  int32_t emit1, x0, nx, ew;         // first output px of the strip, its px; extent width
+  int32_t eh, gray, rot, dst_stride; // dst_stride < 2^31
+  uint8_t *dst;
+  int32_t pad[6];
+};
+static_assert(sizeof(VsRec) == 128, "VsRec is one 128-byte record");
+
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;
   double saturation_bias, saturation_brightness_max, saturation_brightness_min,

@@ -619,6 +619,110 @@ bool build_vm_v(const AxisTable &v, VmV *m) {
   return true;
 }
 
+bool build_vs_v(const AxisTable &v, VsV *m) {
+  *m = VsV();
+  const int ny = (int)v.start.size();
+  if (ny == 0) return false;
+  std::vector<int32_t> idx;
+  touched_list(v, &m->rows, &idx);
+  const int nl = (int)m->rows.size();
+  if (nl == 0) return false;
+  m->nblk = (ny + 15) / 16;
+  m->L.assign(m->nblk, 0);
+  m->R.assign(m->nblk, 0);
+  for (int b = 0; b < m->nblk; b++) {
+    int lo = 1 << 30, hi = -1;
+    for (int y = 16 * b; y < std::min(ny, 16 * b + 16); y++) {
+      int a, e;
+      tap_range(v, idx, y, &a, &e);
+      if (e < a) return false;  // an output row without taps
+      lo = std::min(lo, a);
+      hi = std::max(hi, e);
+    }
+    m->L[b] = lo;
+    m->R[b] = hi + 1;
+    if (b > 0 && (m->L[b] < m->L[b - 1] || m->R[b] < m->R[b - 1])) return false;  // not monotone
+  }
+  m->np = (nl + 63) / 64;
+  m->meta.assign((size_t)m->np * 4, 0);
+  constexpr int kRec = kVsAFragBytes / 4;
+  m->afrag.assign((size_t)m->np * kRec, 0);
+  int bf = 0;
+  for (int p = 0; p < m->np; p++) {
+    const int s = 64 * p, e = std::min(s + 64, nl);
+    while (bf < m->nblk && m->R[bf] <= s) bf++;
+    int nb = 0, comp = 0;
+    while (bf + nb < m->nblk && m->L[bf + nb] < e) nb++;
+    while (bf + comp < m->nblk && m->R[bf + comp] <= e) comp++;
+    if (nb < 1 || nb > kVsSlots || comp > kVsMaxComp || comp > nb) return false;
+    int32_t *mt = &m->meta[(size_t)4 * p];
+    mt[0] = bf;
+    mt[1] = nb;
+    mt[2] = comp;
+    mt[3] = e - s;
+    int32_t *rec = &m->afrag[(size_t)p * kRec];
+    for (int k = 0; k < 4; k++) rec[kVsMeta + k] = mt[k];
+    for (int sl = 0; sl < kVsSlots; sl++) {
+      const int b = bf + sl;
+      if (b >= m->nblk) break;
+      for (int r = 0; r < 16; r++) {
+        const int y = 16 * b + r;
+        int32_t w = 0;
+        if (y < ny)
+          for (int j = 0; j < v.count[y]; j++) w += 128 * quant_w(v.w[v.woff[y] + j]);
+        rec[kVsW128 + 16 * sl + r] = w;
+      }
+      if (sl >= nb) continue;
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int y = 16 * b + (l & 15), li = s + mfma_i8_k(l, j);
+          int32_t limb[3];
+          limbs3(y < ny && li < e ? tap_w(v, m->rows, y, li) : 0, limb);
+          for (int q = 0; q < 3; q++)
+            reinterpret_cast<uint8_t *>(rec + (size_t)(sl * 3 + q) * 256)[l * 16 + j] = (uint8_t)(int8_t)limb[q];
+        }
+    }
+  }
+  // every tap lies in a piece whose slot window holds its block
+  for (int y = 0; y < ny; y++) {
+    const int b = y / 16;
+    for (int j = 0; j < v.count[y]; j++) {
+      if (v.w[v.woff[y] + j] == 0.0f) continue;
+      const int li = idx[v.start[y] + j - v.src_lo], p = li / 64;
+      const int32_t *mt = &m->meta[(size_t)4 * p];
+      if (b < mt[0] || b >= mt[0] + mt[1]) return false;
+    }
+  }
+  m->row0 = m->rows[0];
+  m->rstep = nl > 1 ? m->rows[1] - m->rows[0] : 1;
+  for (int k = 1; k < nl && m->rstep > 0; k++)
+    if (m->rows[k] != m->row0 + m->rstep * k) m->rstep = 0;
+  return true;
+}
+
+void vs_lane_table(const MfmaH &h, const MfmaStrip &st, std::vector<int32_t> *out) {
+  constexpr int waves = kVsThreads / 64, tiles = 32 / waves, items = (12 + waves - 1) / waves;
+  out->assign((size_t)kVsThreads * 4, 0);
+  const int plane = 16 * st.vpitch, nx = st.x1 - st.x0;
+  auto col_off = [](int ci) { return (ci * 16) ^ (((ci >> 4) & 1) << 7); };
+  for (int tid = 0; tid < kVsThreads; tid++) {
+    const int w = tid >> 6, l = tid & 63;
+    for (int j = 0; j < tiles; j++) {
+      const int col = 16 * tiles * w + 16 * j + (l & 15);
+      const int ab = st.b0 + std::min(col, st.nbytes - 1), px = ab / 3, chn = ab - 3 * px;
+      const int ci = h.lut[st.lut + (px - st.lut_px0)];
+      const uint32_t o = (col < st.nbytes && ci >= 0) ? (uint32_t)(chn * plane + col_off(ci) + 4 * (l >> 4)) : 0xFFFFu;
+      (*out)[4 * tid + (j >> 1)] |= (int32_t)(o << (16 * (j & 1)));
+    }
+    for (int k = 0; k < items; k++) {
+      float hws = 0.0f;
+      const int it = w + waves * k, ob = it / 3, hx = 16 * ob + (l & 15);
+      if (it < 3 * st.nocb && hx < nx) hws = 32896.0f * (float)h.wsum[st.x0 + hx];
+      memcpy(&(*out)[4 * tid + 2 + k], &hws, 4);
+    }
+  }
+}
+
 bool build_ring(const AxisTable &v, RingTable *rt) {
   *rt = RingTable();
   const int ny = (int)v.start.size();

@@ -116,6 +116,29 @@ struct VmV {
 };
 bool build_vm_v(const AxisTable &v, VmV *m);
 
+// Streaming vertical tables of k_rs_vs (fi_vs.hip).  The touched-row list is
+// cut into uniform pieces of 64 rows (the last one shorter).  Block b's taps
+// span list rows [L(b), R(b)); a piece touches the blocks whose windows
+// intersect it -- at most kVsSlots consecutive ones, bf .. bf + nb - 1 -- and
+// completes those with R(b) inside it (at most kVsMaxComp).  Per piece one
+// kVsAFragBytes record: the A fragments [slot][limb] (256 int32 each, zero for
+// slots >= nb), at int32 offset kVsW128 128 * sum of the quantized weights
+// of each row of blocks bf .. bf + 2 ([slot][16]), at kVsMeta the piece meta.
+struct VsV {
+  std::vector<int32_t> rows;           // touched source rows, ascending
+  int nblk = 0, np = 0;                // 16-row output blocks; pieces
+  std::vector<int32_t> L, R;           // [nblk] block windows in list rows
+  std::vector<int32_t> meta;           // [np][4]: bf, nb, comp, rows in the piece
+  std::vector<int32_t> afrag;          // [np][kVsAFragBytes / 4]
+  int32_t row0 = 0, rstep = 0;         // rstep > 0: rows[k] == row0 + rstep * k
+};
+bool build_vs_v(const AxisTable &v, VsV *m);
+// Per-lane constants of k_rs_vs for one strip (512 lanes x 4 int32): the Q16
+// plane offsets of the lane's four column tiles (16 bits each, 0xFFFF = column
+// not needed) and, per horizontal item of its wave (wave, wave + 8), the f32
+// bits of 32896 * (horizontal weight sum) of the lane's output pixel.
+void vs_lane_table(const MfmaH &h, const MfmaStrip &st, std::vector<int32_t> *out);
+
 // Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)
 // to `out_size`; taps mapped back to the `in_src` source indices through the
 // SampleImage offsets (identity when !sample) and merged.

@@ -138,6 +138,67 @@ static void check_vm(const AxisTable &v, const char *name) {
   printf("  %s: streaming vertical %d blocks, %d pieces, rstep %d ok\n", name, m.nblk, np, m.rstep);
 }
 
+// k_rs_vs: stream the uniform 64-row pieces with three rotating slots exactly
+// as the kernel does (new slots start at the record's w128 rows, completed
+// slots retire from the bottom) and compare every completed block.
+static void check_vs(const AxisTable &v, const char *name) {
+  VsV m;
+  if (!build_vs_v(v, &m)) {
+    printf("  %s: persistent streaming tables not built, skipped\n", name);
+    CHECK(!g_required, "%s: persistent streaming tables required", name);
+    return;
+  }
+  const int ny = (int)v.start.size();
+  const int nl = (int)m.rows.size();
+  constexpr int kRec = kVsAFragBytes / 4;
+  CHECK(m.np == (nl + 63) / 64, "%s: piece count", name);
+  std::mt19937 rng(777);
+  std::vector<int> px(v.src_hi);
+  for (auto &x : px) x = (int)(rng() & 255);
+  std::vector<int64_t> acc[kVsSlots];
+  for (auto &a : acc) a.assign(16, 0);
+  int live = 0, done = 0, max_nb = 0, max_comp = 0;
+  for (int p = 0; p < m.np; p++) {
+    const int32_t *mt = &m.meta[(size_t)4 * p];
+    const int bf = mt[0], nb = mt[1], comp = mt[2], nrows = mt[3];
+    max_nb = std::max(max_nb, nb);
+    max_comp = std::max(max_comp, comp);
+    CHECK(bf == done, "%s: piece %d starts at block %d, %d done", name, p, bf, done);
+    CHECK(nrows == std::min(64, nl - 64 * p), "%s: piece rows", name);
+    const int32_t *rec = &m.afrag[(size_t)p * kRec];
+    for (int s = live; s < nb; s++)
+      for (int r = 0; r < 16; r++) acc[s][r] = rec[kVsW128 + 16 * s + r];
+    for (int s = 0; s < nb; s++)
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int k = mfma_i8_k(l, j);
+          const int64_t w = limb_w(m.afrag, (size_t)p * kRec + (size_t)s * 3 * 256, l, j);
+          if (k >= nrows) {
+            CHECK(w == 0, "%s: weight past the piece", name);
+            continue;
+          }
+          acc[s][l & 15] += w * (px[m.rows[64 * p + k]] - 128);
+        }
+    for (int c = 0; c < comp; c++) {
+      const int b = bf + c;
+      for (int r = 0; r < 16; r++) {
+        const int y = 16 * b + r;
+        if (y >= ny) continue;
+        int64_t ref = 0;
+        for (int j = 0; j < v.count[y]; j++) ref += (int64_t)qw(v.w[v.woff[y] + j]) * px[v.start[y] + j];
+        CHECK(acc[c][r] == ref, "%s: vs vertical y=%d %lld != %lld", name, y, (long long)acc[c][r], (long long)ref);
+        CHECK(llabs(acc[c][r]) < (1ll << 31), "%s: accumulator exceeds int32", name);
+      }
+      done++;
+    }
+    for (int s = 0; s + comp < kVsSlots; s++) acc[s] = acc[s + comp];
+    live = nb - comp;
+  }
+  CHECK(done == m.nblk, "%s: %d of %d blocks completed", name, done, m.nblk);
+  printf("  %s: persistent streaming %d blocks, %d pieces, max slots %d, max completions %d, rstep %d ok\n", name,
+         m.nblk, m.np, max_nb, max_comp, m.rstep);
+}
+
 static void check_h(const AxisTable &h, const char *name) {
   MfmaH m;
   if (!build_mfma_h(h, &m)) {
@@ -263,6 +324,7 @@ static void geometry(int W, int H, int tw, int th, uint32_t flags, const char *n
   check_v(v, name);
   check_h(h, name);
   check_vm(v, name);
+  check_vs(v, name);
 }
 
 int main() {
@@ -277,6 +339,10 @@ int main() {
   geometry(300, 200, 150, 100, T | S, "300x200 -> 150");
   geometry(900, 600, 250, 300, FI_OP_RESIZE | F | X, "resize 900x600 250x300");
   geometry(120, 90, 300, 0, T, "enlarge 120x90 -> 300");
+  geometry(1000, 600, 0, 300, T | S, "h_300 on 1000x600 (factor 2)");
+  geometry(4000, 3000, 0, 300, T | S, "h_300 on 4000x3000");
+  geometry(1600, 1200, 400, 400, T | F | X, "1600x1200 400x400 c_1");
+  geometry(6000, 400, 60, 0, T | S, "factor 0.01 no sample");
   check_pillow(500, 281, 100, 100, "smartcrop 500x281");
   check_pillow(400, 400, 100, 100, "smartcrop 400x400");
   check_pillow(512, 512, 100, 100, "smartcrop 512x512");
