@@ -76,6 +76,11 @@ int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile 
                  const int32_t *ai, const float *af, int hw_pitch, int max_taps, int max_nbytes);
 // persistent streaming exact-integer MFMA resample (fi_vs.hip)
 size_t vs_lds_bytes(int vpitch_max);
+// persistent row-ring block resample (fi_vb.hip)
+size_t vb_lds_bytes(int vpitch_max);
+bool vb_strip_ok(int nocb, int ks);
+int vb_read_stamps(uint64_t *out, int slots);
+int launch_vb(hipStream_t s, int grid, const VbRec *recs, const int32_t *nitem, const int32_t *ai, int vpitch_max);
 bool vs_strip_ok(int nocb, int ks);
 int vs_read_stamps(uint64_t *out, int slots);
 int launch_vs(hipStream_t s, int grid, const VsRec *recs, const int32_t *qbeg, int32_t *qcnt, const int32_t *ai,
@@ -196,6 +201,8 @@ struct fi_ctx {
   bool vs_rs = false;    // FI_VS_RS=1: k_rs_vs (persistent streaming MFMA resample) before k_rs_vm
   int ncu = 256;         // compute units of the device (k_rs_vs grid)
   std::map<const AxisTable *, VsV> vsv_cache;   // ok iff np > 0
+  bool vb_rs = false;    // FI_VB_RS=1: k_rs_vb (persistent row-ring block resample) first
+  std::map<const AxisTable *, VbV> vbv_cache;   // ok iff nblk > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
   // Device-resident table heaps: every per-geometry table (tap tables, MFMA
@@ -223,6 +230,7 @@ struct fi_ctx {
   std::map<const MfmaV *, std::array<int32_t, 5>> mv_at;
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
   std::map<const VsV *, std::array<int32_t, 3>> vsv_at;  // rows, meta, afrag
+  std::map<const VbV *, std::array<int32_t, 2>> vbv_at;  // rows, block records
   std::map<const MfmaStrip *, int32_t> lanes_at;          // k_rs_vs lane table of a strip
   std::map<const MfmaH *, std::array<int32_t, 4>> mh_at;  // wsum, frag, s0, lut
   int32_t mono_wts_at = -1;
@@ -423,6 +431,7 @@ static void heap_reset(fi_ctx *c) {
   c->mv_at.clear();
   c->vv_at.clear();
   c->vsv_at.clear();
+  c->vbv_at.clear();
   c->lanes_at.clear();
   c->mh_at.clear();
   c->mono_wts_at = -1;
@@ -441,6 +450,7 @@ static int heap_prepare(fi_ctx *c, Exec &E) {
     c->mh_cache.clear();
     c->vmv_cache.clear();
     c->vsv_cache.clear();
+    c->vbv_cache.clear();
     c->vmh_cache.clear();
     c->sc_cache.clear();
     c->imp_cache.clear();
@@ -960,6 +970,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   int h_tile_taps = 0;         // k_rs_h_tile: max horizontal window over the mode-2 images
   std::vector<const VmV *> vm_v;
   std::vector<const MfmaH *> vm_h;
+  std::vector<int> vb_img;     // indices into rd (mode 7)
+  std::vector<const VbV *> vb_v;
+  std::vector<const MfmaH *> vb_h;
   std::vector<int> vs_img;     // indices into rd (mode 6)
   std::vector<const VsV *> vs_v;
   std::vector<const MfmaH *> vs_h;
@@ -1098,7 +1111,30 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         }
         return hit->second.strips.empty() ? nullptr : &hit->second;
       };
-      if (fast_ok && !P.hfirst && c->fused && c->vs_rs && !c->mfma_rs && aligned16 && (int64_t)P.H * im.src_stride < ((int64_t)1 << 31)) {
+      const VbV *bv = nullptr;
+      const MfmaH *bh = nullptr;
+      if (fast_ok && !P.hfirst && c->fused && c->vb_rs && !c->mfma_rs && aligned16 &&
+          (int64_t)P.H * im.src_stride < ((int64_t)1 << 31)) {
+        auto vit = c->vbv_cache.find(vt);
+        if (vit == c->vbv_cache.end()) {
+          VbV m;
+          if (!build_vb_v(*vt, &m)) m = VbV();
+          vit = c->vbv_cache.emplace(vt, std::move(m)).first;
+        }
+        const MfmaH *hh = vit->second.nblk > 0 ? strips_of() : nullptr;
+        int vpm = 0;
+        bool sok = hh != nullptr;
+        if (hh)
+          for (const MfmaStrip &st : hh->strips) {
+            vpm = std::max(vpm, st.vpitch);
+            sok = sok && vb_strip_ok(st.nocb, st.ks);
+          }
+        if (sok && vb_lds_bytes(vpm) <= kVbMaxLds) {
+          bv = &vit->second;
+          bh = hh;
+        }
+      }
+      if (!bv && fast_ok && !P.hfirst && c->fused && c->vs_rs && !c->mfma_rs && aligned16 && (int64_t)P.H * im.src_stride < ((int64_t)1 << 31)) {
         auto vit = c->vsv_cache.find(vt);
         if (vit == c->vsv_cache.end()) {
           VsV m;
@@ -1118,7 +1154,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           sh = hh;
         }
       }
-      if (!sv && fast_ok && !P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && aligned16) {
+      if (!bv && !sv && fast_ok && !P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && aligned16) {
         auto vit = c->vmv_cache.find(vt);
         if (vit == c->vmv_cache.end()) {
           VmV m;
@@ -1131,7 +1167,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
           vh = hh;
         }
       }
-      if (fast_ok && !sv && !vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
+      if (fast_ok && !bv && !sv && !vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0) {
         auto vit = c->mv_cache.find(vt);
         if (vit == c->mv_cache.end()) {
@@ -1151,7 +1187,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         }
       }
       const RingTable *ring = nullptr;
-      if (fast_ok && !sv && !vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
+      if (fast_ok && !bv && !sv && !vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
           (im.src_stride % 16) == 0 && d.h.maxtaps <= 64) {
         auto rit = c->ring_cache.find(vt);
         if (rit == c->ring_cache.end()) {
@@ -1174,7 +1210,13 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
         else
           strips = &sit->second;
       }
-      if (sv) {
+      if (bv) {
+        d.mode = 7;  // persistent row-ring block resample, vertical first
+        vb_img.push_back((int)rd.size());
+        vb_v.push_back(bv);
+        vb_h.push_back(bh);
+        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
+      } else if (sv) {
         d.mode = 6;  // persistent streaming exact-integer MFMA, vertical first
         vs_img.push_back((int)rd.size());
         vs_v.push_back(sv);
@@ -1259,8 +1301,8 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     }
     resize_bytes += (double)src_bytes + (double)need;
     {
-      static const char *kPath[7] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_mfma",
-                                     "path_vm", "path_vs"};
+      static const char *kPath[8] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_mfma",
+                                     "path_vm", "path_vs", "path_vb"};
       c->stats[kPath[d.mode]].launches += 1;  // images per resample path (fi_kernel_stats)
     }
     rd_of[i] = (int)rd.size();
@@ -1785,11 +1827,148 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     }
     sqbeg[8] = (int32_t)srecs.size();
   }
+  // persistent row-ring block resample (k_rs_vb): items (image, strip, band of
+  // blocks) as flat records, statically assigned to the workgroups: record
+  // k * G + g is workgroup g's k-th item (XCD-major within a round, LPT by cost)
+  std::vector<VbRec> brecs;
+  std::vector<int32_t> bcount;
+  int vb_vpitch = 0, vb_grid = 0;
+  {
+    auto align4 = [&]() {
+      while (E.ai.size() % 4) E.ai.push_back(0);
+    };
+    auto put = [&](const std::vector<int32_t> &v) {
+      const int32_t o = E.oi();
+      E.ai.insert(E.ai.end(), v.begin(), v.end());
+      return o;
+    };
+    std::vector<VbRec> items;
+    std::vector<int64_t> cost;
+    int64_t nst = 0;
+    for (size_t q = 0; q < vb_img.size(); q++) nst += (int64_t)vb_h[q]->strips.size();
+    for (size_t q = 0; q < vb_img.size(); q++) {
+      const ResizeDesc &d = rd[vb_img[q]];
+      const VbV &V = *vb_v[q];
+      const MfmaH &H = *vb_h[q];
+      auto vp = c->vbv_at.find(&V);
+      if (vp == c->vbv_at.end()) {
+        std::array<int32_t, 2> o;
+        o[0] = put(V.rows);
+        align4();
+        o[1] = put(V.arec);
+        vp = c->vbv_at.emplace(&V, o).first;
+      }
+      auto ht = c->mh_at.find(&H);
+      if (ht == c->mh_at.end()) {
+        std::array<int32_t, 4> o;
+        o[0] = put(H.wsum);
+        align4();
+        o[1] = put(H.frag);
+        o[2] = put(H.s0);
+        o[3] = put(H.lut);
+        ht = c->mh_at.emplace(&H, o).first;
+      }
+      VbRec base{};
+      base.src_stride = (int32_t)d.src_stride;
+      base.nrows = (int32_t)V.rows.size();
+      base.rows = vp->second[0];
+      base.arec = vp->second[1];
+      base.row0 = V.rows[0];
+      base.rstep = V.rows.size() > 1 ? V.rows[1] - V.rows[0] : 1;
+      for (size_t k = 1; k < V.rows.size() && base.rstep > 0; k++)
+        if (V.rows[k] != base.row0 + base.rstep * (int32_t)k) base.rstep = 0;
+      base.ew = d.ew;
+      base.eh = d.eh;
+      base.gray = d.gray;
+      base.rot = d.rot;
+      base.dst_stride = (int32_t)d.dst_stride;
+      base.dst = d.dst;
+      // bands of blocks only when the batch is too small to fill the chip
+      int bands = nst > 0 ? (int)((1024 + nst - 1) / nst) : 1;
+      bands = std::max(1, std::min(bands, V.nblk));
+      for (int bnd = 0; bnd < bands; bnd++) {
+        const int b0 = (int)((int64_t)V.nblk * bnd / bands), b1 = (int)((int64_t)V.nblk * (bnd + 1) / bands);
+        if (b1 <= b0) continue;
+        for (const MfmaStrip &st : H.strips) {
+          auto lt = c->lanes_at.find(&st);
+          if (lt == c->lanes_at.end()) {
+            std::vector<int32_t> tab;
+            vs_lane_table(H, st, &tab);
+            align4();
+            lt = c->lanes_at.emplace(&st, put(tab)).first;
+          }
+          VbRec r = base;
+          r.src = d.src + st.b0;
+          r.nbytes = st.nbytes;
+          r.b0 = b0;
+          r.b1 = b1;
+          r.g0 = V.K0[b0] / 32;
+          r.gend = (V.R[b1 - 1] - 1) / 32 + 1;
+          r.last0 = (V.R[b0] - 1) / 32 - r.g0;
+          r.lanes = lt->second;
+          r.frag = ht->second[1] + (int32_t)st.frag;
+          r.s0 = ht->second[2] + (int32_t)st.s0;
+          r.ks = st.ks;
+          r.nocb = st.nocb;
+          r.vpitch = st.vpitch;
+          r.x0 = st.x0;
+          r.nx = st.x1 - st.x0;
+          items.push_back(r);
+          cost.push_back((int64_t)(r.gend - r.g0) + (b1 - b0));  // groups streamed + blocks computed
+          vb_vpitch = std::max(vb_vpitch, st.vpitch);
+        }
+      }
+    }
+    const int ni = (int)items.size();
+    if (ni > 0) {
+      const int G = std::min(c->ncu, ni);
+      vb_grid = G;
+      std::vector<std::vector<int>> lists(G);
+      bool uniform = true;
+      for (int i = 1; i < ni && uniform; i++) uniform = cost[i] == cost[0];
+      if (uniform) {
+        // rounds of G consecutive items; within a full round XCD-major (items
+        // p, p + 1, ... of one image share an XCD's L2: workgroup g sits on XCD g % 8)
+        for (int k = 0; k * G < ni; k++) {
+          const int n = std::min(G, ni - k * G);
+          for (int p = 0; p < n; p++) {
+            const int g = (n == G && G % 8 == 0) ? (p % (G / 8)) * 8 + p / (G / 8) : p;
+            lists[g].push_back(k * G + p);
+          }
+        }
+      } else {
+        // longest-processing-time first onto the least-loaded workgroup
+        std::vector<int> order(ni);
+        for (int i = 0; i < ni; i++) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+        std::vector<std::pair<int64_t, int>> heap;
+        for (int g = 0; g < G; g++) heap.push_back({0, g});
+        auto cmp = [](const std::pair<int64_t, int> &a, const std::pair<int64_t, int> &b) { return a > b; };
+        std::make_heap(heap.begin(), heap.end(), cmp);
+        for (int i : order) {
+          std::pop_heap(heap.begin(), heap.end(), cmp);
+          auto &h = heap.back();
+          lists[h.second].push_back(i);
+          h.first += cost[i];
+          std::push_heap(heap.begin(), heap.end(), cmp);
+        }
+      }
+      size_t maxl = 0;
+      for (auto &l : lists) maxl = std::max(maxl, l.size());
+      brecs.assign(maxl * G, VbRec{});
+      bcount.assign(G, 0);
+      for (int g = 0; g < G; g++) {
+        bcount[g] = (int32_t)lists[g].size();
+        for (size_t k = 0; k < lists[g].size(); k++) brecs[k * G + g] = items[lists[g][k]];
+      }
+    }
+  }
   const double t_tiles = now_ms();
   Blob &B = E.blob;
   const size_t all_rd_off = B.addv(rd);
   const size_t mdesc_off = B.addv(mdescs), mstrip_off = B.addv(mstrips), mtile_off = B.addv(mtiles);
   const size_t vdesc_off = B.addv(vdescs), vstrip_off = B.addv(vstrips), vtile_off = B.addv(vtiles);
+  const size_t brec_off = B.addv(brecs), bcount_off = B.addv(bcount);
   const size_t srec_off = B.addv(srecs), sqbeg_off = B.addv(sqbeg), sqcnt_off = B.addv(std::vector<int32_t>(8, 0));
   for (auto &g : fgroups) g.second.off = B.addv(g.second.tiles);
   auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
@@ -1896,6 +2075,9 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       if (L0.tiles)
         hipLaunchKernelGGL(k_rs_copy, dim3(L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L0),
                            pre_p(L0), L0.n);
+      if (!brecs.empty() &&
+          launch_vb(c->stream, vb_grid, (const VbRec *)(ab + brec_off), (const int32_t *)(ab + bcount_off), ai, vb_vpitch) != 0)
+        return set_err(FI_EDEVICE, "row-ring block resample launch rejected (vpitch %d)", vb_vpitch);
       if (!srecs.empty() &&
           launch_vs(c->stream, std::min<int>(c->ncu, (int)srecs.size()), (const VsRec *)(ab + srec_off),
                     (const int32_t *)(ab + sqbeg_off), (int32_t *)(ab + sqcnt_off), ai, vs_vpitch) != 0)
@@ -2175,6 +2357,12 @@ extern "C" {
 
 int32_t fi_abi_version(void) { return FI_ABI_VERSION; }
 // profiling only (not in the public header): k_rs_vm MODE 9 phase sums, 8 u64 per workgroup
+int fi_debug_vb_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
+  if (!c || !out) return FI_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return vb_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
+}
 int fi_debug_vs_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   if (!c || !out) return FI_EINVAL;
   HIP_TRY(hipSetDevice(c->device));
@@ -2348,6 +2536,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_ENABLE_MFMA_RS")) c->mfma_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
   if (const char *e = getenv("FI_VS_RS")) c->vs_rs = e[0] == '1';
+  if (const char *e = getenv("FI_VB_RS")) c->vb_rs = e[0] == '1';
   if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
   if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');

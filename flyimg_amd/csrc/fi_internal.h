@@ -262,6 +262,41 @@ struct VsRec {
 };
 static_assert(sizeof(VsRec) == 128, "VsRec is one 128-byte record");
 
+// k_rs_vb (fi_vb.hip): persistent streaming exact-integer MFMA resample,
+// vertical first, one output block per iteration.  One 1024-thread workgroup
+// per CU (16 waves x 2 column tiles of 16 B = 512-B strips, MStrip); the
+// touched source rows stream through an LDS ring of kVbGroups groups of 32
+// rows (LDS-DMA, issued as far ahead as the ring allows).
+constexpr int kVbThreads = 1024;
+constexpr int kVbGroups = 6;                  // ring: 6 x 32 rows x 512 B = 96 KB
+constexpr int kVbGroupBytes = 32 * 512;
+constexpr int kVbABytes = 7 * 1024;           // per block: 6 fragments + w128 / meta
+constexpr int kVbW128 = 6 * 256;              // int32 offset of the w128 rows in the record
+constexpr int kVbMeta = kVbW128 + 16;         // int32 offset of {K0, ks, R}
+constexpr int kVbARing = 2;
+constexpr int kVbSinkBytes = 256;             // scratch bytes (MODE 1 ablation sink)
+constexpr int kVbHfBytes = 3 * 2 * 3 * 1024;  // the item's horizontal B fragments [ob][t][limb] (nocb <= 3, ks <= 2)
+constexpr int kVbMaxWindow = 112;             // rows a block may read: its groups stay within the ring's first 4
+constexpr int kVbPlaneOff = kVbGroups * kVbGroupBytes + kVbARing * kVbABytes + kVbSinkBytes + kVbHfBytes;
+constexpr int kVbMaxLds = 160 * 1024;
+// One work item: (image, strip, blocks [b0, b1)), flattened with its image's
+// and strip's fields (read with scalar loads).
+struct VbRec {
+  const uint8_t *src;   // image source + the strip's first byte
+  int32_t src_stride, nbytes;
+  int32_t nrows, rows, arec, b0;     // touched-row list (ai offset); block records (ai offset); blocks
+  int32_t b1, lanes, frag, s0;       // lane table / strip B fragments / (w0, ks) pairs (ai offsets)
+  int32_t ks, nocb, vpitch, x0;      // strip: k-steps, 16-px output blocks, plane columns, first output px
+  int32_t nx, ew, eh, gray;
+  int32_t rot, dst_stride;           // dst_stride < 2^31
+  uint8_t *dst;
+  int32_t g0, gend;                  // row groups (32 list rows) the item's blocks read: [g0, gend)
+  int32_t row0, rstep;               // rstep > 0: the touched-row list is row0 + rstep k (no table reads)
+  int32_t last0;                     // the first block's last window group, relative to g0
+  int32_t pad[3];
+};
+static_assert(sizeof(VbRec) == 128, "VbRec is one 128-byte record");
+
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;
   double saturation_bias, saturation_brightness_max, saturation_brightness_min,

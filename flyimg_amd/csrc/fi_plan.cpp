@@ -700,6 +700,59 @@ bool build_vs_v(const AxisTable &v, VsV *m) {
   return true;
 }
 
+bool build_vb_v(const AxisTable &v, VbV *m) {
+  *m = VbV();
+  const int ny = (int)v.start.size();
+  if (ny == 0) return false;
+  std::vector<int32_t> idx;
+  touched_list(v, &m->rows, &idx);
+  const int nl = (int)m->rows.size();
+  if (nl == 0) return false;
+  m->nblk = (ny + 15) / 16;
+  m->K0.assign(m->nblk, 0);
+  m->ks.assign(m->nblk, 0);
+  m->R.assign(m->nblk, 0);
+  constexpr int kRec = kVbABytes / 4;
+  m->arec.assign((size_t)m->nblk * kRec, 0);
+  for (int b = 0; b < m->nblk; b++) {
+    int lo = 1 << 30, hi = -1;
+    for (int y = 16 * b; y < std::min(ny, 16 * b + 16); y++) {
+      int a, e;
+      tap_range(v, idx, y, &a, &e);
+      if (e < a) return false;  // an output row without taps
+      lo = std::min(lo, a);
+      hi = std::max(hi, e);
+    }
+    const int K0 = lo / 16 * 16, ks = (hi + 1 - K0 + 63) / 64;
+    if (ks > 2 || hi + 1 - K0 > kVbMaxWindow) return false;
+    if (b > 0 && (K0 < m->K0[b - 1] || hi + 1 < m->R[b - 1])) return false;  // not monotone
+    m->K0[b] = K0;
+    m->ks[b] = ks;
+    m->R[b] = hi + 1;
+    int32_t *rec = &m->arec[(size_t)b * kRec];
+    for (int t = 0; t < ks; t++)
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int y = 16 * b + (l & 15), li = K0 + 64 * t + mfma_i8_k(l, j);
+          int32_t limb[3];
+          limbs3(y < ny && li < nl ? tap_w(v, m->rows, y, li) : 0, limb);
+          for (int q = 0; q < 3; q++)
+            reinterpret_cast<uint8_t *>(rec + (size_t)(t * 3 + q) * 256)[l * 16 + j] = (uint8_t)(int8_t)limb[q];
+        }
+    for (int r = 0; r < 16; r++) {
+      const int y = 16 * b + r;
+      int32_t w = 0;
+      if (y < ny)
+        for (int j = 0; j < v.count[y]; j++) w += 128 * quant_w(v.w[v.woff[y] + j]);
+      rec[kVbW128 + r] = w;
+    }
+    rec[kVbMeta + 0] = K0;
+    rec[kVbMeta + 1] = ks;
+    rec[kVbMeta + 2] = hi + 1;
+  }
+  return true;
+}
+
 void vs_lane_table(const MfmaH &h, const MfmaStrip &st, std::vector<int32_t> *out) {
   constexpr int waves = kVsThreads / 64, tiles = 32 / waves, items = (12 + waves - 1) / waves;
   out->assign((size_t)kVsThreads * 4, 0);

@@ -133,6 +133,20 @@ struct VsV {
   int32_t row0 = 0, rstep = 0;         // rstep > 0: rows[k] == row0 + rstep * k
 };
 bool build_vs_v(const AxisTable &v, VsV *m);
+// Block tables of k_rs_vb (fi_vb.hip).  Output block b (16 rows) is computed
+// in one pass over its tap window: list rows [K0(b), K0(b) + 64 ks(b)), K0 a
+// multiple of 16, ks <= 2 (window + alignment <= 128 rows).  Per block one
+// kVbABytes record: A fragments [t][limb] (256 int32 each) for list rows
+// K0 + 64 t + k, then at int32 offset kVbW128 the rows' 128 * sum of quantized
+// weights, at kVbMeta {K0, ks, R}.
+struct VbV {
+  std::vector<int32_t> rows;           // touched source rows, ascending
+  int nblk = 0;
+  std::vector<int32_t> K0, ks, R;      // [nblk]
+  std::vector<int32_t> arec;           // [nblk][kVbABytes / 4]
+};
+bool build_vb_v(const AxisTable &v, VbV *m);
+
 // Per-lane constants of k_rs_vs for one strip (512 lanes x 4 int32): the Q16
 // plane offsets of the lane's four column tiles (16 bits each, 0xFFFF = column
 // not needed) and, per horizontal item of its wave (wave, wave + 8), the f32

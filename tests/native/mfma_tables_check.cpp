@@ -199,6 +199,50 @@ static void check_vs(const AxisTable &v, const char *name) {
          m.nblk, m.np, max_nb, max_comp, m.rstep);
 }
 
+// k_rs_vb: each block in one pass over its window with separate limb sums
+static void check_vb(const AxisTable &v, const char *name) {
+  VbV m;
+  if (!build_vb_v(v, &m)) {
+    printf("  %s: block-window tables not built, skipped\n", name);
+    CHECK(!g_required, "%s: block-window tables required", name);
+    return;
+  }
+  const int ny = (int)v.start.size(), nl = (int)m.rows.size();
+  constexpr int kRec = kVbABytes / 4;
+  std::mt19937 rng(31337);
+  std::vector<int> px(v.src_hi);
+  for (auto &x : px) x = (int)(rng() & 255);
+  int maxw = 0;
+  for (int b = 0; b < m.nblk; b++) {
+    const int32_t *rec = &m.arec[(size_t)b * kRec];
+    CHECK(rec[kVbMeta] == m.K0[b] && rec[kVbMeta + 1] == m.ks[b] && m.K0[b] % 16 == 0, "%s: block meta", name);
+    maxw = std::max(maxw, m.R[b] - m.K0[b]);
+    for (int r = 0; r < 16; r++) {
+      const int y = 16 * b + r;
+      if (y >= ny) continue;
+      int64_t a[3] = {0, 0, 0};
+      for (int t = 0; t < m.ks[b]; t++)
+        for (int l = 0; l < 64; l++) {
+          if ((l & 15) != r) continue;
+          for (int j = 0; j < 16; j++) {
+            const int li = m.K0[b] + 64 * t + mfma_i8_k(l, j);
+            for (int q = 0; q < 3; q++) {
+              const int64_t w = frag_byte(m.arec, (size_t)b * kRec + (size_t)t * 3 * 256, q, l, j);
+              if (w && li >= nl) CHECK(false, "%s: weight past the list", name);
+              if (li < nl) a[q] += w * (px[m.rows[li]] - 128);
+            }
+          }
+        }
+      for (int q = 0; q < 3; q++) CHECK(llabs(a[q]) < (1ll << 31), "%s: limb sum exceeds int32", name);
+      const int64_t s = a[0] + 256 * a[1] + 65536 * a[2] + rec[kVbW128 + r];
+      int64_t ref = 0;
+      for (int j = 0; j < v.count[y]; j++) ref += (int64_t)qw(v.w[v.woff[y] + j]) * px[v.start[y] + j];
+      CHECK(s == ref, "%s: vb vertical y=%d %lld != %lld", name, y, (long long)s, (long long)ref);
+    }
+  }
+  printf("  %s: block windows %d blocks, max window %d rows ok\n", name, m.nblk, maxw);
+}
+
 static void check_h(const AxisTable &h, const char *name) {
   MfmaH m;
   if (!build_mfma_h(h, &m)) {
@@ -325,6 +369,7 @@ static void geometry(int W, int H, int tw, int th, uint32_t flags, const char *n
   check_h(h, name);
   check_vm(v, name);
   check_vs(v, name);
+  check_vb(v, name);
 }
 
 int main() {

@@ -45,8 +45,10 @@ def _context_with(env):
 
 
 _ENV = {"FI_DISABLE_FUSED": "0", "FI_ENABLE_MFMA_RS": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0",
-        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0", "FI_VS_RS": "0"}
+        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0", "FI_VS_RS": "0", "FI_VB_RS": "0"}
 PATHS = {
+    # k_rs_vb persistent row-ring block resample (LDS-DMA row ring, one block per iteration)
+    "vb": dict(_ENV, FI_VB_RS="1"),
     # k_rs_vs persistent streaming MFMA resample (LDS-DMA ring, per-XCD work queues)
     "vs": dict(_ENV, FI_VS_RS="1"),
     # default kernels: k_rs_vm streaming MFMA resample; k_sc_hmfma + k_sc_vq prescale; k_sc_score2
@@ -69,7 +71,7 @@ def rctx(request):
     c.close()
 
 
-EXPECTED_PATH = {"vs": "path_vs", "vm": "path_vm", "mfma": "path_mfma", "valu": "path_fused", "generic": "path_generic_v"}
+EXPECTED_PATH = {"vb": "path_vb", "vs": "path_vs", "vm": "path_vm", "mfma": "path_mfma", "valu": "path_fused", "generic": "path_generic_v"}
 
 
 @pytest.mark.parametrize("W,H,opts", [
