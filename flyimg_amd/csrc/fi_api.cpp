@@ -50,11 +50,6 @@ int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, in
                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P);
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
 __global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
-// fused vertical-first resample (fi_fused.hip)
-// exact-integer MFMA resample (fi_mfma.hip)
-size_t mfma_lds_bytes(int nblocks);
-int launch_mfma(hipStream_t s, const MDesc *descs, const MStrip *strips, const MTile *tiles, int ntiles,
-                const int32_t *ai, size_t lds);
 // tiled horizontal-first pass 1 (fi_kernels.hip)
 constexpr int kHTileRows = 16;  // fi_kernels.hip kHTRows
 size_t rs_h_tile_lds(int pitch, int taps);
@@ -72,19 +67,9 @@ size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16);
 int vm_read_stamps(uint64_t *out, int slots);
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
+// fused vertical-first VALU resample (fi_fused.hip)
 int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
                  const int32_t *ai, const float *af, int hw_pitch, int max_taps, int max_nbytes);
-// persistent streaming exact-integer MFMA resample (fi_vs.hip)
-size_t vs_lds_bytes(int vpitch_max);
-// persistent row-ring block resample (fi_vb.hip)
-size_t vb_lds_bytes(int vpitch_max);
-bool vb_strip_ok(int nocb, int ks);
-int vb_read_stamps(uint64_t *out, int slots);
-int launch_vb(hipStream_t s, int grid, const VbRec *recs, const int32_t *nitem, const int32_t *ai, int vpitch_max);
-bool vs_strip_ok(int nocb, int ks);
-int vs_read_stamps(uint64_t *out, int slots);
-int launch_vs(hipStream_t s, int grid, const VsRec *recs, const int32_t *qbeg, int32_t *qcnt, const int32_t *ai,
-              int vpitch_max);
 }  // namespace fi
 
 using namespace fi;
@@ -190,19 +175,11 @@ struct fi_ctx {
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
   std::map<const AxisTable *, RingTable> ring_cache;
   std::map<const AxisTable *, std::vector<StripTab>> strip_cache;
-  std::map<const AxisTable *, MfmaV> mv_cache;  // ok iff nyb > 0
-  std::map<const AxisTable *, MfmaH> mh_cache;  // ok iff !strips.empty()
   bool fused = true;    // FI_DISABLE_FUSED=1 forces the generic two-pass resample
-  bool mfma_rs = false;  // FI_ENABLE_MFMA_RS=1: k_rs_mfma instead of the VALU fused kernel
   bool vm_rs = true;     // FI_DISABLE_VM_RS=1: no k_rs_vm (streaming MFMA resample, the default)
   bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
   bool sc_vq = true;        // FI_DISABLE_SC_VQ=1: k_sc_vmaps (VALU vertical pass) instead of k_sc_vq
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
-  bool vs_rs = false;    // FI_VS_RS=1: k_rs_vs (persistent streaming MFMA resample) before k_rs_vm
-  int ncu = 256;         // compute units of the device (k_rs_vs grid)
-  std::map<const AxisTable *, VsV> vsv_cache;   // ok iff np > 0
-  bool vb_rs = false;    // FI_VB_RS=1: k_rs_vb (persistent row-ring block resample) first
-  std::map<const AxisTable *, VbV> vbv_cache;   // ok iff nblk > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
   // Device-resident table heaps: every per-geometry table (tap tables, MFMA
@@ -227,11 +204,7 @@ struct fi_ctx {
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_at;
   std::map<const RingTable *, std::array<int32_t, 4>> ring_at;
   std::map<const StripTab *, std::pair<int32_t, int32_t>> strip_at;
-  std::map<const MfmaV *, std::array<int32_t, 5>> mv_at;
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
-  std::map<const VsV *, std::array<int32_t, 3>> vsv_at;  // rows, meta, afrag
-  std::map<const VbV *, std::array<int32_t, 2>> vbv_at;  // rows, block records
-  std::map<const MfmaStrip *, int32_t> lanes_at;          // k_rs_vs lane table of a strip
   std::map<const MfmaH *, std::array<int32_t, 4>> mh_at;  // wsum, frag, s0, lut
   int32_t mono_wts_at = -1;
   bool heap_retry = false;
@@ -428,11 +401,7 @@ static void heap_reset(fi_ctx *c) {
   c->imp_at.clear();
   c->ring_at.clear();
   c->strip_at.clear();
-  c->mv_at.clear();
   c->vv_at.clear();
-  c->vsv_at.clear();
-  c->vbv_at.clear();
-  c->lanes_at.clear();
   c->mh_at.clear();
   c->mono_wts_at = -1;
 }
@@ -446,11 +415,7 @@ static int heap_prepare(fi_ctx *c, Exec &E) {
     c->axis_cache.clear();
     c->ring_cache.clear();
     c->strip_cache.clear();
-    c->mv_cache.clear();
-    c->mh_cache.clear();
     c->vmv_cache.clear();
-    c->vsv_cache.clear();
-    c->vbv_cache.clear();
     c->vmh_cache.clear();
     c->sc_cache.clear();
     c->imp_cache.clear();
@@ -939,444 +904,370 @@ static void host_stat(fi_ctx *c, const char *name, double ms) {
   s.launches += 1;
 }
 
-static int drain(fi_ctx *c);
-static int wait_slot(fi_ctx *c, int slot);
-static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
-  const double t_start = now_ms();
-  Exec E;
-  E.c = c;
-  fi_smartcrop_default_params(&E.params);
-  {
-    const int hrc = heap_prepare(c, E);
-    if (hrc) return hrc;
-  }
-  std::vector<ImPlan> plans(n);
-  std::vector<int> status(n, FI_OK);
-  std::vector<std::string> errs(n);
-  std::vector<ResizeDesc> rd;
-  std::vector<int> rd_of(n, -1);
-  std::vector<ScItem> sitems;
-  std::vector<int> sc_of(n, -1);
+// ---------------------------------------------------------------------------
+// batch pipeline.  run_batch strings the units together:
+//   plan_image (per image: geometry, descriptor, resample path + tables)
+//   -> plan_batch_sc (smartcrop stage) -> resolve_workspace (device pointers,
+//   -monochrome / convolution steps, crop apply) -> build_fused_tiles /
+//   build_vm_tiles -> pack_batch (one blob) -> launch_batch (both streams)
+//   -> queue_readback (pinned result records, the in-flight list).
+// ---------------------------------------------------------------------------
+struct MonoItem {
+  int img;
+  size_t g_off, st_off;
+};
+struct ConvItem {
+  int img;
+  size_t a_off, b_off;
+};
+struct FusedGroup {  // fused tiles of one ring size K
+  std::vector<FusedTile> tiles;
+  int pitch = 0, max_taps = 0, max_nbytes = 0;
+  size_t off = 0;
+};
+// Everything a batch plans before it is packed and uploaded.
+struct BatchPlan {
+  fi_image *imgs = nullptr;
+  int n = 0;
+  std::vector<ImPlan> plans;
+  std::vector<int> status;
+  std::vector<std::string> errs;
+  std::vector<ResizeDesc> rd;  // resample descriptors of the images that plan
+  std::vector<int> rd_of;      // image -> rd index (-1: the image failed)
+  std::vector<ScItem> sitems;  // smartcrop jobs
+  std::vector<int> sc_of;      // image -> sitems index (-1: none)
   std::map<const AxisTable *, DevAxis> placed;
+  // resample path members (indices into rd) and their tables
+  std::vector<int> fused_img;
   std::vector<const RingTable *> fused_ring;
-  std::vector<const AxisTable *> fused_h;
   std::vector<const std::vector<StripTab> *> fused_strips_of;
-  std::vector<int> fused_img;  // indices into rd
-  std::vector<int> mfma_img;   // indices into rd (mode 4)
-  std::vector<const MfmaV *> mfma_v;
-  std::vector<const MfmaH *> mfma_h;
-  std::vector<int> vm_img;     // indices into rd (mode 5)
-  int h_tile_pitch = 0;        // k_rs_h_tile: max staged row bytes over the mode-2 images
-  int h_tile_taps = 0;         // k_rs_h_tile: max horizontal window over the mode-2 images
+  std::vector<int> vm_img;
   std::vector<const VmV *> vm_v;
   std::vector<const MfmaH *> vm_h;
-  std::vector<int> vb_img;     // indices into rd (mode 7)
-  std::vector<const VbV *> vb_v;
-  std::vector<const MfmaH *> vb_h;
-  std::vector<int> vs_img;     // indices into rd (mode 6)
-  std::vector<const VsV *> vs_v;
-  std::vector<const MfmaH *> vs_h;
-  // per image resized-buffer workspace offsets (for smartcrop-apply)
-  std::vector<size_t> res_off(n, 0);
-  // final 8-bit output of each image (dst or the apply workspace, tagged); differs
-  // from its ResizeDesc dst only for -monochrome images (Q16 gray scratch)
-  std::vector<uint8_t *> out_of(n, nullptr);
-  struct MonoItem {
-    int img;
-    size_t g_off, st_off;
-  };
+  int h_tile_pitch = 0;  // k_rs_h_tile: max staged row bytes over the mode-2 images
+  int h_tile_taps = 0;   // k_rs_h_tile: max horizontal window over the mode-2 images
+  std::vector<size_t> res_off;    // per image: resized buffer in the workspace (smartcrop apply)
+  std::vector<uint8_t *> out_of;  // per image: the final 8-bit output (dst, or the workspace +1-tagged)
   std::vector<MonoItem> mono;
-  struct ConvItem {
-    int img;
-    size_t a_off, b_off;
-  };
   std::vector<ConvItem> conv_items;
   double resize_bytes = 0;
-  for (int i = 0; i < n; i++) {
-    fi_image &im = imgs[i];
-    int rc = plan_im(im, &plans[i]);
-    const ImPlan &P = plans[i];
-    if (rc != FI_OK) {
-      status[i] = rc;
-      errs[i] = P.err;
-      continue;
+  // smartcrop stage
+  ScLaunchData SL;
+  std::vector<int> sstatus;
+  std::vector<std::string> serrs;
+  size_t results_off = 0, scores_off = 0, outwh_off = 0;
+  // resolved against the slot's workspace
+  std::vector<MonoDesc> mdesc_mono;
+  std::vector<ConvStep> cst[6];  // U-H, U-V+combine, S-2D, B-H, B-V, to8
+  std::vector<ApplyDesc> apply;
+  // tiles
+  std::map<int, FusedGroup> fgroups;
+  std::vector<VDesc> vdescs;
+  std::vector<MStrip> vstrips;
+  std::vector<VTile> vtiles;
+  size_t vm_lds = 0;
+};
+// Blob offsets and launch lists of a packed batch.
+struct Packed {
+  size_t all_rd_off = 0, vdesc_off = 0, vstrip_off = 0, vtile_off = 0, apply_off = 0, mono_off = 0;
+  size_t ai_off = 0, af_off = 0, ad_off = 0, mono_wts = 0;
+  Launch L0, L1a, L2a, L2b, Q0, Q1a, Q2a, Q2b, CL[6];
+  bool h_tiled = false;
+  ScLaunches SX;
+};
+
+// The k_rs_vm column strips of a horizontal table: <= kVmMaxNx output px,
+// narrower when the strip's horizontal fragments would not leave room for two
+// workgroups per CU (nullptr: no strip width fits).
+static const MfmaH *vm_strips(fi_ctx *c, const AxisTable *ht, bool q16) {
+  auto hit = c->vmh_cache.find({ht, q16});
+  if (hit == c->vmh_cache.end()) {
+    MfmaH m;
+    static const int first_nx = getenv("FI_VM_MAXNX") ? atoi(getenv("FI_VM_MAXNX")) : kVmMaxNx;  // tuning
+    for (int mx : {first_nx, 48, 32}) {
+      if (!build_mfma_h(*ht, &m, mx)) {
+        m = MfmaH();
+        break;
+      }
+      bool fits = true;
+      for (const MfmaStrip &st : m.strips) fits = fits && vm_lds_bytes(st.vpitch, st.nocb, st.ks, q16) <= kVmMaxLds;
+      if (fits) break;
+      m = MfmaH();
     }
-    if (!im.src) {
-      status[i] = FI_EINVAL;
-      errs[i] = "src is NULL";
-      continue;
+    hit = c->vmh_cache.emplace(std::make_pair(ht, q16), std::move(m)).first;
+  }
+  return hit->second.strips.empty() ? nullptr : &hit->second;
+}
+
+// Choose the resample kernel of one image (d.mode) and add its tables:
+//   5  k_rs_vm: RGB, vertical first, 16-byte aligned rows (the default);
+//   3  k_rs_fused: the VALU ring kernel (FI_DISABLE_VM_RS=1, or vm tables
+//      that do not fit);
+//   1 / 2  the generic two-pass kernels, vertical / horizontal first (RGBA,
+//      -monochrome and convolution inputs, horizontal-first geometries).
+// Returns the algorithmic source bytes the path reads.
+static int64_t plan_resample(fi_ctx *c, Exec &E, BatchPlan &Bp, const ImPlan &P, const fi_image &im,
+                             ResizeDesc &d) {
+  const AxisTable *vt = add_axis(c, E, P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &d.v, Bp.placed);
+  const AxisTable *ht = add_axis(c, E, P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &d.h, Bp.placed);
+  const bool rgb = P.C == 3;
+  const bool fast_ok = rgb && !P.conv;  // the streaming / fused kernels write 8-bit only
+  if (!rgb) {
+    // matte (RGBA) images: the alpha-weighted f64 generic passes (k_rs4_*)
+    add_axis_f64(c, E, vt, &d.v);
+    add_axis_f64(c, E, ht, &d.h);
+  }
+  const bool aligned16 = ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0;
+  const int64_t strip_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
+  const bool vfirst_fast = fast_ok && !P.hfirst && c->fused && aligned16;
+  if (vfirst_fast && c->vm_rs) {
+    auto vit = c->vmv_cache.find(vt);
+    if (vit == c->vmv_cache.end()) {
+      VmV m;
+      if (!build_vm_v(*vt, &m)) m = VmV();
+      vit = c->vmv_cache.emplace(vt, std::move(m)).first;
     }
-    const bool smc = (im.flags & FI_OP_SMARTCROP) != 0;
-    const bool apply = smc && (im.flags & FI_OP_SMARTCROP_APPLY);
-    im.out_w = P.out_w;
-    im.out_h = P.out_h;
-    im.out_channels = P.out_c;
-    im.out_stride = P.out_w * P.out_c;
-    const int64_t need = (int64_t)im.out_stride * im.out_h;
-    if (!im.dst || im.dst_capacity < need) {
-      status[i] = FI_ECAPACITY;
-      errs[i] = "dst NULL or dst_capacity < out_stride*out_h";
-      continue;
-    }
-    ResizeDesc d{};
-    d.src = im.src;
-    d.src_stride = im.src_stride;
-    d.C = P.C;
-    const bool rgb = P.C == 3;
-    const bool fast_ok = rgb && !P.conv;  // the streaming / fused kernels write 8-bit only
-    d.ew = P.ew;
-    d.eh = P.eh;
-    d.ex0 = P.ex0;
-    d.ey0 = P.ey0;
-    d.gray = P.gray;
-    d.rot = P.rot;
-    d.out_w = P.out_w;
-    d.out_h = P.out_h;
-    d.out_c = P.out_c;
-    d.dst_stride = im.out_stride;
-    if (apply) {
-      res_off[i] = E.work.take((size_t)need);
-      d.dst = (uint8_t *)(uintptr_t)(res_off[i] + 1);  // workspace, fixed below
-    } else {
-      d.dst = im.dst;
-    }
-    out_of[i] = d.dst;
-    if (P.mono) {
-      // the resample epilogue writes the extent window's Q16 gray, unrotated;
-      // fi_mono.hip quantizes it and writes the rotated 0/255 output
-      MonoItem m;
-      m.img = i;
-      m.g_off = E.work.take((size_t)P.ew * P.eh * 2);
-      m.st_off = E.work.take(sizeof(MonoState));
-      mono.push_back(m);
-      d.dst = (uint8_t *)(uintptr_t)(m.g_off + 1);
-      d.dst_stride = (int64_t)P.ew * 2;
-      d.gray = 2;
-      d.rot = 0;
-    }
-    if (P.conv) {
-      // the epilogue writes the rotated Q16 image; the convolutions ping-pong
-      // between two such buffers and the last step writes the 8-bit output
-      ConvItem ci;
-      ci.img = i;
-      const size_t qb = (size_t)P.out_w * P.out_h * P.out_c * 2;
-      ci.a_off = E.work.take(qb);
-      ci.b_off = E.work.take(qb);
-      conv_items.push_back(ci);
-      d.dst = (uint8_t *)(uintptr_t)(ci.a_off + 1);
-      d.dst_stride = (int64_t)P.out_w * P.out_c * 2;
-      d.q16out = 1;
-    }
-    int64_t src_bytes = 0;
-    if (!P.resize) {
-      d.mode = 0;
-      src_bytes = (int64_t)P.ew * P.eh * P.C;
-    } else {
-      const AxisTable *vt =
-          add_axis(c, E, P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &d.v, placed);
-      const AxisTable *ht =
-          add_axis(c, E, P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &d.h, placed);
-      const MfmaV *mv = nullptr;
-      const MfmaH *mh = nullptr;
-      const VmV *vv = nullptr;
-      const MfmaH *vh = nullptr;
-      if (!rgb) {
-        // matte (RGBA) images: the alpha-weighted f64 generic passes (k_rs4_*)
-        add_axis_f64(c, E, vt, &d.v);
-        add_axis_f64(c, E, ht, &d.h);
-      }
-      const VsV *sv = nullptr;
-      const MfmaH *sh = nullptr;
-      const bool aligned16 = ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0;
-      // the Q16 output tile (gray / rotation) needs more LDS than the 8-bit one
-      const bool q16 = P.gray || P.rot != 0;
-      auto strips_of = [&]() -> const MfmaH * {
-        auto hit = c->vmh_cache.find({ht, q16});
-        if (hit == c->vmh_cache.end()) {
-          // strips of <= 64 px; narrower when the horizontal fragments would not
-          // leave room for two k_rs_vm workgroups per CU
-          MfmaH m;
-          static const int first_nx = getenv("FI_VM_MAXNX") ? atoi(getenv("FI_VM_MAXNX")) : kVmMaxNx;  // tuning
-          for (int mx : {first_nx, 48, 32}) {
-            if (!build_mfma_h(*ht, &m, mx)) {
-              m = MfmaH();
-              break;
-            }
-            bool fits = true;
-            for (const MfmaStrip &st : m.strips) fits = fits && vm_lds_bytes(st.vpitch, st.nocb, st.ks, q16) <= kVmMaxLds;
-            if (fits) break;
-            m = MfmaH();
-          }
-          hit = c->vmh_cache.emplace(std::make_pair(ht, q16), std::move(m)).first;
-        }
-        return hit->second.strips.empty() ? nullptr : &hit->second;
-      };
-      const VbV *bv = nullptr;
-      const MfmaH *bh = nullptr;
-      if (fast_ok && !P.hfirst && c->fused && c->vb_rs && !c->mfma_rs && aligned16 &&
-          (int64_t)P.H * im.src_stride < ((int64_t)1 << 31)) {
-        auto vit = c->vbv_cache.find(vt);
-        if (vit == c->vbv_cache.end()) {
-          VbV m;
-          if (!build_vb_v(*vt, &m)) m = VbV();
-          vit = c->vbv_cache.emplace(vt, std::move(m)).first;
-        }
-        const MfmaH *hh = vit->second.nblk > 0 ? strips_of() : nullptr;
-        int vpm = 0;
-        bool sok = hh != nullptr;
-        if (hh)
-          for (const MfmaStrip &st : hh->strips) {
-            vpm = std::max(vpm, st.vpitch);
-            sok = sok && vb_strip_ok(st.nocb, st.ks);
-          }
-        if (sok && vb_lds_bytes(vpm) <= kVbMaxLds) {
-          bv = &vit->second;
-          bh = hh;
-        }
-      }
-      if (!bv && fast_ok && !P.hfirst && c->fused && c->vs_rs && !c->mfma_rs && aligned16 && (int64_t)P.H * im.src_stride < ((int64_t)1 << 31)) {
-        auto vit = c->vsv_cache.find(vt);
-        if (vit == c->vsv_cache.end()) {
-          VsV m;
-          if (!build_vs_v(*vt, &m)) m = VsV();
-          vit = c->vsv_cache.emplace(vt, std::move(m)).first;
-        }
-        const MfmaH *hh = vit->second.np > 0 ? strips_of() : nullptr;
-        int vpm = 0;
-        bool sok = hh != nullptr;
-        if (hh)
-          for (const MfmaStrip &st : hh->strips) {
-            vpm = std::max(vpm, st.vpitch);
-            sok = sok && vs_strip_ok(st.nocb, st.ks);
-          }
-        if (sok && vs_lds_bytes(vpm) <= kVsMaxLds) {
-          sv = &vit->second;
-          sh = hh;
-        }
-      }
-      if (!bv && !sv && fast_ok && !P.hfirst && c->fused && c->vm_rs && !c->mfma_rs && aligned16) {
-        auto vit = c->vmv_cache.find(vt);
-        if (vit == c->vmv_cache.end()) {
-          VmV m;
-          if (!build_vm_v(*vt, &m)) m = VmV();
-          vit = c->vmv_cache.emplace(vt, std::move(m)).first;
-        }
-        const MfmaH *hh = strips_of();
-        if (vit->second.nblk > 0 && hh) {
-          vv = &vit->second;
-          vh = hh;
-        }
-      }
-      if (fast_ok && !bv && !sv && !vv && !P.mono && !P.hfirst && c->fused && c->mfma_rs && ((uintptr_t)im.src % 16) == 0 &&
-          (im.src_stride % 16) == 0) {
-        auto vit = c->mv_cache.find(vt);
-        if (vit == c->mv_cache.end()) {
-          MfmaV m;
-          if (!build_mfma_v(*vt, &m)) m = MfmaV();
-          vit = c->mv_cache.emplace(vt, std::move(m)).first;
-        }
-        auto hit = c->mh_cache.find(ht);
-        if (hit == c->mh_cache.end()) {
-          MfmaH m;
-          if (!build_mfma_h(*ht, &m)) m = MfmaH();
-          hit = c->mh_cache.emplace(ht, std::move(m)).first;
-        }
-        if (vit->second.nyb > 0 && !hit->second.strips.empty()) {
-          mv = &vit->second;
-          mh = &hit->second;
-        }
-      }
-      const RingTable *ring = nullptr;
-      if (fast_ok && !bv && !sv && !vv && !mv && !P.mono && !P.hfirst && c->fused && ((uintptr_t)im.src % 16) == 0 &&
-          (im.src_stride % 16) == 0 && d.h.maxtaps <= 64) {
-        auto rit = c->ring_cache.find(vt);
-        if (rit == c->ring_cache.end()) {
-          RingTable rt;
-          if (!build_ring(*vt, &rt)) rt.K = 0;
-          rit = c->ring_cache.emplace(vt, std::move(rt)).first;
-        }
-        if (rit->second.K && rit->second.K <= 8) ring = &rit->second;  // K=16 would spill
-      }
-      const std::vector<StripTab> *strips = nullptr;
-      if (ring) {
-        auto sit = c->strip_cache.find(ht);
-        if (sit == c->strip_cache.end()) {
-          std::vector<StripTab> st;
-          if (!fused_strips(*ht, P.ew, &st)) st.clear();
-          sit = c->strip_cache.emplace(ht, std::move(st)).first;
-        }
-        if (sit->second.empty())
-          ring = nullptr;
-        else
-          strips = &sit->second;
-      }
-      if (bv) {
-        d.mode = 7;  // persistent row-ring block resample, vertical first
-        vb_img.push_back((int)rd.size());
-        vb_v.push_back(bv);
-        vb_h.push_back(bh);
-        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
-      } else if (sv) {
-        d.mode = 6;  // persistent streaming exact-integer MFMA, vertical first
-        vs_img.push_back((int)rd.size());
-        vs_v.push_back(sv);
-        vs_h.push_back(sh);
-        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
-      } else if (vv) {
-        d.mode = 5;  // streaming exact-integer MFMA, vertical first
-        vm_img.push_back((int)rd.size());
-        vm_v.push_back(vv);
-        vm_h.push_back(vh);
-        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
-      } else if (mv) {
-        d.mode = 4;  // exact-integer MFMA, vertical first
-        mfma_img.push_back((int)rd.size());
-        mfma_v.push_back(mv);
-        mfma_h.push_back(mh);
-        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
-      } else if (ring) {
-        d.mode = 3;  // fused vertical-first
-        d.fused_k = ring->K;
-        d.ring_n = (int32_t)ring->rows.size();
-        auto pr = c->ring_at.find(ring);
-        if (pr == c->ring_at.end()) {
-          std::array<int32_t, 4> o;
-          o[0] = E.oi();
-          E.ai.insert(E.ai.end(), ring->rows.begin(), ring->rows.end());
-          o[1] = E.of();
-          E.af.insert(E.af.end(), ring->ringw.begin(), ring->ringw.end());
-          o[2] = E.oi();
-          E.ai.insert(E.ai.end(), ring->ringy.begin(), ring->ringy.end());
-          o[3] = E.oi();
-          E.ai.insert(E.ai.end(), ring->flush.begin(), ring->flush.end());
-          pr = c->ring_at.emplace(ring, o).first;
-        }
-        d.ring_rows = pr->second[0];
-        d.ring_w = pr->second[1];
-        d.ring_y = pr->second[2];
-        d.ring_flush = pr->second[3];
-        fused_ring.push_back(ring);
-        fused_h.push_back(ht);
-        fused_strips_of.push_back(strips);
-        fused_img.push_back((int)rd.size());
-        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
-      } else if (!rgb && !P.hfirst) {
-        d.mode = 1;  // RGBA: mid = [eh][source columns src_lo..src_hi) x 4 Q16
-        d.mid_c0 = d.h.src_lo;
-        d.mid_cols = d.h.src_hi - d.h.src_lo;
-        d.mid_rows = P.eh;
-        d.mid_stride = 4 * (int64_t)d.mid_cols;
-      } else if (!rgb) {
-        d.mode = 2;  // RGBA: mid = [source rows src_lo..src_hi][ew] x 4 Q16
-        d.mid_r0 = d.v.src_lo;
-        d.mid_rows = d.v.src_hi - d.v.src_lo;
-        d.mid_cols = P.ew;
-        d.mid_stride = 4 * (int64_t)P.ew;
-      } else if (!P.hfirst) {
-        d.mode = 1;
-        const int64_t b_lo = (int64_t)3 * d.h.src_lo / 8 * 8;
-        const int64_t b_hi = std::min<int64_t>((int64_t)3 * P.W, ((int64_t)3 * d.h.src_hi + 7) / 8 * 8);
-        d.mid_c0 = (int32_t)b_lo;
-        d.mid_cols = (int32_t)(b_hi - b_lo);
-        d.mid_rows = P.eh;
-        d.mid_stride = (d.mid_cols + 7) / 8 * 8;
-      } else {
-        d.mode = 2;
-        d.mid_r0 = d.v.src_lo;
-        d.mid_rows = d.v.src_hi - d.v.src_lo;
-        d.mid_cols = P.ew;
-        d.mid_stride = (3 * P.ew + 7) / 8 * 8;
-        // k_rs_h_tile LDS row pitch: the source bytes of a 256-column chunk's windows
-        for (int x0 = 0; x0 < P.ew; x0 += 256) {
-          const int x1 = std::min(P.ew, x0 + 256);
-          const int lo = ht->start[x0], hi = ht->start[x1 - 1] + ht->count[x1 - 1];
-          h_tile_pitch = std::max(h_tile_pitch, (3 * (hi - lo) + 8 + 15) / 16 * 16);
-          h_tile_taps = std::max(h_tile_taps, (int)d.h.maxtaps);
-        }
-      }
-      if (d.mode < 3) {
-        d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
-        src_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * P.C;
-      }
-    }
-    resize_bytes += (double)src_bytes + (double)need;
-    {
-      static const char *kPath[8] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_mfma",
-                                     "path_vm", "path_vs", "path_vb"};
-      c->stats[kPath[d.mode]].launches += 1;  // images per resample path (fi_kernel_stats)
-    }
-    rd_of[i] = (int)rd.size();
-    rd.push_back(d);
-    if (smc) {
-      ScItem it{};
-      it.img = (const uint8_t *)(uintptr_t)0;  // resolved after workspace allocation
-      it.stride = im.out_stride;
-      it.W = P.out_w;
-      it.H = P.out_h;
-      it.C = P.out_c;
-      it.tw = im.smartcrop_w > 0 ? im.smartcrop_w : 100;
-      it.th = im.smartcrop_h > 0 ? im.smartcrop_h : 100;
-      it.result = (int)sitems.size();
-      fi_smartcrop_default_options(&it.opt);
-      sc_of[i] = (int)sitems.size();
-      sitems.push_back(it);
-      (void)0;
+    // the Q16 output tile (gray / rotation) needs more LDS than the 8-bit one
+    const MfmaH *hh = vm_strips(c, ht, P.gray || P.rot != 0);
+    if (vit->second.nblk > 0 && hh) {
+      d.mode = 5;  // streaming exact-integer MFMA, vertical first
+      Bp.vm_img.push_back((int)Bp.rd.size());
+      Bp.vm_v.push_back(&vit->second);
+      Bp.vm_h.push_back(hh);
+      return strip_bytes;
     }
   }
-  const double t_images = now_ms();
-  // smartcrop planning
-  ScLaunchData SL;
-  std::vector<int> sstatus(sitems.size(), FI_OK);
-  std::vector<std::string> serrs(sitems.size());
-  for (int i = 0; i < n; i++)
-    if (sc_of[i] >= 0) {
-      // smartcrop input: the resized image (workspace if apply, else dst)
-      ScItem &it = sitems[sc_of[i]];
-      it.img = out_of[i];  // may still be a workspace offset (+1 tagged); fixed below
+  if (vfirst_fast && !P.mono && d.h.maxtaps <= 64) {
+    auto rit = c->ring_cache.find(vt);
+    if (rit == c->ring_cache.end()) {
+      RingTable rt;
+      if (!build_ring(*vt, &rt)) rt.K = 0;
+      rit = c->ring_cache.emplace(vt, std::move(rt)).first;
     }
-  plan_smartcrop(c, E, sitems, &SL, &sstatus, &serrs, false);
-  const size_t results_off = E.work.take(sizeof(ScResult) * std::max<size_t>(sitems.size(), 1));
-  const size_t scores_off = E.work.take(sizeof(CropScore) * std::max(SL.nscores, 1));
-  const size_t outwh_off = E.work.take(sizeof(int32_t) * 2 * std::max(n, 1));
-  // the batch's slot: pinned staging + device blob/workspace (the batch that
-  // used it last must be done before anything here is overwritten)
-  const int slot = c->next_slot;
-  int rc = wait_slot(c, slot);
-  if (rc) return rc;
-  Slot &S = c->slots[slot];
-  rc = ensure(c, &S.work, E.work.size + 256);
-  if (rc) return rc;
-  uint8_t *wb = (uint8_t *)S.work.p;
-  // resolve tagged workspace offsets
-  for (int i = 0; i < n; i++) {
-    if (rd_of[i] < 0) continue;
-    ResizeDesc &d = rd[rd_of[i]];
+    const RingTable *ring = (rit->second.K && rit->second.K <= 8) ? &rit->second : nullptr;  // K=16 would spill
+    const std::vector<StripTab> *strips = nullptr;
+    if (ring) {
+      auto sit = c->strip_cache.find(ht);
+      if (sit == c->strip_cache.end()) {
+        std::vector<StripTab> st;
+        if (!fused_strips(*ht, P.ew, &st)) st.clear();
+        sit = c->strip_cache.emplace(ht, std::move(st)).first;
+      }
+      if (!sit->second.empty()) strips = &sit->second;
+    }
+    if (strips) {
+      d.mode = 3;  // fused vertical-first
+      d.fused_k = ring->K;
+      d.ring_n = (int32_t)ring->rows.size();
+      auto pr = c->ring_at.find(ring);
+      if (pr == c->ring_at.end()) {
+        std::array<int32_t, 4> o;
+        o[0] = E.oi();
+        E.ai.insert(E.ai.end(), ring->rows.begin(), ring->rows.end());
+        o[1] = E.of();
+        E.af.insert(E.af.end(), ring->ringw.begin(), ring->ringw.end());
+        o[2] = E.oi();
+        E.ai.insert(E.ai.end(), ring->ringy.begin(), ring->ringy.end());
+        o[3] = E.oi();
+        E.ai.insert(E.ai.end(), ring->flush.begin(), ring->flush.end());
+        pr = c->ring_at.emplace(ring, o).first;
+      }
+      d.ring_rows = pr->second[0];
+      d.ring_w = pr->second[1];
+      d.ring_y = pr->second[2];
+      d.ring_flush = pr->second[3];
+      Bp.fused_ring.push_back(ring);
+      Bp.fused_strips_of.push_back(strips);
+      Bp.fused_img.push_back((int)Bp.rd.size());
+      return strip_bytes;
+    }
+  }
+  if (!rgb && !P.hfirst) {
+    d.mode = 1;  // RGBA: mid = [eh][source columns src_lo..src_hi) x 4 Q16
+    d.mid_c0 = d.h.src_lo;
+    d.mid_cols = d.h.src_hi - d.h.src_lo;
+    d.mid_rows = P.eh;
+    d.mid_stride = 4 * (int64_t)d.mid_cols;
+  } else if (!rgb) {
+    d.mode = 2;  // RGBA: mid = [source rows src_lo..src_hi][ew] x 4 Q16
+    d.mid_r0 = d.v.src_lo;
+    d.mid_rows = d.v.src_hi - d.v.src_lo;
+    d.mid_cols = P.ew;
+    d.mid_stride = 4 * (int64_t)P.ew;
+  } else if (!P.hfirst) {
+    d.mode = 1;
+    const int64_t b_lo = (int64_t)3 * d.h.src_lo / 8 * 8;
+    const int64_t b_hi = std::min<int64_t>((int64_t)3 * P.W, ((int64_t)3 * d.h.src_hi + 7) / 8 * 8);
+    d.mid_c0 = (int32_t)b_lo;
+    d.mid_cols = (int32_t)(b_hi - b_lo);
+    d.mid_rows = P.eh;
+    d.mid_stride = (d.mid_cols + 7) / 8 * 8;
+  } else {
+    d.mode = 2;
+    d.mid_r0 = d.v.src_lo;
+    d.mid_rows = d.v.src_hi - d.v.src_lo;
+    d.mid_cols = P.ew;
+    d.mid_stride = (3 * P.ew + 7) / 8 * 8;
+    // k_rs_h_tile LDS row pitch: the source bytes of a 256-column chunk's windows
+    for (int x0 = 0; x0 < P.ew; x0 += 256) {
+      const int x1 = std::min(P.ew, x0 + 256);
+      const int lo = ht->start[x0], hi = ht->start[x1 - 1] + ht->count[x1 - 1];
+      Bp.h_tile_pitch = std::max(Bp.h_tile_pitch, (3 * (hi - lo) + 8 + 15) / 16 * 16);
+      Bp.h_tile_taps = std::max(Bp.h_tile_taps, (int)d.h.maxtaps);
+    }
+  }
+  d.mid = (uint16_t *)(uintptr_t)(E.work.take((size_t)d.mid_stride * d.mid_rows * 2) + 1);
+  return (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * P.C;
+}
+
+// Plan image i: geometry (plan_im), output record, the resample descriptor
+// and its destination (dst, the apply / -monochrome / convolution workspace),
+// and its smartcrop job.  Failures go to the image's status.
+static void plan_image(fi_ctx *c, Exec &E, BatchPlan &Bp, int i) {
+  fi_image &im = Bp.imgs[i];
+  ImPlan &P = Bp.plans[i];
+  const int rc = plan_im(im, &P);
+  if (rc != FI_OK) {
+    Bp.status[i] = rc;
+    Bp.errs[i] = P.err;
+    return;
+  }
+  if (!im.src) {
+    Bp.status[i] = FI_EINVAL;
+    Bp.errs[i] = "src is NULL";
+    return;
+  }
+  const bool smc = (im.flags & FI_OP_SMARTCROP) != 0;
+  const bool apply = smc && (im.flags & FI_OP_SMARTCROP_APPLY);
+  im.out_w = P.out_w;
+  im.out_h = P.out_h;
+  im.out_channels = P.out_c;
+  im.out_stride = P.out_w * P.out_c;
+  const int64_t need = (int64_t)im.out_stride * im.out_h;
+  if (!im.dst || im.dst_capacity < need) {
+    Bp.status[i] = FI_ECAPACITY;
+    Bp.errs[i] = "dst NULL or dst_capacity < out_stride*out_h";
+    return;
+  }
+  ResizeDesc d{};
+  d.src = im.src;
+  d.src_stride = im.src_stride;
+  d.C = P.C;
+  d.ew = P.ew;
+  d.eh = P.eh;
+  d.ex0 = P.ex0;
+  d.ey0 = P.ey0;
+  d.gray = P.gray;
+  d.rot = P.rot;
+  d.out_w = P.out_w;
+  d.out_h = P.out_h;
+  d.out_c = P.out_c;
+  d.dst_stride = im.out_stride;
+  if (apply) {
+    Bp.res_off[i] = E.work.take((size_t)need);
+    d.dst = (uint8_t *)(uintptr_t)(Bp.res_off[i] + 1);  // workspace, resolved later
+  } else {
+    d.dst = im.dst;
+  }
+  Bp.out_of[i] = d.dst;
+  if (P.mono) {
+    // the resample epilogue writes the extent window's Q16 gray, unrotated;
+    // fi_mono.hip quantizes it and writes the rotated 0/255 output
+    MonoItem m;
+    m.img = i;
+    m.g_off = E.work.take((size_t)P.ew * P.eh * 2);
+    m.st_off = E.work.take(sizeof(MonoState));
+    Bp.mono.push_back(m);
+    d.dst = (uint8_t *)(uintptr_t)(m.g_off + 1);
+    d.dst_stride = (int64_t)P.ew * 2;
+    d.gray = 2;
+    d.rot = 0;
+  }
+  if (P.conv) {
+    // the epilogue writes the rotated Q16 image; the convolutions ping-pong
+    // between two such buffers and the last step writes the 8-bit output
+    ConvItem ci;
+    ci.img = i;
+    const size_t qb = (size_t)P.out_w * P.out_h * P.out_c * 2;
+    ci.a_off = E.work.take(qb);
+    ci.b_off = E.work.take(qb);
+    Bp.conv_items.push_back(ci);
+    d.dst = (uint8_t *)(uintptr_t)(ci.a_off + 1);
+    d.dst_stride = (int64_t)P.out_w * P.out_c * 2;
+    d.q16out = 1;
+  }
+  int64_t src_bytes;
+  if (!P.resize) {
+    d.mode = 0;
+    src_bytes = (int64_t)P.ew * P.eh * P.C;
+  } else {
+    src_bytes = plan_resample(c, E, Bp, P, im, d);
+  }
+  Bp.resize_bytes += (double)src_bytes + (double)need;
+  static const char *kPath[6] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_none",
+                                 "path_vm"};
+  c->stats[kPath[d.mode]].launches += 1;  // images per resample path (fi_kernel_stats)
+  Bp.rd_of[i] = (int)Bp.rd.size();
+  Bp.rd.push_back(d);
+  if (smc) {
+    ScItem it{};
+    it.img = nullptr;  // the resized image: resolved with the workspace
+    it.stride = im.out_stride;
+    it.W = P.out_w;
+    it.H = P.out_h;
+    it.C = P.out_c;
+    it.tw = im.smartcrop_w > 0 ? im.smartcrop_w : 100;
+    it.th = im.smartcrop_h > 0 ? im.smartcrop_h : 100;
+    it.result = (int)Bp.sitems.size();
+    fi_smartcrop_default_options(&it.opt);
+    Bp.sc_of[i] = (int)Bp.sitems.size();
+    Bp.sitems.push_back(it);
+  }
+}
+
+// The smartcrop stage of the batch: input = each image's resized output.
+static void plan_batch_sc(fi_ctx *c, Exec &E, BatchPlan &Bp) {
+  Bp.sstatus.assign(Bp.sitems.size(), FI_OK);
+  Bp.serrs.assign(Bp.sitems.size(), std::string());
+  for (int i = 0; i < Bp.n; i++)
+    if (Bp.sc_of[i] >= 0) Bp.sitems[Bp.sc_of[i]].img = Bp.out_of[i];  // may be +1-tagged workspace
+  plan_smartcrop(c, E, Bp.sitems, &Bp.SL, &Bp.sstatus, &Bp.serrs, false);
+  Bp.results_off = E.work.take(sizeof(ScResult) * std::max<size_t>(Bp.sitems.size(), 1));
+  Bp.scores_off = E.work.take(sizeof(CropScore) * std::max(Bp.SL.nscores, 1));
+  Bp.outwh_off = E.work.take(sizeof(int32_t) * 2 * std::max(Bp.n, 1));
+}
+
+// Resolve the +1-tagged workspace offsets against the slot's workspace wb and
+// build what needs device pointers: -monochrome descriptors, the forwarded
+// convolution steps (per image in IM's order: unsharp, sharpen, blur; one
+// launch per stage), the smartcrop descriptors' buffers and crop apply.
+static void resolve_workspace(Exec &E, BatchPlan &Bp, uint8_t *wb) {
+  fi_image *imgs = Bp.imgs;
+  for (int i = 0; i < Bp.n; i++) {
+    if (Bp.rd_of[i] < 0) continue;
+    ResizeDesc &d = Bp.rd[Bp.rd_of[i]];
     if (d.mid) fix_ptr(d.mid, wb);
     const bool apply = (imgs[i].flags & FI_OP_SMARTCROP) && (imgs[i].flags & FI_OP_SMARTCROP_APPLY);
-    if (apply) fix_ptr(out_of[i], wb);
+    if (apply) fix_ptr(Bp.out_of[i], wb);
     if (d.gray == 2 || d.q16out)
       fix_ptr(d.dst, wb);
     else
-      d.dst = out_of[i];
+      d.dst = Bp.out_of[i];
   }
-  std::vector<MonoDesc> mdesc_mono;
-  for (const MonoItem &m : mono) {
-    const ResizeDesc &d = rd[rd_of[m.img]];
+  for (const MonoItem &m : Bp.mono) {
+    const ResizeDesc &d = Bp.rd[Bp.rd_of[m.img]];
     MonoDesc md{};
     md.g = (const uint16_t *)(wb + m.g_off);
     md.w = d.ew;
     md.h = d.eh;
-    md.rot = plans[m.img].rot;
-    md.dst = out_of[m.img];
+    md.rot = Bp.plans[m.img].rot;
+    md.dst = Bp.out_of[m.img];
     md.dst_stride = imgs[m.img].out_stride;
     md.st = (MonoState *)(wb + m.st_off);
-    mdesc_mono.push_back(md);
+    Bp.mdesc_mono.push_back(md);
   }
-  // forwarded convolutions: per image, steps in IM's order (unsharp, sharpen,
-  // blur), grouped into one launch per stage
-  std::vector<ConvStep> cst[6];  // U-H, U-V+combine, S-2D, B-H, B-V, to8
-  for (const ConvItem &ci : conv_items) {
-    const ImPlan &P = plans[ci.img];
+  for (const ConvItem &ci : Bp.conv_items) {
+    const ImPlan &P = Bp.plans[ci.img];
     uint16_t *A = (uint16_t *)(wb + ci.a_off), *Bf = (uint16_t *)(wb + ci.b_off);
     uint16_t *cur = A, *oth = Bf;
     ConvStep base{};
@@ -1397,15 +1288,15 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       v.kw = 1, v.kh = w, v.in = oth, v.orig = cur, v.out = cur;
       v.gain = P.cv[2];
       v.thr = 65535.0 * P.cv[3];
-      cst[0].push_back(h);
-      cst[1].push_back(v);
+      Bp.cst[0].push_back(h);
+      Bp.cst[1].push_back(v);
     }
     if (P.conv & 2) {
       const int w = im_sharpen_kernel(P.cv[4], P.cv[5], &kk);
       ConvStep t = base;
       t.k = table(kk);
       t.kw = t.kh = w, t.in = cur, t.out = oth;
-      cst[2].push_back(t);
+      Bp.cst[2].push_back(t);
       std::swap(cur, oth);
     }
     if (P.conv & 4) {
@@ -1414,612 +1305,262 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
       h.k = v.k = table(kk);
       h.kw = w, h.kh = 1, h.in = cur, h.out = oth;
       v.kw = 1, v.kh = w, v.in = oth, v.out = cur;
-      cst[3].push_back(h);
-      cst[4].push_back(v);
+      Bp.cst[3].push_back(h);
+      Bp.cst[4].push_back(v);
     }
     ConvStep f = base;
     f.in = cur;
-    f.dst8 = out_of[ci.img];
+    f.dst8 = Bp.out_of[ci.img];
     f.dst_stride = imgs[ci.img].out_stride;
-    cst[5].push_back(f);
+    Bp.cst[5].push_back(f);
   }
-  for (size_t k = 0; k < SL.descs.size(); k++) {
-    ScDesc &d = SL.descs[k];
+  for (ScDesc &d : Bp.SL.descs) {
     fix_ptr(d.red, wb);
     fix_ptr(d.hbuf, wb);
     fix_ptr(d.pre, wb);
     fix_ptr(d.maps, wb);
   }
-  for (int i = 0; i < n; i++)
-    if (sc_of[i] >= 0) SL.descs[sc_of[i]].img = out_of[i];
-  const double t_sc = now_ms();
-  // ---- build launches
-  std::vector<int> m0, m1, m2, q0, q1, q2;  // q*: RGBA (matte) images of modes 0 / 1 / 2
-  for (size_t k = 0; k < rd.size(); k++) {
-    if (rd[k].mode >= 3) continue;
-    if (rd[k].C == 4)
-      (rd[k].mode == 0 ? q0 : rd[k].mode == 1 ? q1 : q2).push_back((int)k);
-    else
-      (rd[k].mode == 0 ? m0 : rd[k].mode == 1 ? m1 : m2).push_back((int)k);
-  }
-  // fused tiles: (image, column strip, row band); grouped by ring size K
-  struct FusedGroup {
-    std::vector<FusedTile> tiles;
-    int pitch = 0, max_taps = 0, max_nbytes = 0;
-    size_t off = 0;
-  };
-  std::map<int, FusedGroup> fgroups;
-  {
-    const int nf = (int)fused_img.size();
-    for (int q = 0; q < nf; q++) {
-      const ResizeDesc &d = rd[fused_img[q]];
-      const RingTable &R = *fused_ring[q];
-      const AxisTable &H = *fused_h[q];
-      FusedGroup &G = fgroups[d.fused_k];
-      const std::vector<StripTab> &strips = *fused_strips_of[q];
-      // row bands: enough work items to fill the chip (>= ~1024 per batch)
-      const int per_img = (int)strips.size();
-      int B = (1024 + nf * per_img - 1) / (nf * per_img);
-      B = std::max(1, std::min(B, d.eh / 16 > 0 ? d.eh / 16 : 1));
-      for (int b = 0; b < B; b++) {
-        const int y0 = (int)((int64_t)d.eh * b / B), y1 = (int)((int64_t)d.eh * (b + 1) / B);
-        if (y1 <= y0) continue;
-        for (const StripTab &st : strips) {
-          auto sp = c->strip_at.find(&st);
-          if (sp == c->strip_at.end()) {
-            const int32_t so = E.oi();
-            E.ai.insert(E.ai.end(), st.starts.begin(), st.starts.end());
-            const int32_t wo = E.of();
-            E.af.insert(E.af.end(), st.wT.begin(), st.wT.end());
-            sp = c->strip_at.emplace(&st, std::make_pair(so, wo)).first;
-          }
-          FusedTile t = st.t;
-          t.hstart = sp->second.first;
-          t.hw = sp->second.second;
-          t.image = fused_img[q];
-          t.y0 = y0;
-          t.y1 = y1;
-          t.i0 = R.first_i[y0];
-          t.i1 = R.last_i[y1 - 1] + 1;
-          G.tiles.push_back(t);
-          G.pitch = std::max(G.pitch, t.x1 - t.x0);
-          G.max_nbytes = std::max(G.max_nbytes, t.nbytes);
-          G.max_taps = std::max(G.max_taps, t.htaps);
-        }
-      }
-      (void)H;
-    }
-  }
-  // MFMA tiles: (image, strip, band of 16-row blocks); tables placed once per geometry
-  std::vector<MDesc> mdescs;
-  std::vector<MStrip> mstrips;
-  std::vector<MTile> mtiles;
-  size_t mfma_lds = 0;
-  {
-    auto align4 = [&]() {
-      while (E.ai.size() % 4) E.ai.push_back(0);
-    };
-    auto put = [&](const std::vector<int32_t> &v) {
-      const int32_t o = E.oi();
-      E.ai.insert(E.ai.end(), v.begin(), v.end());
-      return o;
-    };
-    std::map<const MfmaH *, std::pair<int32_t, int32_t>> hplaced;  // first strip, hwsum
-    std::vector<std::array<int32_t, 3>> mpairs;                       // (image, strip, mfma index)
-    const int nm = (int)mfma_img.size();
-    for (int q = 0; q < nm; q++) {
-      const ResizeDesc &d = rd[mfma_img[q]];
-      const MfmaV &V = *mfma_v[q];
-      const MfmaH &H = *mfma_h[q];
-      auto vp = c->mv_at.find(&V);
-      if (vp == c->mv_at.end()) {
-        std::array<int32_t, 5> o;
-        o[0] = put(V.rows);
-        o[1] = put(V.ya);
-        o[2] = put(V.yn);
-        o[4] = put(V.wsum);
-        align4();
-        o[3] = put(V.frag);
-        vp = c->mv_at.emplace(&V, o).first;
-      }
-      auto hp = hplaced.find(&H);
-      if (hp == hplaced.end()) {
-        const int32_t first = (int32_t)mstrips.size();
-        auto ht = c->mh_at.find(&H);
-        if (ht == c->mh_at.end()) {
-          std::array<int32_t, 4> o;
-          o[0] = put(H.wsum);
-          align4();
-          o[1] = put(H.frag);
-          o[2] = put(H.s0);
-          o[3] = put(H.lut);
-          ht = c->mh_at.emplace(&H, o).first;
-        }
-        const int32_t hw = ht->second[0], frag = ht->second[1], s0 = ht->second[2], lut = ht->second[3];
-        for (const MfmaStrip &st : H.strips) {
-          MStrip m{};
-          m.x0 = st.x0;
-          m.x1 = st.x1;
-          m.b0 = st.b0;
-          m.nbytes = st.nbytes;
-          m.c_lo = st.c_lo;
-          m.ncols = st.ncols;
-          m.pitch = st.pitch;
-          m.nocb = st.nocb;
-          m.ks = st.ks;
-          m.lut_px0 = st.lut_px0;
-          m.lut_n = st.lut_n;
-          m.frag = frag + (int32_t)st.frag;
-          m.s0 = s0 + (int32_t)st.s0;
-          m.lut = lut + (int32_t)st.lut;
-          mstrips.push_back(m);
-        }
-        hp = hplaced.emplace(&H, std::make_pair(first, hw)).first;
-      }
-      MDesc m{};
-      m.src = d.src;
-      m.src_stride = d.src_stride;
-      m.dst = d.dst;
-      m.dst_stride = d.dst_stride;
-      m.ew = d.ew;
-      m.eh = d.eh;
-      m.rot = d.rot;
-      m.gray = d.gray;
-      m.rows = vp->second[0];
-      m.ya = vp->second[1];
-      m.yn = vp->second[2];
-      m.row0 = V.rows.empty() ? 0 : V.rows[0];
-      m.rstep = V.rows.size() > 1 ? V.rows[1] - V.rows[0] : 1;
-      for (size_t k = 1; k < V.rows.size() && m.rstep > 0; k++)
-        if (V.rows[k] != m.row0 + m.rstep * (int32_t)k) m.rstep = 0;
-      m.vfrag = vp->second[3];
-      m.vwsum = vp->second[4];
-      m.ks = V.ks;
-      m.hwsum = hp->second.second;
-      const int32_t img = (int32_t)mdescs.size();
-      mdescs.push_back(m);
-      for (int k = 0; k < (int)H.strips.size(); k++) mpairs.push_back({img, hp->second.first + k, q});
-    }
-    // one workgroup per (image, strip), looping over its 16-row blocks; bands of
-    // blocks only when the batch is too small to fill the chip
-    const int np = (int)mpairs.size();
-    for (int j = 0; j < np; j++) {
-      const MfmaV &V = *mfma_v[mpairs[j][2]];
-      int bands = (2048 + np - 1) / std::max(np, 1);
-      bands = std::max(1, std::min(bands, V.nyb));
-      for (int bnd = 0; bnd < bands; bnd++) {
-        const int yb0 = (int)((int64_t)V.nyb * bnd / bands), yb1 = (int)((int64_t)V.nyb * (bnd + 1) / bands);
-        if (yb1 <= yb0) continue;
-        mtiles.push_back(MTile{mpairs[j][0], mpairs[j][1], yb0, yb1});
-        mfma_lds = std::max(mfma_lds, mfma_lds_bytes(yb1 - yb0));
-      }
-    }
-  }
-  const double t_tiles0 = now_ms();
-  // streaming MFMA tiles (k_rs_vm): (image, strip, band of blocks); tables placed once per geometry
-  std::vector<VDesc> vdescs;
-  std::vector<MStrip> vstrips;
-  std::vector<VTile> vtiles;
-  size_t vm_lds = 0;
-  {
-    auto align4 = [&]() {
-      while (E.ai.size() % 4) E.ai.push_back(0);
-    };
-    auto put = [&](const std::vector<int32_t> &v) {
-      const int32_t o = E.oi();
-      E.ai.insert(E.ai.end(), v.begin(), v.end());
-      return o;
-    };
-    std::map<const MfmaH *, std::pair<int32_t, int32_t>> hplaced;  // first strip, hwsum
-    struct Work1 {
-      int32_t img, first_strip, nstrips;
-      const VmV *V;
-    };
-    std::vector<Work1> work;
-    const int nv = (int)vm_img.size();
-    for (int q = 0; q < nv; q++) {
-      const ResizeDesc &d = rd[vm_img[q]];
-      const VmV &V = *vm_v[q];
-      const MfmaH &H = *vm_h[q];
-      auto vp = c->vv_at.find(&V);
-      if (vp == c->vv_at.end()) {
-        std::array<int32_t, 8> o;
-        std::vector<int32_t> meta;
-        for (size_t k = 0; k < V.plo.size(); k++) {
-          meta.push_back(V.plo[k]);
-          meta.push_back(V.pn[k]);
-          meta.push_back(V.pblk[k]);
-          meta.push_back(V.plast[k]);
-        }
-        align4();
-        o[7] = put(meta);
-        o[0] = put(V.rows);
-        o[1] = put(V.plo);
-        o[2] = put(V.pn);
-        o[3] = put(V.pblk);
-        o[4] = put(V.plast);
-        align4();
-        o[5] = put(V.w128);
-        align4();
-        o[6] = put(V.frag);
-        vp = c->vv_at.emplace(&V, o).first;
-      }
-      auto hp = hplaced.find(&H);
-      if (hp == hplaced.end()) {
-        const int32_t first = (int32_t)vstrips.size();
-        auto ht = c->mh_at.find(&H);
-        if (ht == c->mh_at.end()) {
-          std::array<int32_t, 4> o;
-          o[0] = put(H.wsum);
-          align4();
-          o[1] = put(H.frag);
-          o[2] = put(H.s0);
-          o[3] = put(H.lut);
-          ht = c->mh_at.emplace(&H, o).first;
-        }
-        const int32_t hw = ht->second[0], frag = ht->second[1], s0 = ht->second[2], lut = ht->second[3];
-        for (const MfmaStrip &st : H.strips) {
-          MStrip m{};
-          m.x0 = st.x0;
-          m.x1 = st.x1;
-          m.b0 = st.b0;
-          m.nbytes = st.nbytes;
-          m.c_lo = st.c_lo;
-          m.ncols = st.ncols;
-          m.pitch = st.pitch;
-          m.nocb = st.nocb;
-          m.ks = st.ks;
-          m.lut_px0 = st.lut_px0;
-          m.lut_n = st.lut_n;
-          m.frag = frag + (int32_t)st.frag;
-          m.s0 = s0 + (int32_t)st.s0;
-          m.lut = lut + (int32_t)st.lut;
-          m.vpitch = st.vpitch;
-          vstrips.push_back(m);
-        }
-        hp = hplaced.emplace(&H, std::make_pair(first, hw)).first;
-      }
-      for (const MfmaStrip &st : H.strips)  // the workgroup's LDS layout follows its strip and tile kind
-        vm_lds = std::max(vm_lds, vm_lds_bytes(st.vpitch, st.nocb, st.ks, d.gray || d.rot != 0));
-      VDesc m{};
-      m.src = d.src;
-      m.src_stride = d.src_stride;
-      m.dst = d.dst;
-      m.dst_stride = d.dst_stride;
-      m.ew = d.ew;
-      m.eh = d.eh;
-      m.rot = d.rot;
-      m.gray = d.gray;
-      m.rows = vp->second[0];
-      m.nrows = (int32_t)V.rows.size();
-      m.row0 = V.row0;
-      m.rstep = V.rstep;
-      m.plo = vp->second[1];
-      m.pn = vp->second[2];
-      m.pblk = vp->second[3];
-      m.plast = vp->second[4];
-      m.w128 = vp->second[5];
-      m.frag = vp->second[6];
-      m.pmeta = vp->second[7];
-      m.hwsum = hp->second.second;
-      m.nblk = V.nblk;
-      work.push_back({(int32_t)vdescs.size(), hp->second.first, (int32_t)H.strips.size(), &V});
-      vdescs.push_back(m);
-    }
-    // bands of blocks only when the batch is too small to fill the chip
-    int64_t nst = 0;
-    for (const Work1 &w : work) nst += w.nstrips;
-    // XCD-aware order: the strips of one image go to one XCD queue (blockIdx % 8 under
-    // round-robin dispatch) back to back, so the halo columns they share hit that L2
-    std::vector<std::vector<VTile>> q8(8);
-    for (size_t k = 0; k < work.size(); k++) {
-      const Work1 &w = work[k];
-      const VmV &V = *w.V;
-      int bands = nst > 0 ? (int)((2048 + nst - 1) / nst) : 1;
-      bands = std::max(1, std::min(bands, V.nblk));
-      std::vector<int> first_piece(V.nblk + 1, (int)V.plo.size());
-      for (int p = (int)V.plo.size() - 1; p >= 0; p--) first_piece[V.pblk[p]] = p;
-      for (int bnd = 0; bnd < bands; bnd++) {
-        const int b0 = (int)((int64_t)V.nblk * bnd / bands), b1 = (int)((int64_t)V.nblk * (bnd + 1) / bands);
-        if (b1 <= b0) continue;
-        const int p0 = first_piece[b0 > 0 ? b0 - 1 : 0];
-        const int p1 = first_piece[b1];
-        for (int st = 0; st < w.nstrips; st++)
-          q8[k % 8].push_back(VTile{w.img, w.first_strip + st, p0, p1, b0, 0});
-      }
-    }
-    size_t mx = 0;
-    for (auto &q : q8) mx = std::max(mx, q.size());
-    for (size_t i = 0; i < mx; i++)
-      for (int x = 0; x < 8; x++)
-        if (i < q8[x].size()) vtiles.push_back(q8[x][i]);
-  }
-  // persistent streaming work (k_rs_vs): one flat record per item (image, strip,
-  // band), in 8 per-XCD queues (all strips of an image in one queue)
-  std::vector<VsRec> srecs;
-  std::vector<int32_t> sqbeg(9, 0);
-  int vs_vpitch = 0;
-  {
-    auto align4 = [&]() {
-      while (E.ai.size() % 4) E.ai.push_back(0);
-    };
-    auto put = [&](const std::vector<int32_t> &v) {
-      const int32_t o = E.oi();
-      E.ai.insert(E.ai.end(), v.begin(), v.end());
-      return o;
-    };
-    std::vector<std::vector<VsRec>> q8(8);
-    int64_t nst = 0;
-    for (size_t q = 0; q < vs_img.size(); q++) nst += (int64_t)vs_h[q]->strips.size();
-    for (size_t q = 0; q < vs_img.size(); q++) {
-      const ResizeDesc &d = rd[vs_img[q]];
-      const VsV &V = *vs_v[q];
-      const MfmaH &H = *vs_h[q];
-      auto vp = c->vsv_at.find(&V);
-      if (vp == c->vsv_at.end()) {
-        std::array<int32_t, 3> o;
-        o[0] = put(V.rows);
-        align4();
-        o[1] = put(V.meta);
-        align4();
-        o[2] = put(V.afrag);
-        vp = c->vsv_at.emplace(&V, o).first;
-      }
-      auto ht = c->mh_at.find(&H);
-      if (ht == c->mh_at.end()) {
-        std::array<int32_t, 4> o;
-        o[0] = put(H.wsum);
-        align4();
-        o[1] = put(H.frag);
-        o[2] = put(H.s0);
-        o[3] = put(H.lut);
-        ht = c->mh_at.emplace(&H, o).first;
-      }
-      const int32_t frag = ht->second[1], s0 = ht->second[2];
-      VsRec base{};
-      base.src_stride = (int32_t)d.src_stride;
-      base.nrows = (int32_t)V.rows.size();
-      base.rows = vp->second[0];
-      base.afrag = vp->second[2];
-      base.ew = d.ew;
-      base.eh = d.eh;
-      base.gray = d.gray;
-      base.rot = d.rot;
-      base.dst_stride = (int32_t)d.dst_stride;
-      base.dst = d.dst;
-      // bands of blocks only when the batch is too small to fill the chip
-      int bands = nst > 0 ? (int)((2048 + nst - 1) / nst) : 1;
-      bands = std::max(1, std::min(bands, V.nblk));
-      for (int bnd = 0; bnd < bands; bnd++) {
-        const int b0 = (int)((int64_t)V.nblk * bnd / bands), b1 = (int)((int64_t)V.nblk * (bnd + 1) / bands);
-        if (b1 <= b0) continue;
-        for (const MfmaStrip &st : H.strips) {
-          auto lt = c->lanes_at.find(&st);
-          if (lt == c->lanes_at.end()) {
-            std::vector<int32_t> tab;
-            vs_lane_table(H, st, &tab);
-            align4();
-            lt = c->lanes_at.emplace(&st, put(tab)).first;
-          }
-          VsRec r = base;
-          r.src = d.src + st.b0;
-          r.nbytes = st.nbytes;
-          r.p0 = V.L[b0] / 64;
-          r.p1 = (V.R[b1 - 1] - 1) / 64 + 1;
-          r.emit0 = b0;
-          r.emit1 = b1;
-          r.lanes = lt->second;
-          r.frag = frag + (int32_t)st.frag;
-          r.s0 = s0 + (int32_t)st.s0;
-          r.ks = st.ks;
-          r.nocb = st.nocb;
-          r.vpitch = st.vpitch;
-          r.x0 = st.x0;
-          r.nx = st.x1 - st.x0;
-          q8[q % 8].push_back(r);
-          vs_vpitch = std::max(vs_vpitch, st.vpitch);
-        }
-      }
-    }
-    for (int x = 0; x < 8; x++) {
-      sqbeg[x] = (int32_t)srecs.size();
-      srecs.insert(srecs.end(), q8[x].begin(), q8[x].end());
-    }
-    sqbeg[8] = (int32_t)srecs.size();
-  }
-  // persistent row-ring block resample (k_rs_vb): items (image, strip, band of
-  // blocks) as flat records, statically assigned to the workgroups: record
-  // k * G + g is workgroup g's k-th item (XCD-major within a round, LPT by cost)
-  std::vector<VbRec> brecs;
-  std::vector<int32_t> bcount;
-  int vb_vpitch = 0, vb_grid = 0;
-  {
-    auto align4 = [&]() {
-      while (E.ai.size() % 4) E.ai.push_back(0);
-    };
-    auto put = [&](const std::vector<int32_t> &v) {
-      const int32_t o = E.oi();
-      E.ai.insert(E.ai.end(), v.begin(), v.end());
-      return o;
-    };
-    std::vector<VbRec> items;
-    std::vector<int64_t> cost;
-    int64_t nst = 0;
-    for (size_t q = 0; q < vb_img.size(); q++) nst += (int64_t)vb_h[q]->strips.size();
-    for (size_t q = 0; q < vb_img.size(); q++) {
-      const ResizeDesc &d = rd[vb_img[q]];
-      const VbV &V = *vb_v[q];
-      const MfmaH &H = *vb_h[q];
-      auto vp = c->vbv_at.find(&V);
-      if (vp == c->vbv_at.end()) {
-        std::array<int32_t, 2> o;
-        o[0] = put(V.rows);
-        align4();
-        o[1] = put(V.arec);
-        vp = c->vbv_at.emplace(&V, o).first;
-      }
-      auto ht = c->mh_at.find(&H);
-      if (ht == c->mh_at.end()) {
-        std::array<int32_t, 4> o;
-        o[0] = put(H.wsum);
-        align4();
-        o[1] = put(H.frag);
-        o[2] = put(H.s0);
-        o[3] = put(H.lut);
-        ht = c->mh_at.emplace(&H, o).first;
-      }
-      VbRec base{};
-      base.src_stride = (int32_t)d.src_stride;
-      base.nrows = (int32_t)V.rows.size();
-      base.rows = vp->second[0];
-      base.arec = vp->second[1];
-      base.row0 = V.rows[0];
-      base.rstep = V.rows.size() > 1 ? V.rows[1] - V.rows[0] : 1;
-      for (size_t k = 1; k < V.rows.size() && base.rstep > 0; k++)
-        if (V.rows[k] != base.row0 + base.rstep * (int32_t)k) base.rstep = 0;
-      base.ew = d.ew;
-      base.eh = d.eh;
-      base.gray = d.gray;
-      base.rot = d.rot;
-      base.dst_stride = (int32_t)d.dst_stride;
-      base.dst = d.dst;
-      // bands of blocks only when the batch is too small to fill the chip
-      int bands = nst > 0 ? (int)((1024 + nst - 1) / nst) : 1;
-      bands = std::max(1, std::min(bands, V.nblk));
-      for (int bnd = 0; bnd < bands; bnd++) {
-        const int b0 = (int)((int64_t)V.nblk * bnd / bands), b1 = (int)((int64_t)V.nblk * (bnd + 1) / bands);
-        if (b1 <= b0) continue;
-        for (const MfmaStrip &st : H.strips) {
-          auto lt = c->lanes_at.find(&st);
-          if (lt == c->lanes_at.end()) {
-            std::vector<int32_t> tab;
-            vs_lane_table(H, st, &tab);
-            align4();
-            lt = c->lanes_at.emplace(&st, put(tab)).first;
-          }
-          VbRec r = base;
-          r.src = d.src + st.b0;
-          r.nbytes = st.nbytes;
-          r.b0 = b0;
-          r.b1 = b1;
-          r.g0 = V.K0[b0] / 32;
-          r.gend = (V.R[b1 - 1] - 1) / 32 + 1;
-          r.last0 = (V.R[b0] - 1) / 32 - r.g0;
-          r.lanes = lt->second;
-          r.frag = ht->second[1] + (int32_t)st.frag;
-          r.s0 = ht->second[2] + (int32_t)st.s0;
-          r.ks = st.ks;
-          r.nocb = st.nocb;
-          r.vpitch = st.vpitch;
-          r.x0 = st.x0;
-          r.nx = st.x1 - st.x0;
-          items.push_back(r);
-          cost.push_back((int64_t)(r.gend - r.g0) + (b1 - b0));  // groups streamed + blocks computed
-          vb_vpitch = std::max(vb_vpitch, st.vpitch);
-        }
-      }
-    }
-    const int ni = (int)items.size();
-    if (ni > 0) {
-      const int G = std::min(c->ncu, ni);
-      vb_grid = G;
-      std::vector<std::vector<int>> lists(G);
-      bool uniform = true;
-      for (int i = 1; i < ni && uniform; i++) uniform = cost[i] == cost[0];
-      if (uniform) {
-        // rounds of G consecutive items; within a full round XCD-major (items
-        // p, p + 1, ... of one image share an XCD's L2: workgroup g sits on XCD g % 8)
-        for (int k = 0; k * G < ni; k++) {
-          const int n = std::min(G, ni - k * G);
-          for (int p = 0; p < n; p++) {
-            const int g = (n == G && G % 8 == 0) ? (p % (G / 8)) * 8 + p / (G / 8) : p;
-            lists[g].push_back(k * G + p);
-          }
-        }
-      } else {
-        // longest-processing-time first onto the least-loaded workgroup
-        std::vector<int> order(ni);
-        for (int i = 0; i < ni; i++) order[i] = i;
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
-        std::vector<std::pair<int64_t, int>> heap;
-        for (int g = 0; g < G; g++) heap.push_back({0, g});
-        auto cmp = [](const std::pair<int64_t, int> &a, const std::pair<int64_t, int> &b) { return a > b; };
-        std::make_heap(heap.begin(), heap.end(), cmp);
-        for (int i : order) {
-          std::pop_heap(heap.begin(), heap.end(), cmp);
-          auto &h = heap.back();
-          lists[h.second].push_back(i);
-          h.first += cost[i];
-          std::push_heap(heap.begin(), heap.end(), cmp);
-        }
-      }
-      size_t maxl = 0;
-      for (auto &l : lists) maxl = std::max(maxl, l.size());
-      brecs.assign(maxl * G, VbRec{});
-      bcount.assign(G, 0);
-      for (int g = 0; g < G; g++) {
-        bcount[g] = (int32_t)lists[g].size();
-        for (size_t k = 0; k < lists[g].size(); k++) brecs[k * G + g] = items[lists[g][k]];
-      }
-    }
-  }
-  const double t_tiles = now_ms();
-  Blob &B = E.blob;
-  const size_t all_rd_off = B.addv(rd);
-  const size_t mdesc_off = B.addv(mdescs), mstrip_off = B.addv(mstrips), mtile_off = B.addv(mtiles);
-  const size_t vdesc_off = B.addv(vdescs), vstrip_off = B.addv(vstrips), vtile_off = B.addv(vtiles);
-  const size_t brec_off = B.addv(brecs), bcount_off = B.addv(bcount);
-  const size_t srec_off = B.addv(srecs), sqbeg_off = B.addv(sqbeg), sqcnt_off = B.addv(std::vector<int32_t>(8, 0));
-  for (auto &g : fgroups) g.second.off = B.addv(g.second.tiles);
-  auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
-  auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
-  Launch L0 = add_launch(B, rd, m0, eh_tiles);
-  Launch L1a = add_launch(B, rd, m1, eh_tiles);
-  const bool h_tiled = rs_h_tile_lds(h_tile_pitch, h_tile_taps) <= 64 * 1024;
-  Launch L2a = h_tiled ? add_launch(B, rd, m2, [](const ResizeDesc &d) {
-    return ((d.mid_rows + kHTileRows - 1) / kHTileRows) * ((d.ew + 255) / 256);
-  }) : add_launch(B, rd, m2, mid_tiles);
-  Launch L2b = add_launch(B, rd, m2, eh_tiles);
-  Launch Q0 = add_launch(B, rd, q0, eh_tiles), Q1a = add_launch(B, rd, q1, eh_tiles),
-         Q2a = add_launch(B, rd, q2, mid_tiles), Q2b = add_launch(B, rd, q2, eh_tiles);
-  ScLaunches SX;
-  add_sc_launches(c, B, SL, sstatus, &SX);
-  const bool any_sc = SX.nsl + SX.nsg > 0;
-  std::vector<ApplyDesc> apply;
-  std::vector<int> apply_img;
-  for (int i = 0; i < n; i++) {
-    if (rd_of[i] < 0 || sc_of[i] < 0) continue;
+  for (int i = 0; i < Bp.n; i++)
+    if (Bp.sc_of[i] >= 0) Bp.SL.descs[Bp.sc_of[i]].img = Bp.out_of[i];
+  for (int i = 0; i < Bp.n; i++) {
+    if (Bp.rd_of[i] < 0 || Bp.sc_of[i] < 0) continue;
     if (!(imgs[i].flags & FI_OP_SMARTCROP_APPLY)) continue;
-    if (sstatus[sc_of[i]] != FI_OK) continue;
-    const ResizeDesc &d = rd[rd_of[i]];
+    if (Bp.sstatus[Bp.sc_of[i]] != FI_OK) continue;
+    const ResizeDesc &d = Bp.rd[Bp.rd_of[i]];
     ApplyDesc a{};
-    a.src = out_of[i];
+    a.src = Bp.out_of[i];
     a.src_stride = imgs[i].out_stride;
     a.W = d.out_w;
     a.H = d.out_h;
     a.C = d.out_c;
-    a.result = sc_of[i];
-    a.crop0 = SL.descs[sc_of[i]].crop0;
+    a.result = Bp.sc_of[i];
+    a.crop0 = Bp.SL.descs[Bp.sc_of[i]].crop0;
     a.dst = imgs[i].dst;
-    a.out_wh = (int32_t *)(wb + outwh_off + 8 * (size_t)i);
-    apply.push_back(a);
-    apply_img.push_back(i);
+    a.out_wh = (int32_t *)(wb + Bp.outwh_off + 8 * (size_t)i);
+    Bp.apply.push_back(a);
   }
-  const size_t apply_off = B.addv(apply);
-  const size_t mono_off = B.addv(mdesc_mono);
-  Launch CL[6];
+}
+
+// k_rs_fused tiles: (image, column strip, row band), grouped by ring size K.
+static void build_fused_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
+  const int nf = (int)Bp.fused_img.size();
+  for (int q = 0; q < nf; q++) {
+    const ResizeDesc &d = Bp.rd[Bp.fused_img[q]];
+    const RingTable &R = *Bp.fused_ring[q];
+    FusedGroup &G = Bp.fgroups[d.fused_k];
+    const std::vector<StripTab> &strips = *Bp.fused_strips_of[q];
+    // row bands: enough work items to fill the chip (>= ~1024 per batch)
+    const int per_img = (int)strips.size();
+    int B = (1024 + nf * per_img - 1) / (nf * per_img);
+    B = std::max(1, std::min(B, d.eh / 16 > 0 ? d.eh / 16 : 1));
+    for (int b = 0; b < B; b++) {
+      const int y0 = (int)((int64_t)d.eh * b / B), y1 = (int)((int64_t)d.eh * (b + 1) / B);
+      if (y1 <= y0) continue;
+      for (const StripTab &st : strips) {
+        auto sp = c->strip_at.find(&st);
+        if (sp == c->strip_at.end()) {
+          const int32_t so = E.oi();
+          E.ai.insert(E.ai.end(), st.starts.begin(), st.starts.end());
+          const int32_t wo = E.of();
+          E.af.insert(E.af.end(), st.wT.begin(), st.wT.end());
+          sp = c->strip_at.emplace(&st, std::make_pair(so, wo)).first;
+        }
+        FusedTile t = st.t;
+        t.hstart = sp->second.first;
+        t.hw = sp->second.second;
+        t.image = Bp.fused_img[q];
+        t.y0 = y0;
+        t.y1 = y1;
+        t.i0 = R.first_i[y0];
+        t.i1 = R.last_i[y1 - 1] + 1;
+        G.tiles.push_back(t);
+        G.pitch = std::max(G.pitch, t.x1 - t.x0);
+        G.max_nbytes = std::max(G.max_nbytes, t.nbytes);
+        G.max_taps = std::max(G.max_taps, t.htaps);
+      }
+    }
+  }
+}
+
+// k_rs_vm workgroups: (image, strip, band of blocks); the tables of a geometry
+// are placed in the heap once.
+static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
+  auto align4 = [&]() {
+    while (E.ai.size() % 4) E.ai.push_back(0);
+  };
+  auto put = [&](const std::vector<int32_t> &v) {
+    const int32_t o = E.oi();
+    E.ai.insert(E.ai.end(), v.begin(), v.end());
+    return o;
+  };
+  std::map<const MfmaH *, std::pair<int32_t, int32_t>> hplaced;  // first strip, hwsum
+  struct Work1 {
+    int32_t img, first_strip, nstrips;
+    const VmV *V;
+  };
+  std::vector<Work1> work;
+  const int nv = (int)Bp.vm_img.size();
+  for (int q = 0; q < nv; q++) {
+    const ResizeDesc &d = Bp.rd[Bp.vm_img[q]];
+    const VmV &V = *Bp.vm_v[q];
+    const MfmaH &H = *Bp.vm_h[q];
+    auto vp = c->vv_at.find(&V);
+    if (vp == c->vv_at.end()) {
+      std::array<int32_t, 8> o;
+      std::vector<int32_t> meta;
+      for (size_t k = 0; k < V.plo.size(); k++) {
+        meta.push_back(V.plo[k]);
+        meta.push_back(V.pn[k]);
+        meta.push_back(V.pblk[k]);
+        meta.push_back(V.plast[k]);
+      }
+      align4();
+      o[7] = put(meta);
+      o[0] = put(V.rows);
+      o[1] = put(V.plo);
+      o[2] = put(V.pn);
+      o[3] = put(V.pblk);
+      o[4] = put(V.plast);
+      align4();
+      o[5] = put(V.w128);
+      align4();
+      o[6] = put(V.frag);
+      vp = c->vv_at.emplace(&V, o).first;
+    }
+    auto hp = hplaced.find(&H);
+    if (hp == hplaced.end()) {
+      const int32_t first = (int32_t)Bp.vstrips.size();
+      auto ht = c->mh_at.find(&H);
+      if (ht == c->mh_at.end()) {
+        std::array<int32_t, 4> o;
+        o[0] = put(H.wsum);
+        align4();
+        o[1] = put(H.frag);
+        o[2] = put(H.s0);
+        o[3] = put(H.lut);
+        ht = c->mh_at.emplace(&H, o).first;
+      }
+      const int32_t hw = ht->second[0], frag = ht->second[1], s0 = ht->second[2], lut = ht->second[3];
+      for (const MfmaStrip &st : H.strips) {
+        MStrip m{};
+        m.x0 = st.x0;
+        m.x1 = st.x1;
+        m.b0 = st.b0;
+        m.nbytes = st.nbytes;
+        m.c_lo = st.c_lo;
+        m.ncols = st.ncols;
+        m.pitch = st.pitch;
+        m.nocb = st.nocb;
+        m.ks = st.ks;
+        m.lut_px0 = st.lut_px0;
+        m.lut_n = st.lut_n;
+        m.frag = frag + (int32_t)st.frag;
+        m.s0 = s0 + (int32_t)st.s0;
+        m.lut = lut + (int32_t)st.lut;
+        m.vpitch = st.vpitch;
+        Bp.vstrips.push_back(m);
+      }
+      hp = hplaced.emplace(&H, std::make_pair(first, hw)).first;
+    }
+    for (const MfmaStrip &st : H.strips)  // the workgroup's LDS layout follows its strip and tile kind
+      Bp.vm_lds = std::max(Bp.vm_lds, vm_lds_bytes(st.vpitch, st.nocb, st.ks, d.gray || d.rot != 0));
+    VDesc m{};
+    m.src = d.src;
+    m.src_stride = d.src_stride;
+    m.dst = d.dst;
+    m.dst_stride = d.dst_stride;
+    m.ew = d.ew;
+    m.eh = d.eh;
+    m.rot = d.rot;
+    m.gray = d.gray;
+    m.rows = vp->second[0];
+    m.nrows = (int32_t)V.rows.size();
+    m.row0 = V.row0;
+    m.rstep = V.rstep;
+    m.plo = vp->second[1];
+    m.pn = vp->second[2];
+    m.pblk = vp->second[3];
+    m.plast = vp->second[4];
+    m.w128 = vp->second[5];
+    m.frag = vp->second[6];
+    m.pmeta = vp->second[7];
+    m.hwsum = hp->second.second;
+    m.nblk = V.nblk;
+    work.push_back({(int32_t)Bp.vdescs.size(), hp->second.first, (int32_t)H.strips.size(), &V});
+    Bp.vdescs.push_back(m);
+  }
+  // bands of blocks only when the batch is too small to fill the chip
+  int64_t nst = 0;
+  for (const Work1 &w : work) nst += w.nstrips;
+  // XCD-aware order: the strips of one image go to one XCD queue (blockIdx % 8 under
+  // round-robin dispatch) back to back, so the halo columns they share hit that L2
+  std::vector<std::vector<VTile>> q8(8);
+  for (size_t k = 0; k < work.size(); k++) {
+    const Work1 &w = work[k];
+    const VmV &V = *w.V;
+    int bands = nst > 0 ? (int)((2048 + nst - 1) / nst) : 1;
+    bands = std::max(1, std::min(bands, V.nblk));
+    std::vector<int> first_piece(V.nblk + 1, (int)V.plo.size());
+    for (int p = (int)V.plo.size() - 1; p >= 0; p--) first_piece[V.pblk[p]] = p;
+    for (int bnd = 0; bnd < bands; bnd++) {
+      const int b0 = (int)((int64_t)V.nblk * bnd / bands), b1 = (int)((int64_t)V.nblk * (bnd + 1) / bands);
+      if (b1 <= b0) continue;
+      const int p0 = first_piece[b0 > 0 ? b0 - 1 : 0];
+      const int p1 = first_piece[b1];
+      for (int st = 0; st < w.nstrips; st++) q8[k % 8].push_back(VTile{w.img, w.first_strip + st, p0, p1, b0, 0});
+    }
+  }
+  size_t mx = 0;
+  for (auto &q : q8) mx = std::max(mx, q.size());
+  for (size_t i = 0; i < mx; i++)
+    for (int x = 0; x < 8; x++)
+      if (i < q8[x].size()) Bp.vtiles.push_back(q8[x][i]);
+}
+
+// Pack descriptors, tiles, launch lists and the batch's new heap tables into
+// the upload blob E.blob.
+static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
+  Blob &B = E.blob;
+  std::vector<int> m0, m1, m2, q0, q1, q2;  // q*: RGBA (matte) images of modes 0 / 1 / 2
+  for (size_t k = 0; k < Bp.rd.size(); k++) {
+    if (Bp.rd[k].mode >= 3) continue;
+    if (Bp.rd[k].C == 4)
+      (Bp.rd[k].mode == 0 ? q0 : Bp.rd[k].mode == 1 ? q1 : q2).push_back((int)k);
+    else
+      (Bp.rd[k].mode == 0 ? m0 : Bp.rd[k].mode == 1 ? m1 : m2).push_back((int)k);
+  }
+  K.all_rd_off = B.addv(Bp.rd);
+  K.vdesc_off = B.addv(Bp.vdescs);
+  K.vstrip_off = B.addv(Bp.vstrips);
+  K.vtile_off = B.addv(Bp.vtiles);
+  for (auto &g : Bp.fgroups) g.second.off = B.addv(g.second.tiles);
+  auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
+  auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
+  K.L0 = add_launch(B, Bp.rd, m0, eh_tiles);
+  K.L1a = add_launch(B, Bp.rd, m1, eh_tiles);
+  K.h_tiled = rs_h_tile_lds(Bp.h_tile_pitch, Bp.h_tile_taps) <= 64 * 1024;
+  K.L2a = K.h_tiled ? add_launch(B, Bp.rd, m2, [](const ResizeDesc &d) {
+    return ((d.mid_rows + kHTileRows - 1) / kHTileRows) * ((d.ew + 255) / 256);
+  }) : add_launch(B, Bp.rd, m2, mid_tiles);
+  K.L2b = add_launch(B, Bp.rd, m2, eh_tiles);
+  K.Q0 = add_launch(B, Bp.rd, q0, eh_tiles);
+  K.Q1a = add_launch(B, Bp.rd, q1, eh_tiles);
+  K.Q2a = add_launch(B, Bp.rd, q2, mid_tiles);
+  K.Q2b = add_launch(B, Bp.rd, q2, eh_tiles);
+  add_sc_launches(c, B, Bp.SL, Bp.sstatus, &K.SX);
+  K.apply_off = B.addv(Bp.apply);
+  K.mono_off = B.addv(Bp.mdesc_mono);
   for (int k = 0; k < 6; k++) {
-    std::vector<int> all(cst[k].size());
+    std::vector<int> all(Bp.cst[k].size());
     for (size_t j = 0; j < all.size(); j++) all[j] = (int)j;
-    CL[k] = add_launch(B, cst[k], all, [](const ConvStep &st) { return st.H; });
+    K.CL[k] = add_launch(B, Bp.cst[k], all, [](const ConvStep &st) { return st.H; });
   }
-  size_t mono_wts = 0;
-  if (!mono.empty() && c->mono_wts_at >= 0) mono_wts = (size_t)c->mono_wts_at;
-  if (!mono.empty() && c->mono_wts_at < 0) {
+  if (!Bp.mono.empty() && c->mono_wts_at >= 0) K.mono_wts = (size_t)c->mono_wts_at;
+  if (!Bp.mono.empty() && c->mono_wts_at < 0) {
     // the Riemersma error-queue weights (quantize.c), computed with libm at run
     // time exactly as oracle/fi_oracle.c does
-    mono_wts = (size_t)E.od();
-    c->mono_wts_at = (int32_t)mono_wts;
+    K.mono_wts = (size_t)E.od();
+    c->mono_wts_at = (int32_t)K.mono_wts;
     volatile double qr1 = 65535.0 + 1.0, span = 16 - 1.0;
     const double step = exp(log((double)qr1) / (double)span);
     double weight = 1.0, wts[16];
@@ -2029,7 +1570,169 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     }
     E.ad.insert(E.ad.end(), wts, wts + 16);
   }
-  const size_t ai_off = B.addv(E.ai), af_off = B.addv(E.af), ad_off = B.addv(E.ad);
+  K.ai_off = B.addv(E.ai);
+  K.af_off = B.addv(E.af);
+  K.ad_off = B.addv(E.ad);
+}
+
+// Enqueue the batch: resample, convolutions and -monochrome on the main
+// stream; the smartcrop stage and crop apply on sc_stream behind this batch's
+// resample (so they overlap the next batch's upload and resample).
+static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Packed &K, uint8_t *ab, uint8_t *wb,
+                        Slot &S) {
+  const int32_t *ai = (const int32_t *)c->heap_i.p;
+  const float *af = (const float *)c->heap_f.p;
+  const double *ad = (const double *)c->heap_d.p;
+  const ScParamsDev PD = to_dev(E.params);
+  auto desc_p = [&](const Launch &L) { return ab + L.desc_off; };
+  auto pre_p = [&](const Launch &L) { return (const int32_t *)(ab + L.prefix_off); };
+  Timer tb(c, "batch", 0, c->stream, c->sc_stream);
+  {
+    Timer t(c, "resize", Bp.resize_bytes);
+    if (K.L0.tiles)
+      hipLaunchKernelGGL(k_rs_copy, dim3(K.L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(K.L0),
+                         pre_p(K.L0), K.L0.n);
+    if (!Bp.vtiles.empty() &&
+        launch_vm(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
+                  (const VTile *)(ab + K.vtile_off), (int)Bp.vtiles.size(), ai, Bp.vm_lds) != 0)
+      return set_err(FI_EDEVICE, "streaming MFMA resample launch rejected (LDS %zu)", Bp.vm_lds);
+    for (auto &g : Bp.fgroups) {
+      const FusedGroup &G = g.second;
+      if (G.tiles.empty()) continue;
+      const int pitch = (G.pitch + 3) & ~3;
+      if (launch_fused(c->stream, g.first, (const ResizeDesc *)(ab + K.all_rd_off), (const FusedTile *)(ab + G.off),
+                       (int)G.tiles.size(), ai, af, pitch, G.max_taps, G.max_nbytes) != 0)
+        return set_err(FI_EDEVICE, "fused resample launch rejected (K=%d, LDS budget)", g.first);
+    }
+    if (K.Q0.tiles || K.Q1a.tiles || K.Q2a.tiles) {
+      const ResizeDesc *dq0 = (const ResizeDesc *)desc_p(K.Q0), *dq1 = (const ResizeDesc *)desc_p(K.Q1a),
+                       *dq2a = (const ResizeDesc *)desc_p(K.Q2a), *dq2b = (const ResizeDesc *)desc_p(K.Q2b);
+      launch_rs4(c->stream, 0, dq0, pre_p(K.Q0), K.Q0.n, K.Q0.tiles, nullptr, nullptr, 0, 0, ai, ad);
+      launch_rs4(c->stream, 1, dq1, pre_p(K.Q1a), K.Q1a.n, K.Q1a.tiles, dq1, pre_p(K.Q1a), K.Q1a.n, K.Q1a.tiles, ai,
+                 ad);
+      launch_rs4(c->stream, 2, dq2a, pre_p(K.Q2a), K.Q2a.n, K.Q2a.tiles, dq2b, pre_p(K.Q2b), K.Q2b.n, K.Q2b.tiles,
+                 ai, ad);
+    }
+    if (K.L1a.tiles) {
+      hipLaunchKernelGGL(k_rs_v_u8, dim3(K.L1a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(K.L1a),
+                         pre_p(K.L1a), K.L1a.n, ai, af);
+      hipLaunchKernelGGL(k_rs_h_final, dim3(K.L1a.tiles), dim3(256), 0, c->stream,
+                         (const ResizeDesc *)desc_p(K.L1a), pre_p(K.L1a), K.L1a.n, ai, af);
+    }
+    if (K.L2a.tiles) {
+      if (K.h_tiled)
+        launch_rs_h_tile(c->stream, (const ResizeDesc *)desc_p(K.L2a), pre_p(K.L2a), K.L2a.n, K.L2a.tiles, ai, af,
+                         Bp.h_tile_pitch, Bp.h_tile_taps);
+      else
+        hipLaunchKernelGGL(k_rs_h_u8, dim3(K.L2a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(K.L2a),
+                           pre_p(K.L2a), K.L2a.n, ai, af);
+      hipLaunchKernelGGL(k_rs_v_final, dim3(K.L2b.tiles), dim3(256), 0, c->stream,
+                         (const ResizeDesc *)desc_p(K.L2b), pre_p(K.L2b), K.L2b.n, ai, af);
+    }
+  }
+  if (!Bp.conv_items.empty()) {
+    Timer t(c, "conv", 0);
+    static const int kMode[6] = {0, 2, 3, 0, 1, 4};
+    for (int k = 0; k < 6; k++)
+      launch_conv(c->stream, kMode[k], (const ConvStep *)desc_p(K.CL[k]), pre_p(K.CL[k]), K.CL[k].n, K.CL[k].tiles,
+                  ad);
+  }
+  if (!Bp.mono.empty()) {
+    Timer t(c, "mono", 0);
+    (void)launch_mono(c->stream, (const MonoDesc *)(ab + K.mono_off), (int)Bp.mono.size(), ad + K.mono_wts);
+  }
+  HIP_TRY(hipGetLastError());
+  if (!S.rs_done) HIP_TRY(hipEventCreateWithFlags(&S.rs_done, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(S.rs_done, c->stream));
+  HIP_TRY(hipStreamWaitEvent(c->sc_stream, S.rs_done, 0));
+  if (K.SX.nsl + K.SX.nsg > 0) {
+    const int rc = enqueue_sc(c, c->sc_stream, ab, K.SX, ai, ad, (CropScore *)(wb + Bp.scores_off),
+                              (ScResult *)(wb + Bp.results_off), PD);
+    if (rc) return rc;
+    if (!Bp.apply.empty()) {
+      Timer t(c, "crop_apply", 0, c->sc_stream, c->sc_stream);
+      (void)launch_crop_apply(c->sc_stream, (const ApplyDesc *)(ab + K.apply_off), (int)Bp.apply.size(),
+                              (const DevCrop *)(ab + K.SX.crops_off), (const ScResult *)(wb + Bp.results_off));
+    }
+    HIP_TRY(hipGetLastError());
+  }
+  return FI_OK;
+}
+
+// Per-image result records into the slot's pinned readback; the batch joins
+// the in-flight list (finalize_front fills the caller's records).
+static int queue_readback(fi_ctx *c, BatchPlan &Bp, int slot, uint8_t *wb, double t_start) {
+  Slot &S = c->slots[slot];
+  uint8_t *rp = (uint8_t *)S.res;
+  const size_t res_bytes = sizeof(ScResult) * Bp.sitems.size();
+  const size_t outwh_bytes = sizeof(int32_t) * 2 * (size_t)Bp.n;
+  if (!Bp.sitems.empty())
+    HIP_TRY(hipMemcpyAsync(rp, wb + Bp.results_off, res_bytes, hipMemcpyDeviceToHost, c->sc_stream));
+  if (!Bp.apply.empty())
+    HIP_TRY(hipMemcpyAsync(rp + res_bytes, wb + Bp.outwh_off, outwh_bytes, hipMemcpyDeviceToHost, c->sc_stream));
+  if (!S.done) HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(S.done, c->sc_stream));
+  S.busy = true;
+  c->next_slot = (slot + 1) % kSlots;
+  PendingBatch pb;
+  pb.imgs = Bp.imgs;
+  pb.n = Bp.n;
+  pb.slot = slot;
+  pb.t_start = t_start;
+  pb.status = std::move(Bp.status);
+  pb.errs = std::move(Bp.errs);
+  pb.sc_of = std::move(Bp.sc_of);
+  pb.sstatus = std::move(Bp.sstatus);
+  pb.serrs = std::move(Bp.serrs);
+  pb.crop0.resize(Bp.SL.descs.size());
+  for (size_t k = 0; k < Bp.SL.descs.size(); k++) pb.crop0[k] = Bp.SL.descs[k].crop0;
+  pb.crops = std::move(Bp.SL.crops);
+  pb.nres = Bp.sitems.size();
+  pb.any_apply = !Bp.apply.empty();
+  pb.timers.swap(c->pending);  // waited for when this batch is finalized
+  c->inflight.push_back(std::move(pb));
+  return FI_OK;
+}
+
+static int drain(fi_ctx *c);
+static int wait_slot(fi_ctx *c, int slot);
+static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
+  const double t_start = now_ms();
+  Exec E;
+  E.c = c;
+  fi_smartcrop_default_params(&E.params);
+  int rc = heap_prepare(c, E);
+  if (rc) return rc;
+  BatchPlan Bp;
+  Bp.imgs = imgs;
+  Bp.n = n;
+  Bp.plans.resize(n);
+  Bp.status.assign(n, FI_OK);
+  Bp.errs.resize(n);
+  Bp.rd_of.assign(n, -1);
+  Bp.sc_of.assign(n, -1);
+  Bp.res_off.assign(n, 0);
+  Bp.out_of.assign(n, nullptr);
+  for (int i = 0; i < n; i++) plan_image(c, E, Bp, i);
+  const double t_images = now_ms();
+  plan_batch_sc(c, E, Bp);
+  // the batch's slot: pinned staging + device blob/workspace (the batch that
+  // used it last must be done before anything here is overwritten)
+  const int slot = c->next_slot;
+  rc = wait_slot(c, slot);
+  if (rc) return rc;
+  Slot &S = c->slots[slot];
+  rc = ensure(c, &S.work, E.work.size + 256);
+  if (rc) return rc;
+  uint8_t *wb = (uint8_t *)S.work.p;
+  resolve_workspace(E, Bp, wb);
+  const double t_sc = now_ms();
+  build_fused_tiles(c, E, Bp);
+  const double t_tiles0 = now_ms();
+  build_vm_tiles(c, E, Bp);
+  const double t_tiles = now_ms();
+  Packed K;
+  pack_batch(c, E, Bp, K);
   if (!heap_fits(c, E)) {
     // the batch's new tables overflow the heaps: start them empty and plan again
     if (c->heap_retry) return set_err(FI_ENOMEM, "batch tables exceed the device table heap");
@@ -2040,13 +1743,12 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     return rrc;
   }
   // ---- upload (pinned slot: the previous batch may still be running)
+  const Blob &B = E.blob;
   rc = ensure(c, &S.arena, B.b.size() + 256);
   if (rc) return rc;
   rc = ensure_pinned_buf(&S.blob, &S.blob_cap, B.b.size() + 256);
   if (rc) return rc;
-  const size_t res_bytes = sizeof(ScResult) * sitems.size();
-  const size_t outwh_bytes = sizeof(int32_t) * 2 * (size_t)n;
-  rc = ensure_pinned_buf(&S.res, &S.res_cap, res_bytes + outwh_bytes + 64);
+  rc = ensure_pinned_buf(&S.res, &S.res_cap, sizeof(ScResult) * Bp.sitems.size() + sizeof(int32_t) * 2 * (size_t)n + 64);
   if (rc) return rc;
   memcpy(S.blob, B.b.data(), B.b.size());
   HIP_TRY(hipMemcpyAsync(S.arena.p, S.blob, B.b.size(), hipMemcpyHostToDevice, c->stream));
@@ -2059,124 +1761,12 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   host_stat(c, "host_plan_blob", t_planned - t_tiles);
   if (c->timing) c->stats["host_plan"].bytes += (double)B.b.size();
   uint8_t *ab = (uint8_t *)S.arena.p;
-  rc = heap_commit(c, E, ab, ai_off, af_off, ad_off);
+  rc = heap_commit(c, E, ab, K.ai_off, K.af_off, K.ad_off);
   if (rc) return rc;
-  const int32_t *ai = (const int32_t *)c->heap_i.p;
-  const float *af = (const float *)c->heap_f.p;
-  const double *ad = (const double *)c->heap_d.p;
-  const ScParamsDev PD = to_dev(E.params);
-  auto desc_p = [&](const Launch &L) { return ab + L.desc_off; };
-  auto pre_p = [&](const Launch &L) { return (const int32_t *)(ab + L.prefix_off); };
-  // ---- resample kernels
-  {
-    Timer tb(c, "batch", 0, c->stream, c->sc_stream);
-    {
-      Timer t(c, "resize", resize_bytes);
-      if (L0.tiles)
-        hipLaunchKernelGGL(k_rs_copy, dim3(L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L0),
-                           pre_p(L0), L0.n);
-      if (!brecs.empty() &&
-          launch_vb(c->stream, vb_grid, (const VbRec *)(ab + brec_off), (const int32_t *)(ab + bcount_off), ai, vb_vpitch) != 0)
-        return set_err(FI_EDEVICE, "row-ring block resample launch rejected (vpitch %d)", vb_vpitch);
-      if (!srecs.empty() &&
-          launch_vs(c->stream, std::min<int>(c->ncu, (int)srecs.size()), (const VsRec *)(ab + srec_off),
-                    (const int32_t *)(ab + sqbeg_off), (int32_t *)(ab + sqcnt_off), ai, vs_vpitch) != 0)
-        return set_err(FI_EDEVICE, "persistent streaming resample launch rejected (vpitch %d)", vs_vpitch);
-      if (!vtiles.empty() &&
-          launch_vm(c->stream, (const VDesc *)(ab + vdesc_off), (const MStrip *)(ab + vstrip_off),
-                    (const VTile *)(ab + vtile_off), (int)vtiles.size(), ai, vm_lds) != 0)
-        return set_err(FI_EDEVICE, "streaming MFMA resample launch rejected (LDS %zu)", vm_lds);
-      if (!mtiles.empty() &&
-          launch_mfma(c->stream, (const MDesc *)(ab + mdesc_off), (const MStrip *)(ab + mstrip_off),
-                      (const MTile *)(ab + mtile_off), (int)mtiles.size(), ai, mfma_lds) != 0)
-        return set_err(FI_EDEVICE, "MFMA resample launch rejected (LDS %zu)", mfma_lds);
-      for (auto &g : fgroups) {
-        const FusedGroup &G = g.second;
-        if (G.tiles.empty()) continue;
-        const int pitch = (G.pitch + 3) & ~3;
-        if (launch_fused(c->stream, g.first, (const ResizeDesc *)(ab + all_rd_off), (const FusedTile *)(ab + G.off),
-                         (int)G.tiles.size(), ai, af, pitch, G.max_taps, G.max_nbytes) != 0)
-          return set_err(FI_EDEVICE, "fused resample launch rejected (K=%d, LDS budget)", g.first);
-      }
-      if (Q0.tiles || Q1a.tiles || Q2a.tiles) {
-        const ResizeDesc *dq0 = (const ResizeDesc *)desc_p(Q0), *dq1 = (const ResizeDesc *)desc_p(Q1a),
-                         *dq2a = (const ResizeDesc *)desc_p(Q2a), *dq2b = (const ResizeDesc *)desc_p(Q2b);
-        launch_rs4(c->stream, 0, dq0, pre_p(Q0), Q0.n, Q0.tiles, nullptr, nullptr, 0, 0, ai, ad);
-        launch_rs4(c->stream, 1, dq1, pre_p(Q1a), Q1a.n, Q1a.tiles, dq1, pre_p(Q1a), Q1a.n, Q1a.tiles, ai, ad);
-        launch_rs4(c->stream, 2, dq2a, pre_p(Q2a), Q2a.n, Q2a.tiles, dq2b, pre_p(Q2b), Q2b.n, Q2b.tiles, ai, ad);
-      }
-      if (L1a.tiles) {
-        hipLaunchKernelGGL(k_rs_v_u8, dim3(L1a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L1a),
-                           pre_p(L1a), L1a.n, ai, af);
-        hipLaunchKernelGGL(k_rs_h_final, dim3(L1a.tiles), dim3(256), 0, c->stream,
-                           (const ResizeDesc *)desc_p(L1a), pre_p(L1a), L1a.n, ai, af);
-      }
-      if (L2a.tiles) {
-        if (h_tiled)
-          launch_rs_h_tile(c->stream, (const ResizeDesc *)desc_p(L2a), pre_p(L2a), L2a.n, L2a.tiles, ai, af,
-                           h_tile_pitch, h_tile_taps);
-        else
-          hipLaunchKernelGGL(k_rs_h_u8, dim3(L2a.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(L2a),
-                             pre_p(L2a), L2a.n, ai, af);
-        hipLaunchKernelGGL(k_rs_v_final, dim3(L2b.tiles), dim3(256), 0, c->stream,
-                           (const ResizeDesc *)desc_p(L2b), pre_p(L2b), L2b.n, ai, af);
-      }
-    }
-    if (!conv_items.empty()) {
-      Timer t(c, "conv", 0);
-      static const int kMode[6] = {0, 2, 3, 0, 1, 4};
-      for (int k = 0; k < 6; k++)
-        launch_conv(c->stream, kMode[k], (const ConvStep *)desc_p(CL[k]), pre_p(CL[k]), CL[k].n, CL[k].tiles, ad);
-    }
-    if (!mono.empty()) {
-      Timer t(c, "mono", 0);
-      (void)launch_mono(c->stream, (const MonoDesc *)(ab + mono_off), (int)mono.size(), ad + mono_wts);
-    }
-    HIP_TRY(hipGetLastError());
-    // the smartcrop stage, crop apply and readback go on sc_stream behind this
-    // batch's resample, so they overlap the next batch's upload and resample
-    if (!S.rs_done) HIP_TRY(hipEventCreateWithFlags(&S.rs_done, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(S.rs_done, c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->sc_stream, S.rs_done, 0));
-    if (any_sc) {
-      rc = enqueue_sc(c, c->sc_stream, ab, SX, ai, ad, (CropScore *)(wb + scores_off),
-                      (ScResult *)(wb + results_off), PD);
-      if (rc) return rc;
-      if (!apply.empty()) {
-        Timer t(c, "crop_apply", 0, c->sc_stream, c->sc_stream);
-        (void)launch_crop_apply(c->sc_stream, (const ApplyDesc *)(ab + apply_off), (int)apply.size(),
-                                (const DevCrop *)(ab + SX.crops_off), (const ScResult *)(wb + results_off));
-      }
-      HIP_TRY(hipGetLastError());
-    }
-  }
-  // ---- results: per-image records into the slot's pinned readback
-  uint8_t *rp = (uint8_t *)S.res;
-  if (!sitems.empty())
-    HIP_TRY(hipMemcpyAsync(rp, wb + results_off, res_bytes, hipMemcpyDeviceToHost, c->sc_stream));
-  if (!apply.empty())
-    HIP_TRY(hipMemcpyAsync(rp + res_bytes, wb + outwh_off, outwh_bytes, hipMemcpyDeviceToHost, c->sc_stream));
-  if (!S.done) HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(S.done, c->sc_stream));
-  S.busy = true;
-  c->next_slot = (slot + 1) % kSlots;
-  PendingBatch pb;
-  pb.imgs = imgs;
-  pb.n = n;
-  pb.slot = slot;
-  pb.t_start = t_start;
-  pb.status = std::move(status);
-  pb.errs = std::move(errs);
-  pb.sc_of = std::move(sc_of);
-  pb.sstatus = std::move(sstatus);
-  pb.serrs = std::move(serrs);
-  pb.crop0.resize(SL.descs.size());
-  for (size_t k = 0; k < SL.descs.size(); k++) pb.crop0[k] = SL.descs[k].crop0;
-  pb.crops = std::move(SL.crops);
-  pb.nres = sitems.size();
-  pb.any_apply = !apply.empty();
-  pb.timers.swap(c->pending);  // waited for when this batch is finalized
-  c->inflight.push_back(std::move(pb));
+  rc = launch_batch(c, E, Bp, K, ab, wb, S);
+  if (rc) return rc;
+  rc = queue_readback(c, Bp, slot, wb, t_start);
+  if (rc) return rc;
   host_stat(c, "host_launch", now_ms() - t_planned);
   if (async) return FI_OK;
   return drain(c);
@@ -2357,18 +1947,6 @@ extern "C" {
 
 int32_t fi_abi_version(void) { return FI_ABI_VERSION; }
 // profiling only (not in the public header): k_rs_vm MODE 9 phase sums, 8 u64 per workgroup
-int fi_debug_vb_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
-  if (!c || !out) return FI_EINVAL;
-  HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return vb_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
-}
-int fi_debug_vs_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
-  if (!c || !out) return FI_EINVAL;
-  HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return vs_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
-}
 int fi_debug_vm_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   if (!c || !out) return FI_EINVAL;
   HIP_TRY(hipSetDevice(c->device));
@@ -2531,12 +2109,8 @@ int fi_create(fi_ctx **out, int32_t device) {
     return set_err(FI_EDEVICE, "device %d is %s; libflyimg_hip.so is built for gfx950 only", device, prop.gcnArchName);
   fi_ctx *c = new fi_ctx();
   c->device = device;
-  c->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
-  if (const char *e = getenv("FI_ENABLE_MFMA_RS")) c->mfma_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
-  if (const char *e = getenv("FI_VS_RS")) c->vs_rs = e[0] == '1';
-  if (const char *e = getenv("FI_VB_RS")) c->vb_rs = e[0] == '1';
   if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
   if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');

@@ -158,18 +158,6 @@ __host__ __device__ inline int mfma_i8_k(int l, int j) {
   return j < 8 ? 8 * (l >> 4) + j : 32 + 8 * (l >> 4) + (j - 8);
 #endif
 }
-// k_rs_mfma (fi_mfma.hip): exact-integer MFMA resample, vertical first.
-struct MDesc {                // one image
-  const uint8_t *src;
-  int64_t src_stride;
-  uint8_t *dst;
-  int64_t dst_stride;
-  int32_t ew, eh, rot, gray;
-  int32_t rows, ya, yn, vfrag, vwsum;  // arena offsets (int32 units) of the MfmaV tables
-  int32_t ks;                          // vertical k-steps (1 or 2)
-  int32_t hwsum;                       // arena offset of the horizontal per-px weight sums
-  int32_t row0, rstep;                 // rstep > 0: touched rows are row0 + rstep * k (no list lookup)
-};
 struct MStrip {               // one column strip (fi_plan.h MfmaStrip) placed in the arena
   int32_t x0, x1, b0, nbytes;
   int32_t c_lo, ncols, pitch, nocb, ks;
@@ -177,14 +165,6 @@ struct MStrip {               // one column strip (fi_plan.h MfmaStrip) placed i
   int32_t frag, s0, lut;      // arena offsets (int32 units; frag 16-B aligned)
   int32_t vpitch;             // k_rs_vm: Q16 plane columns (multiple of 16)
 };
-struct MTile {                // one workgroup: image x strip x band [yb0, yb1) of 16-row blocks
-  int32_t img, strip, yb0, yb1;
-};
-constexpr int kMfmaThreads = 256;  // 4 waves; three workgroups per CU overlap their phases
-// LDS plane pitch of k_rs_mfma (bytes): fixed so row offsets are instruction
-// immediates; = 8 (mod 32) spreads rows 4 apart over the banks.
-constexpr int kMfmaPitch = 232;
-
 // k_sc_hmfma (fi_smartcrop.hip): Pillow's horizontal pass as exact integer
 // MFMA.  Per 16-column output block b: source window [s0(b), s0(b) + 64 KS),
 // coefficient limbs L0 + 256 L1 + 65536 L2 (signed i8) in fragment order;
@@ -221,81 +201,6 @@ constexpr int kVmOtilePitch = 64 * 3 + 4;      // Q16 output tile row, u16 units
 constexpr int kVmOtileBytes = 16 * kVmOtilePitch * 2;
 constexpr int kVmOtile8Pitch = 64 * 3 + 4;     // 8-bit tile row (fast RGB path)
 constexpr int kVmOtile8Bytes = 16 * kVmOtile8Pitch;
-
-// k_rs_vs (fi_vs.hip): persistent streaming exact-integer MFMA resample,
-// vertical first.  One workgroup per CU: kVsThreads / 64 waves x (32 / waves)
-// column tiles of 16 B = 512-B strips (MStrip, shared with k_rs_vm).  Source pieces (64
-// rows x 512 B) and their A-fragment records arrive by LDS-DMA in a 3-deep
-// ring; work items come from per-XCD queues.
-constexpr int kVsThreads = 1024;
-constexpr int kVsSlots = 3;              // accumulator slots (blocks touched by one piece)
-constexpr int kVsMaxComp = 2;            // blocks completing at one piece
-constexpr int kVsRing = 3;               // A-record ring depth (pieces)
-constexpr int kVsDataRing = 2;           // source-piece ring depth: a piece's B operands go to registers first
-constexpr int kVsPieceBytes = 64 * 512;
-constexpr int kVsAFragBytes = 10 * 1024;  // per piece: 9 fragments + w128 rows
-constexpr int kVsW128 = 9 * 256;          // int32 offset of the w128 rows in the record
-constexpr int kVsMeta = kVsW128 + 48;     // int32 offset of the piece meta {bf, nb, comp, rows}
-constexpr int kVsRecRing = 8;             // LDS ring of item records
-constexpr int kVsCtlBytes = kVsRecRing * 128 + 2 * 256;  // + 2 row tables of 64 source rows
-constexpr int kVsHfBytes = 4 * 2 * 3 * 1024;  // the item's horizontal B fragments [ob][t][limb] (nocb <= 4, ks <= 2)
-constexpr int kVsPlaneOff = kVsDataRing * kVsPieceBytes + kVsRing * kVsAFragBytes + kVsCtlBytes + kVsHfBytes;
-constexpr int kVsMaxLds = 160 * 1024;
-// One work item of k_rs_vs -- (image, strip, pieces [p0, p1)), emitting blocks
-// [emit0, emit1) -- flattened with its image's and strip's fields, so the
-// kernel fetches one 128-byte record per item (no dependent descriptor loads).
-struct VsRec {
-  // issue cursor (words 0-8)
-  const uint8_t *src;   // image source + the strip's first byte
-  int32_t src_stride, nbytes;
-  int32_t nrows, rows, afrag, p0;    // touched-row list (ai offset; rows[k]); piece records (ai offset); pieces
-  int32_t p1;
-  // item entry (words 9-13)
-  int32_t lanes, frag, s0;           // lane table / strip B fragments / (w0, ks) pairs (ai offsets)
-  int32_t ks, nocb;                  // strip: k-steps, 16-px output blocks
-  // block phase and stores (words 14-25)
-  int32_t vpitch, emit0;             // plane columns; emitted blocks [emit0, emit1)
-  int32_t emit1, x0, nx, ew;         // first output px of the strip, its px; extent width
-  int32_t eh, gray, rot, dst_stride; // dst_stride < 2^31
-  uint8_t *dst;
-  int32_t pad[6];
-};
-static_assert(sizeof(VsRec) == 128, "VsRec is one 128-byte record");
-
-// k_rs_vb (fi_vb.hip): persistent streaming exact-integer MFMA resample,
-// vertical first, one output block per iteration.  One 1024-thread workgroup
-// per CU (16 waves x 2 column tiles of 16 B = 512-B strips, MStrip); the
-// touched source rows stream through an LDS ring of kVbGroups groups of 32
-// rows (LDS-DMA, issued as far ahead as the ring allows).
-constexpr int kVbThreads = 1024;
-constexpr int kVbGroups = 6;                  // ring: 6 x 32 rows x 512 B = 96 KB
-constexpr int kVbGroupBytes = 32 * 512;
-constexpr int kVbABytes = 7 * 1024;           // per block: 6 fragments + w128 / meta
-constexpr int kVbW128 = 6 * 256;              // int32 offset of the w128 rows in the record
-constexpr int kVbMeta = kVbW128 + 16;         // int32 offset of {K0, ks, R}
-constexpr int kVbARing = 2;
-constexpr int kVbSinkBytes = 256;             // scratch bytes (MODE 1 ablation sink)
-constexpr int kVbHfBytes = 3 * 2 * 3 * 1024;  // the item's horizontal B fragments [ob][t][limb] (nocb <= 3, ks <= 2)
-constexpr int kVbMaxWindow = 112;             // rows a block may read: its groups stay within the ring's first 4
-constexpr int kVbPlaneOff = kVbGroups * kVbGroupBytes + kVbARing * kVbABytes + kVbSinkBytes + kVbHfBytes;
-constexpr int kVbMaxLds = 160 * 1024;
-// One work item: (image, strip, blocks [b0, b1)), flattened with its image's
-// and strip's fields (read with scalar loads).
-struct VbRec {
-  const uint8_t *src;   // image source + the strip's first byte
-  int32_t src_stride, nbytes;
-  int32_t nrows, rows, arec, b0;     // touched-row list (ai offset); block records (ai offset); blocks
-  int32_t b1, lanes, frag, s0;       // lane table / strip B fragments / (w0, ks) pairs (ai offsets)
-  int32_t ks, nocb, vpitch, x0;      // strip: k-steps, 16-px output blocks, plane columns, first output px
-  int32_t nx, ew, eh, gray;
-  int32_t rot, dst_stride;           // dst_stride < 2^31
-  uint8_t *dst;
-  int32_t g0, gend;                  // row groups (32 list rows) the item's blocks read: [g0, gend)
-  int32_t row0, rstep;               // rstep > 0: the touched-row list is row0 + rstep k (no table reads)
-  int32_t last0;                     // the first block's last window group, relative to g0
-  int32_t pad[3];
-};
-static_assert(sizeof(VbRec) == 128, "VbRec is one 128-byte record");
 
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;

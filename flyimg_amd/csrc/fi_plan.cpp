@@ -421,47 +421,6 @@ static void put_frag(std::vector<int32_t> &frag, size_t base, int lane, int j, c
     reinterpret_cast<uint8_t *>(&frag[base + (size_t)q * 256])[lane * 16 + j] = (uint8_t)(int8_t)limb[q];
 }
 
-bool build_mfma_v(const AxisTable &v, MfmaV *m) {
-  *m = MfmaV();
-  const int ny = (int)v.start.size();
-  if (ny == 0) return false;
-  std::vector<int32_t> idx;
-  touched_list(v, &m->rows, &idx);
-  m->nyb = (ny + 15) / 16;
-  m->ya.assign(m->nyb, 0);
-  m->yn.assign(m->nyb, 0);
-  int ks = 1;
-  for (int b = 0; b < m->nyb; b++) {
-    int lo = 1 << 30, hi = -1;
-    for (int y = 16 * b; y < std::min(ny, 16 * b + 16); y++) {
-      int a, e;
-      tap_range(v, idx, y, &a, &e);
-      lo = std::min(lo, a);
-      hi = std::max(hi, e);
-    }
-    if (hi < lo) continue;
-    m->ya[b] = lo;
-    m->yn[b] = hi - lo + 1;
-    ks = std::max(ks, (m->yn[b] + 63) / 64);
-  }
-  if (ks > 2) return false;
-  m->ks = ks;
-  m->wsum.assign((size_t)16 * m->nyb, 0);
-  for (int y = 0; y < ny; y++)
-    for (int j = 0; j < v.count[y]; j++) m->wsum[y] += quant_w(v.w[v.woff[y] + j]);
-  m->frag.assign((size_t)m->nyb * ks * 3 * 256, 0);
-  for (int b = 0; b < m->nyb; b++)
-    for (int t = 0; t < ks; t++)
-      for (int l = 0; l < 64; l++)
-        for (int j = 0; j < 16; j++) {
-          const int y = 16 * b + (l & 15), li = m->ya[b] + 64 * t + mfma_i8_k(l, j);
-          int32_t limb[3];
-          limbs3(y < ny && li < m->ya[b] + m->yn[b] ? tap_w(v, m->rows, y, li) : 0, limb);
-          put_frag(m->frag, (size_t)(b * ks + t) * 3 * 256, l, j, limb);
-        }
-  return true;
-}
-
 bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
   *m = MfmaH();
   const int nx = (int)h.start.size();
@@ -512,8 +471,7 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
     // fragment reads of rows 1 apart spread over the LDS banks
     S.pitch = pitch + ((8 - pitch % 32) + 32) % 32;
     if (getenv("FI_DEBUG_MFMA_PITCH")) fprintf(stderr, "strip %d..%d ncols %d pitch %d\n", x0, x1, S.ncols, S.pitch);
-    if (S.pitch > kMfmaPitch) return false;
-    S.pitch = kMfmaPitch;
+    if (S.pitch > kMfmaMaxPitch) return false;
     S.vpitch = (pitch + 15) / 16 * 16;
     S.lut_px0 = S.b0 / 3;
     S.lut_n = (S.b0 + S.nbytes + 2) / 3 - S.lut_px0;
@@ -619,162 +577,6 @@ bool build_vm_v(const AxisTable &v, VmV *m) {
   return true;
 }
 
-bool build_vs_v(const AxisTable &v, VsV *m) {
-  *m = VsV();
-  const int ny = (int)v.start.size();
-  if (ny == 0) return false;
-  std::vector<int32_t> idx;
-  touched_list(v, &m->rows, &idx);
-  const int nl = (int)m->rows.size();
-  if (nl == 0) return false;
-  m->nblk = (ny + 15) / 16;
-  m->L.assign(m->nblk, 0);
-  m->R.assign(m->nblk, 0);
-  for (int b = 0; b < m->nblk; b++) {
-    int lo = 1 << 30, hi = -1;
-    for (int y = 16 * b; y < std::min(ny, 16 * b + 16); y++) {
-      int a, e;
-      tap_range(v, idx, y, &a, &e);
-      if (e < a) return false;  // an output row without taps
-      lo = std::min(lo, a);
-      hi = std::max(hi, e);
-    }
-    m->L[b] = lo;
-    m->R[b] = hi + 1;
-    if (b > 0 && (m->L[b] < m->L[b - 1] || m->R[b] < m->R[b - 1])) return false;  // not monotone
-  }
-  m->np = (nl + 63) / 64;
-  m->meta.assign((size_t)m->np * 4, 0);
-  constexpr int kRec = kVsAFragBytes / 4;
-  m->afrag.assign((size_t)m->np * kRec, 0);
-  int bf = 0;
-  for (int p = 0; p < m->np; p++) {
-    const int s = 64 * p, e = std::min(s + 64, nl);
-    while (bf < m->nblk && m->R[bf] <= s) bf++;
-    int nb = 0, comp = 0;
-    while (bf + nb < m->nblk && m->L[bf + nb] < e) nb++;
-    while (bf + comp < m->nblk && m->R[bf + comp] <= e) comp++;
-    if (nb < 1 || nb > kVsSlots || comp > kVsMaxComp || comp > nb) return false;
-    int32_t *mt = &m->meta[(size_t)4 * p];
-    mt[0] = bf;
-    mt[1] = nb;
-    mt[2] = comp;
-    mt[3] = e - s;
-    int32_t *rec = &m->afrag[(size_t)p * kRec];
-    for (int k = 0; k < 4; k++) rec[kVsMeta + k] = mt[k];
-    for (int sl = 0; sl < kVsSlots; sl++) {
-      const int b = bf + sl;
-      if (b >= m->nblk) break;
-      for (int r = 0; r < 16; r++) {
-        const int y = 16 * b + r;
-        int32_t w = 0;
-        if (y < ny)
-          for (int j = 0; j < v.count[y]; j++) w += 128 * quant_w(v.w[v.woff[y] + j]);
-        rec[kVsW128 + 16 * sl + r] = w;
-      }
-      if (sl >= nb) continue;
-      for (int l = 0; l < 64; l++)
-        for (int j = 0; j < 16; j++) {
-          const int y = 16 * b + (l & 15), li = s + mfma_i8_k(l, j);
-          int32_t limb[3];
-          limbs3(y < ny && li < e ? tap_w(v, m->rows, y, li) : 0, limb);
-          for (int q = 0; q < 3; q++)
-            reinterpret_cast<uint8_t *>(rec + (size_t)(sl * 3 + q) * 256)[l * 16 + j] = (uint8_t)(int8_t)limb[q];
-        }
-    }
-  }
-  // every tap lies in a piece whose slot window holds its block
-  for (int y = 0; y < ny; y++) {
-    const int b = y / 16;
-    for (int j = 0; j < v.count[y]; j++) {
-      if (v.w[v.woff[y] + j] == 0.0f) continue;
-      const int li = idx[v.start[y] + j - v.src_lo], p = li / 64;
-      const int32_t *mt = &m->meta[(size_t)4 * p];
-      if (b < mt[0] || b >= mt[0] + mt[1]) return false;
-    }
-  }
-  m->row0 = m->rows[0];
-  m->rstep = nl > 1 ? m->rows[1] - m->rows[0] : 1;
-  for (int k = 1; k < nl && m->rstep > 0; k++)
-    if (m->rows[k] != m->row0 + m->rstep * k) m->rstep = 0;
-  return true;
-}
-
-bool build_vb_v(const AxisTable &v, VbV *m) {
-  *m = VbV();
-  const int ny = (int)v.start.size();
-  if (ny == 0) return false;
-  std::vector<int32_t> idx;
-  touched_list(v, &m->rows, &idx);
-  const int nl = (int)m->rows.size();
-  if (nl == 0) return false;
-  m->nblk = (ny + 15) / 16;
-  m->K0.assign(m->nblk, 0);
-  m->ks.assign(m->nblk, 0);
-  m->R.assign(m->nblk, 0);
-  constexpr int kRec = kVbABytes / 4;
-  m->arec.assign((size_t)m->nblk * kRec, 0);
-  for (int b = 0; b < m->nblk; b++) {
-    int lo = 1 << 30, hi = -1;
-    for (int y = 16 * b; y < std::min(ny, 16 * b + 16); y++) {
-      int a, e;
-      tap_range(v, idx, y, &a, &e);
-      if (e < a) return false;  // an output row without taps
-      lo = std::min(lo, a);
-      hi = std::max(hi, e);
-    }
-    const int K0 = lo / 16 * 16, ks = (hi + 1 - K0 + 63) / 64;
-    if (ks > 2 || hi + 1 - K0 > kVbMaxWindow) return false;
-    if (b > 0 && (K0 < m->K0[b - 1] || hi + 1 < m->R[b - 1])) return false;  // not monotone
-    m->K0[b] = K0;
-    m->ks[b] = ks;
-    m->R[b] = hi + 1;
-    int32_t *rec = &m->arec[(size_t)b * kRec];
-    for (int t = 0; t < ks; t++)
-      for (int l = 0; l < 64; l++)
-        for (int j = 0; j < 16; j++) {
-          const int y = 16 * b + (l & 15), li = K0 + 64 * t + mfma_i8_k(l, j);
-          int32_t limb[3];
-          limbs3(y < ny && li < nl ? tap_w(v, m->rows, y, li) : 0, limb);
-          for (int q = 0; q < 3; q++)
-            reinterpret_cast<uint8_t *>(rec + (size_t)(t * 3 + q) * 256)[l * 16 + j] = (uint8_t)(int8_t)limb[q];
-        }
-    for (int r = 0; r < 16; r++) {
-      const int y = 16 * b + r;
-      int32_t w = 0;
-      if (y < ny)
-        for (int j = 0; j < v.count[y]; j++) w += 128 * quant_w(v.w[v.woff[y] + j]);
-      rec[kVbW128 + r] = w;
-    }
-    rec[kVbMeta + 0] = K0;
-    rec[kVbMeta + 1] = ks;
-    rec[kVbMeta + 2] = hi + 1;
-  }
-  return true;
-}
-
-void vs_lane_table(const MfmaH &h, const MfmaStrip &st, std::vector<int32_t> *out) {
-  constexpr int waves = kVsThreads / 64, tiles = 32 / waves, items = (12 + waves - 1) / waves;
-  out->assign((size_t)kVsThreads * 4, 0);
-  const int plane = 16 * st.vpitch, nx = st.x1 - st.x0;
-  auto col_off = [](int ci) { return (ci * 16) ^ (((ci >> 4) & 1) << 7); };
-  for (int tid = 0; tid < kVsThreads; tid++) {
-    const int w = tid >> 6, l = tid & 63;
-    for (int j = 0; j < tiles; j++) {
-      const int col = 16 * tiles * w + 16 * j + (l & 15);
-      const int ab = st.b0 + std::min(col, st.nbytes - 1), px = ab / 3, chn = ab - 3 * px;
-      const int ci = h.lut[st.lut + (px - st.lut_px0)];
-      const uint32_t o = (col < st.nbytes && ci >= 0) ? (uint32_t)(chn * plane + col_off(ci) + 4 * (l >> 4)) : 0xFFFFu;
-      (*out)[4 * tid + (j >> 1)] |= (int32_t)(o << (16 * (j & 1)));
-    }
-    for (int k = 0; k < items; k++) {
-      float hws = 0.0f;
-      const int it = w + waves * k, ob = it / 3, hx = 16 * ob + (l & 15);
-      if (it < 3 * st.nocb && hx < nx) hws = 32896.0f * (float)h.wsum[st.x0 + hx];
-      memcpy(&(*out)[4 * tid + 2 + k], &hws, 4);
-    }
-  }
-}
 
 bool build_ring(const AxisTable &v, RingTable *rt) {
   *rt = RingTable();

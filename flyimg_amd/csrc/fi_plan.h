@@ -64,21 +64,14 @@ struct RingTable {
 // active on one source row, or a non-monotone tap layout).
 bool build_ring(const AxisTable &v, RingTable *rt);
 
-// Exact-integer MFMA resample tables (k_rs_mfma, fi_mfma.hip).  Weights are
-// quantized to W = rint(w * 2^kMfmaWBits) and split into three signed-byte
-// limbs; fragments are in the v_mfma_i32_16x16x64_i8 lane order
+// Exact-integer MFMA resample tables (k_rs_vm, fi_vm.hip; k_sc_hmfma).
+// Weights are quantized to W = rint(w * 2^kMfmaWBits) and split into three
+// signed-byte limbs; fragments are in the v_mfma_i32_16x16x64_i8 lane order
 // (fi_internal.h mfma_i8_k), 256 int32 (1 KB) each.
 constexpr int kMfmaWBits = 22;
 constexpr int kMfmaStripBytes = 512;   // source bytes per column strip
-constexpr int kMfmaMaxNx = 168;        // output px per strip (out tile aliases the wave tiles)
-struct MfmaV {                         // vertical pass over the touched-row list
-  std::vector<int32_t> rows;           // touched source rows, ascending
-  int nyb = 0, ks = 0;                 // blocks of 16 output rows; k-steps of 64 list rows
-  std::vector<int32_t> ya, yn;         // [nyb] window start (list index), window rows
-  std::vector<int32_t> frag;           // [nyb][ks][3] A fragments (weights)
-  std::vector<int32_t> wsum;           // [16 nyb] sum of quantized weights per output row
-};
-bool build_mfma_v(const AxisTable &v, MfmaV *m);
+constexpr int kMfmaMaxNx = 168;        // output px per strip
+constexpr int kMfmaMaxPitch = 232;     // widest strip window (touched columns incl. fragment padding)
 struct MfmaStrip {                     // one column strip of the horizontal pass
   int32_t x0, x1;                      // output px [x0, x1)
   int32_t b0, nbytes;                  // source bytes loaded (16-B aligned)
@@ -115,43 +108,6 @@ struct VmV {
   int32_t row0 = 0, rstep = 0;         // rstep > 0: rows[k] == row0 + rstep * k
 };
 bool build_vm_v(const AxisTable &v, VmV *m);
-
-// Streaming vertical tables of k_rs_vs (fi_vs.hip).  The touched-row list is
-// cut into uniform pieces of 64 rows (the last one shorter).  Block b's taps
-// span list rows [L(b), R(b)); a piece touches the blocks whose windows
-// intersect it -- at most kVsSlots consecutive ones, bf .. bf + nb - 1 -- and
-// completes those with R(b) inside it (at most kVsMaxComp).  Per piece one
-// kVsAFragBytes record: the A fragments [slot][limb] (256 int32 each, zero for
-// slots >= nb), at int32 offset kVsW128 128 * sum of the quantized weights
-// of each row of blocks bf .. bf + 2 ([slot][16]), at kVsMeta the piece meta.
-struct VsV {
-  std::vector<int32_t> rows;           // touched source rows, ascending
-  int nblk = 0, np = 0;                // 16-row output blocks; pieces
-  std::vector<int32_t> L, R;           // [nblk] block windows in list rows
-  std::vector<int32_t> meta;           // [np][4]: bf, nb, comp, rows in the piece
-  std::vector<int32_t> afrag;          // [np][kVsAFragBytes / 4]
-  int32_t row0 = 0, rstep = 0;         // rstep > 0: rows[k] == row0 + rstep * k
-};
-bool build_vs_v(const AxisTable &v, VsV *m);
-// Block tables of k_rs_vb (fi_vb.hip).  Output block b (16 rows) is computed
-// in one pass over its tap window: list rows [K0(b), K0(b) + 64 ks(b)), K0 a
-// multiple of 16, ks <= 2 (window + alignment <= 128 rows).  Per block one
-// kVbABytes record: A fragments [t][limb] (256 int32 each) for list rows
-// K0 + 64 t + k, then at int32 offset kVbW128 the rows' 128 * sum of quantized
-// weights, at kVbMeta {K0, ks, R}.
-struct VbV {
-  std::vector<int32_t> rows;           // touched source rows, ascending
-  int nblk = 0;
-  std::vector<int32_t> K0, ks, R;      // [nblk]
-  std::vector<int32_t> arec;           // [nblk][kVbABytes / 4]
-};
-bool build_vb_v(const AxisTable &v, VbV *m);
-
-// Per-lane constants of k_rs_vs for one strip (512 lanes x 4 int32): the Q16
-// plane offsets of the lane's four column tiles (16 bits each, 0xFFFF = column
-// not needed) and, per horizontal item of its wave (wave, wave + 8), the f32
-// bits of 32896 * (horizontal weight sum) of the lane's output pixel.
-void vs_lane_table(const MfmaH &h, const MfmaStrip &st, std::vector<int32_t> *out);
 
 // Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)
 // to `out_size`; taps mapped back to the `in_src` source indices through the

@@ -97,7 +97,8 @@ __device__ uint64_t g_vm_stamps[kVmStampSlots * (kVmStampN + 1)];
 // MODE (profiling ablations, FI_VM_VARIANT; wrong pixels): 0 production,
 // 1 loads + LDS writes only, 2 no horizontal pass / epilogue, 3 no stores,
 // 4 no horizontal pass (planes + stores kept), 5 as 4 without stores, 6 as 4
-// without planes (stores kept), 9 production + per-phase s_memtime sums
+// without planes (stores kept), 7 one horizontal item per wave (the 9th of
+// an RGB nocb = 3 strip skipped), 9 production + per-phase s_memtime sums
 // (tools/vm_timing.py).
 // Launch bound: 8-wave workgroups, two per CU -> 4 waves per SIMD (<= 128 VGPRs).
 template <int MODE>
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
     }
     if (tid < 388) *reinterpret_cast<i32x4 *>(apl + 16 * tid) = aq;
     stamp(2);
-    if ((MODE == 0 || MODE == 4 || MODE == 6 || MODE == 9) && pend >= 0) {
+    if ((MODE == 0 || MODE == 4 || MODE == 6 || MODE == 7 || MODE == 9) && pend >= 0) {
       store_block(pend);
       pend = -1;
     }
@@ -405,7 +406,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
 #pragma unroll
           for (int k = 0; k < 2; k++) {
             const int it = wv + kVmWaves * k;
-            if (it >= 3 * S.nocb) break;
+            if (it >= 3 * S.nocb || (MODE == 7 && k > 0)) break;
             const int ob = it / 3, chn = it - 3 * ob;
             const int hw0 = hw0k[k], hks = hksk[k];
             i32x4 hh[3], hl[3];
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
     }
     mc = mn;
   }
-  if ((MODE == 0 || MODE == 4 || MODE == 6 || MODE == 9) && pend >= 0) {
+  if ((MODE == 0 || MODE == 4 || MODE == 6 || MODE == 7 || MODE == 9) && pend >= 0) {
     __syncthreads();
     store_block(pend);
   }
@@ -508,6 +509,8 @@ int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTi
     hipLaunchKernelGGL((k_rs_vm<5>), dim3(ntiles), dim3(kVmThreads), lds, s, descs, strips, tiles, ai);
   else if (v == 6)
     hipLaunchKernelGGL((k_rs_vm<6>), dim3(ntiles), dim3(kVmThreads), lds, s, descs, strips, tiles, ai);
+  else if (v == 7)
+    hipLaunchKernelGGL((k_rs_vm<7>), dim3(ntiles), dim3(kVmThreads), lds, s, descs, strips, tiles, ai);
   else if (v == 9)
     hipLaunchKernelGGL((k_rs_vm<9>), dim3(ntiles), dim3(kVmThreads), lds, s, descs, strips, tiles, ai);
   else

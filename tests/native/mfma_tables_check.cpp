@@ -1,4 +1,4 @@
-// CPU check of the k_rs_mfma / k_sc_hmfma host tables (fi_plan.cpp): the
+// CPU check of the k_rs_vm / k_sc_hmfma host tables (fi_plan.cpp): the
 // weight matrices rebuilt from the fragment bytes through mfma_i8_k must give,
 // with the kernel's integer algebra, exactly sum(quant(w) * p) for every
 // output -- for the vertical pass over the touched-row list, the horizontal
@@ -39,48 +39,6 @@ static int64_t limb_w(const std::vector<int32_t> &f, size_t base, int lane, int 
 }
 
 static bool g_required = false;  // the geometry must take the MFMA path
-static void check_v(const AxisTable &v, const char *name) {
-  MfmaV m;
-  if (!build_mfma_v(v, &m)) {
-    printf("  %s: vertical tables not built (ks > 2), skipped\n", name);
-    CHECK(!g_required, "%s: vertical MFMA tables required", name);
-    return;
-  }
-  const int ny = (int)v.start.size();
-  std::mt19937 rng(1234);
-  const int H = v.src_hi;
-  std::vector<int> p(H);
-  for (auto &x : p) x = (int)(rng() & 255);
-  for (int b = 0; b < m.nyb; b++) {
-    // W[m][k] over the block's k-steps
-    std::vector<int64_t> W((size_t)16 * 64 * m.ks, 0);
-    for (int t = 0; t < m.ks; t++)
-      for (int l = 0; l < 64; l++)
-        for (int j = 0; j < 16; j++)
-          W[(size_t)(l & 15) * 64 * m.ks + 64 * t + mfma_i8_k(l, j)] =
-              limb_w(m.frag, (size_t)(b * m.ks + t) * 3 * 256, l, j);
-    for (int r = 0; r < 16; r++) {
-      const int y = 16 * b + r;
-      if (y >= ny) continue;
-      int64_t s = 0;  // kernel: sum W (p - 128) + 128 wsum
-      for (int k = 0; k < 64 * m.ks; k++) {
-        const int64_t w = W[(size_t)r * 64 * m.ks + k];
-        if (k >= m.yn[b]) {
-          CHECK(w == 0, "%s: weight beyond the window y=%d k=%d", name, y, k);
-          continue;
-        }
-        s += w * (p[m.rows[m.ya[b] + k]] - 128);
-      }
-      s += 128 * (int64_t)m.wsum[y];
-      int64_t ref = 0;
-      for (int j = 0; j < v.count[y]; j++) ref += (int64_t)qw(v.w[v.woff[y] + j]) * p[v.start[y] + j];
-      CHECK(s == ref, "%s: vertical y=%d %lld != %lld", name, y, (long long)s, (long long)ref);
-      CHECK(llabs(s) < (1ll << 31), "%s: vertical sum exceeds int32", name);
-    }
-  }
-  printf("  %s: vertical %d blocks ks=%d rows=%zu ok\n", name, m.nyb, m.ks, m.rows.size());
-}
-
 // k_rs_vm: stream the pieces in order with two accumulator slots exactly as
 // the kernel does (slot 0 = the piece's block, slot 1 = the next block,
 // started at its w128 correction) and compare every completed block.
@@ -141,108 +99,6 @@ static void check_vm(const AxisTable &v, const char *name) {
 // k_rs_vs: stream the uniform 64-row pieces with three rotating slots exactly
 // as the kernel does (new slots start at the record's w128 rows, completed
 // slots retire from the bottom) and compare every completed block.
-static void check_vs(const AxisTable &v, const char *name) {
-  VsV m;
-  if (!build_vs_v(v, &m)) {
-    printf("  %s: persistent streaming tables not built, skipped\n", name);
-    CHECK(!g_required, "%s: persistent streaming tables required", name);
-    return;
-  }
-  const int ny = (int)v.start.size();
-  const int nl = (int)m.rows.size();
-  constexpr int kRec = kVsAFragBytes / 4;
-  CHECK(m.np == (nl + 63) / 64, "%s: piece count", name);
-  std::mt19937 rng(777);
-  std::vector<int> px(v.src_hi);
-  for (auto &x : px) x = (int)(rng() & 255);
-  std::vector<int64_t> acc[kVsSlots];
-  for (auto &a : acc) a.assign(16, 0);
-  int live = 0, done = 0, max_nb = 0, max_comp = 0;
-  for (int p = 0; p < m.np; p++) {
-    const int32_t *mt = &m.meta[(size_t)4 * p];
-    const int bf = mt[0], nb = mt[1], comp = mt[2], nrows = mt[3];
-    max_nb = std::max(max_nb, nb);
-    max_comp = std::max(max_comp, comp);
-    CHECK(bf == done, "%s: piece %d starts at block %d, %d done", name, p, bf, done);
-    CHECK(nrows == std::min(64, nl - 64 * p), "%s: piece rows", name);
-    const int32_t *rec = &m.afrag[(size_t)p * kRec];
-    for (int s = live; s < nb; s++)
-      for (int r = 0; r < 16; r++) acc[s][r] = rec[kVsW128 + 16 * s + r];
-    for (int s = 0; s < nb; s++)
-      for (int l = 0; l < 64; l++)
-        for (int j = 0; j < 16; j++) {
-          const int k = mfma_i8_k(l, j);
-          const int64_t w = limb_w(m.afrag, (size_t)p * kRec + (size_t)s * 3 * 256, l, j);
-          if (k >= nrows) {
-            CHECK(w == 0, "%s: weight past the piece", name);
-            continue;
-          }
-          acc[s][l & 15] += w * (px[m.rows[64 * p + k]] - 128);
-        }
-    for (int c = 0; c < comp; c++) {
-      const int b = bf + c;
-      for (int r = 0; r < 16; r++) {
-        const int y = 16 * b + r;
-        if (y >= ny) continue;
-        int64_t ref = 0;
-        for (int j = 0; j < v.count[y]; j++) ref += (int64_t)qw(v.w[v.woff[y] + j]) * px[v.start[y] + j];
-        CHECK(acc[c][r] == ref, "%s: vs vertical y=%d %lld != %lld", name, y, (long long)acc[c][r], (long long)ref);
-        CHECK(llabs(acc[c][r]) < (1ll << 31), "%s: accumulator exceeds int32", name);
-      }
-      done++;
-    }
-    for (int s = 0; s + comp < kVsSlots; s++) acc[s] = acc[s + comp];
-    live = nb - comp;
-  }
-  CHECK(done == m.nblk, "%s: %d of %d blocks completed", name, done, m.nblk);
-  printf("  %s: persistent streaming %d blocks, %d pieces, max slots %d, max completions %d, rstep %d ok\n", name,
-         m.nblk, m.np, max_nb, max_comp, m.rstep);
-}
-
-// k_rs_vb: each block in one pass over its window with separate limb sums
-static void check_vb(const AxisTable &v, const char *name) {
-  VbV m;
-  if (!build_vb_v(v, &m)) {
-    printf("  %s: block-window tables not built, skipped\n", name);
-    CHECK(!g_required, "%s: block-window tables required", name);
-    return;
-  }
-  const int ny = (int)v.start.size(), nl = (int)m.rows.size();
-  constexpr int kRec = kVbABytes / 4;
-  std::mt19937 rng(31337);
-  std::vector<int> px(v.src_hi);
-  for (auto &x : px) x = (int)(rng() & 255);
-  int maxw = 0;
-  for (int b = 0; b < m.nblk; b++) {
-    const int32_t *rec = &m.arec[(size_t)b * kRec];
-    CHECK(rec[kVbMeta] == m.K0[b] && rec[kVbMeta + 1] == m.ks[b] && m.K0[b] % 16 == 0, "%s: block meta", name);
-    maxw = std::max(maxw, m.R[b] - m.K0[b]);
-    for (int r = 0; r < 16; r++) {
-      const int y = 16 * b + r;
-      if (y >= ny) continue;
-      int64_t a[3] = {0, 0, 0};
-      for (int t = 0; t < m.ks[b]; t++)
-        for (int l = 0; l < 64; l++) {
-          if ((l & 15) != r) continue;
-          for (int j = 0; j < 16; j++) {
-            const int li = m.K0[b] + 64 * t + mfma_i8_k(l, j);
-            for (int q = 0; q < 3; q++) {
-              const int64_t w = frag_byte(m.arec, (size_t)b * kRec + (size_t)t * 3 * 256, q, l, j);
-              if (w && li >= nl) CHECK(false, "%s: weight past the list", name);
-              if (li < nl) a[q] += w * (px[m.rows[li]] - 128);
-            }
-          }
-        }
-      for (int q = 0; q < 3; q++) CHECK(llabs(a[q]) < (1ll << 31), "%s: limb sum exceeds int32", name);
-      const int64_t s = a[0] + 256 * a[1] + 65536 * a[2] + rec[kVbW128 + r];
-      int64_t ref = 0;
-      for (int j = 0; j < v.count[y]; j++) ref += (int64_t)qw(v.w[v.woff[y] + j]) * px[v.start[y] + j];
-      CHECK(s == ref, "%s: vb vertical y=%d %lld != %lld", name, y, (long long)s, (long long)ref);
-    }
-  }
-  printf("  %s: block windows %d blocks, max window %d rows ok\n", name, m.nblk, maxw);
-}
-
 static void check_h(const AxisTable &h, const char *name) {
   MfmaH m;
   if (!build_mfma_h(h, &m)) {
@@ -365,11 +221,8 @@ static void geometry(int W, int H, int tw, int th, uint32_t flags, const char *n
   AxisTable v, h;
   build_axis(P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &v);
   build_axis(P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &h);
-  check_v(v, name);
   check_h(h, name);
   check_vm(v, name);
-  check_vs(v, name);
-  check_vb(v, name);
 }
 
 int main() {

@@ -44,19 +44,15 @@ def _context_with(env):
                 os.environ[k] = v
 
 
-_ENV = {"FI_DISABLE_FUSED": "0", "FI_ENABLE_MFMA_RS": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0",
-        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0", "FI_VS_RS": "0", "FI_VB_RS": "0"}
+_ENV = {"FI_DISABLE_FUSED": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0",
+        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0"}
 PATHS = {
-    # k_rs_vb persistent row-ring block resample (LDS-DMA row ring, one block per iteration)
-    "vb": dict(_ENV, FI_VB_RS="1"),
-    # k_rs_vs persistent streaming MFMA resample (LDS-DMA ring, per-XCD work queues)
-    "vs": dict(_ENV, FI_VS_RS="1"),
     # default kernels: k_rs_vm streaming MFMA resample; k_sc_hmfma + k_sc_vq prescale; k_sc_score2
     "vm": dict(_ENV),
     # VALU fused resample (k_rs_fused); VALU vertical prescale + maps (k_sc_vmaps)
     "valu": dict(_ENV, FI_DISABLE_VM_RS="1", FI_DISABLE_SC_VQ="1"),
-    # exact-integer MFMA resample (opt-in) with the VALU horizontal prescale (k_sc_hrows)
-    "mfma": dict(_ENV, FI_ENABLE_MFMA_RS="1", FI_DISABLE_SC_MFMA="1"),
+    # default resample with the VALU horizontal prescale (k_sc_hrows)
+    "schrows": dict(_ENV, FI_DISABLE_SC_MFMA="1"),
     # generic kernels: two-pass resample; per-row prescale/maps kernels
     "generic": dict(_ENV, FI_DISABLE_FUSED="1", FI_DISABLE_SC_PREP="1", FI_DISABLE_SC_MFMA="1"),
 }
@@ -71,7 +67,7 @@ def rctx(request):
     c.close()
 
 
-EXPECTED_PATH = {"vb": "path_vb", "vs": "path_vs", "vm": "path_vm", "mfma": "path_mfma", "valu": "path_fused", "generic": "path_generic_v"}
+EXPECTED_PATH = {"vm": "path_vm", "schrows": "path_vm", "valu": "path_fused", "generic": "path_generic_v"}
 
 
 @pytest.mark.parametrize("W,H,opts", [

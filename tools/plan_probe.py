@@ -32,5 +32,5 @@ for rep in range(3):
     L.check(ctx.submit_device(arr, n)); L.check(ctx.wait(0))
     el = time.perf_counter() - t
     print(f"rep {rep}: {n} distinct sizes, wall {el*1e3:.1f} ms, host_plan {ctx.stats('host_plan')[0]:.1f} ms, batch {ctx.stats('batch')[0]:.2f} ms, resize {ctx.stats('resize')[0]:.2f} ms",
-          {p: ctx.stats(p)[1] for p in ['path_vm','path_fused','path_generic_v','path_generic_h','path_copy','path_mfma']})
+          {p: ctx.stats(p)[1] for p in ['path_vm','path_fused','path_generic_v','path_generic_h','path_copy']})
     print("status", sum(arr[i].status != 0 for i in range(n)))
