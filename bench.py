@@ -78,11 +78,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(W, H, options, budget_s=8.0, threads=None):
+def cpu_baseline(W, H, options, budget_s=8.0, threads=None, max_images=None):
     """The oracle restatement (oracle/fi_oracle.c) on the host cores: the same
     per-image work (IM resample -> smartcrop -> crop) on synthetic images of the
     same shape, one image per thread at a time (ctypes releases the GIL, the C
-    code has no shared state), for about ``budget_s`` seconds of wall time.
+    code has no shared state), for about ``budget_s`` seconds of wall time
+    (or until ``max_images`` images are done).
     ImageMagick itself runs its OpenMP loops over the host cores, so the
     baseline uses as many threads as this process' CPU share allows (16 on
     a one-GPU box; ``nproc`` shows the whole machine there)."""
@@ -126,9 +127,16 @@ def cpu_baseline(W, H, options, budget_s=8.0, threads=None):
     t0 = time.perf_counter()
     deadline = t0 + budget_s
 
+    lock = threading.Lock()
+    started = [0]
+
     def worker(i):
         k = i
         while time.perf_counter() < deadline:
+            with lock:
+                if max_images is not None and started[0] >= max_images:
+                    return
+                started[0] += 1
             one(k)
             counts[i] += 1
             k += threads
@@ -142,9 +150,29 @@ def cpu_baseline(W, H, options, budget_s=8.0, threads=None):
     n = sum(counts)
     mpix = n * W * H / 1e6
     return {"value": round(mpix / wall, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "images": n, "wall_s": round(wall, 3),
             "sample": f"{n} images {W}x{H} '{options}' through oracle/fi_oracle.c (IM restatement + smartcrop "
                       f"restatement + crop), {threads} threads, {wall:.1f} s wall; ImageMagick convert and "
                       f"python smartcrop.py are not installed on the GPU box"}
+
+
+def cfg4_cpu_baseline(items, n_sample=8, threads=None):
+    """The oracle on the first ``n_sample`` images of the cfg4 list, each
+    image's class timed on its own (``cpu_baseline`` with max_images =
+    threads, so every thread does one image): Mpix / summed measured wall."""
+    mpix = wall = 0.0
+    cores = 0
+    done = 0
+    for W, H, k in items[:n_sample]:
+        r = cpu_baseline(W, H, CFG4_OPS[k], budget_s=30.0, threads=threads, max_images=threads or 16)
+        mpix += r["images"] * W * H / 1e6
+        wall += r["wall_s"]
+        cores = max(cores, r["cores"])
+        done += r["images"]
+    return {"value": round(mpix / wall, 4) if wall > 0 else None, "unit": "Mpix/s", "cores": cores,
+            "kind": "port", "images": done, "wall_s": round(wall, 3),
+            "sample": f"{done} images of the first {n_sample} cfg4 (size, op) classes through oracle/fi_oracle.c, "
+                      f"{cores} threads (one image per thread per class), {wall:.1f} s measured wall"}
 
 
 def main():
@@ -322,10 +350,19 @@ def run_cfg4(args, rank, world, local_rank, comm):
     from flyimg_amd.processor import ImageProcessor, OptionsBag
     from flyimg_amd.runtime import Context
     from flyimg_amd.runtime import plan as fi_plan
+    from flyimg_amd.runtime import plan_bytes
 
     n_total = args.images or 65536
     items = cfg4_list(n_total)
-    shard = shard_lpt([float(W) * H for W, H, _ in items], world)[rank]
+    # greedy LPT by SURVEY 8(e) B_img (the bytes the resample reads + writes),
+    # planned per (size, op) class
+    op_of = {}
+    for W, H, k in items:
+        if (W, H, k) not in op_of:
+            op_of[(W, H, k)] = ImageProcessor(OptionsBag(CFG4_OPS[k]), W, H).to_op()
+    keys = list(op_of)
+    b_of = dict(zip(keys, plan_bytes([(W, H, op_of[(W, H, k)]) for W, H, k in keys])))
+    shard = shard_lpt([float(max(b_of[it], 1)) for it in items], world)[rank]
     ctx = Context(int(os.environ.get("FI_BENCH_DEVICE", local_rank)))  # override: rehearsal of N ranks on one GPU
     gather = RecordGather(comm, ctx)
     sizes = sorted({(W, H) for W, H, _ in items})
@@ -431,7 +468,7 @@ def run_cfg4(args, rank, world, local_rank, comm):
                 "images_total": n_total, "size_classes": len(sizes),
                 "mean_mpix_per_image": round(mpix / args.steps / n_total, 3),
                 "ops": CFG4_OPS, "batch": B,
-                "parallelism": f"dp{world} (LPT shards by input bytes, RCCL gather of result records)",
+                "parallelism": f"dp{world} (LPT shards by B_img, RCCL gather of result records)",
             },
             "roofline": {
                 "bound": "hbm",
@@ -451,22 +488,7 @@ def run_cfg4(args, rank, world, local_rank, comm):
             "failed_images": sum(v["bad"] for v in allv),
         }
         if not args.no_cpu_baseline:
-            try:
-                # the oracle on the first images of the list (bounded sample)
-                cb = None
-                for W, H, k in items[:8]:
-                    r = cpu_baseline(W, H, CFG4_OPS[k], budget_s=2.0, max_images=1)
-                    if cb is None:
-                        cb = {"mpix": 0.0, "s": 0.0, "n": 0}
-                    cb["mpix"] += W * H / 1e6
-                    cb["s"] += W * H / 1e6 / r["value"]
-                    cb["n"] += 1
-                result["cpu_baseline"] = {"value": round(cb["mpix"] / cb["s"], 4), "unit": "Mpix/s", "cores": 1,
-                                          "kind": "port",
-                                          "sample": f"first {cb['n']} images of the cfg4 list through "
-                                                    f"oracle/fi_oracle.c, single thread, {cb['s']:.1f} s"}
-            except Exception as e:  # noqa: BLE001
-                result["cpu_baseline"] = {"value": None, "error": repr(e)}
+            result["cpu_baseline"] = cfg4_cpu_baseline(items)
         print(json.dumps(result), flush=True)
     ctx.free(pool)
     for d in dst:

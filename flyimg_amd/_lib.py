@@ -35,6 +35,7 @@ FI_OP_SMARTCROP_APPLY = 1 << 9
 FI_OP_UNSHARP = 1 << 10
 FI_OP_SHARPEN = 1 << 11
 FI_OP_BLUR = 1 << 12
+FI_SRC_PSEUDOCLASS = 1 << 13  # IM PseudoClass source (palette / gray): Mitchell (resize.c)
 
 GRAVITY = {
     "NorthWest": 1, "North": 2, "NorthEast": 3, "West": 4, "Center": 5,
@@ -132,6 +133,7 @@ def lib():
     L.fi_destroy.argtypes = [vp]
     L.fi_destroy.restype = None
     L.fi_plan.argtypes = [P(FiImage), i32]
+    L.fi_plan_bytes.argtypes = [P(FiImage), i32, P(i64)]
     L.fi_process_batch.argtypes = [vp, P(FiImage), i32]
     L.fi_process_batch_device.argtypes = [vp, P(FiImage), i32]
     L.fi_submit_batch_device.argtypes = [vp, P(FiImage), i32]

@@ -14,8 +14,11 @@ ImageHandler::processNewImage end to end for a batch of encoded images.
            (IM's own JPEG coder is libjpeg as well).  Images with alpha are
            written as PNG.
 
-Gray (L) and palette sources are expanded to RGB / RGBA before the GPU
-(IM would keep a gray JPEG gray: the channels are equal either way).
+Gray (L), bilevel and palette sources are expanded to RGB / RGBA before the
+GPU (IM would keep a gray JPEG gray: the channels are equal either way), and
+flagged FI_SRC_PSEUDOCLASS: IM's readers give them a colormap (1-component
+JPEG, palette / 8-bit gray PNG, GIF), so ResizeImage filters them with
+Mitchell instead of Lanczos (resize.c).
 """
 from __future__ import annotations
 
@@ -28,16 +31,28 @@ from . import _lib as L
 from .processor import ExecFailedException, ExtractProcessor, ImageProcessor, OptionsBag, _empty
 
 
-def decode(blob: bytes) -> np.ndarray:
-    """Encoded bytes -> HWC uint8 (RGB, or RGBA when the file has alpha),
-    EXIF orientation applied (-auto-orient)."""
+# Pillow modes whose IM reading is a PseudoClass image: bilevel, 8-bit gray and
+# palette (16-bit gray "I;16" / "I" stays DirectClass, depth > 8)
+PSEUDOCLASS_MODES = ("1", "L", "P")
+
+
+def decode_ex(blob: bytes):
+    """Encoded bytes -> (HWC uint8 RGB, or RGBA when the file has alpha, EXIF
+    orientation applied (-auto-orient); True when IM would read a PseudoClass
+    image)."""
     from PIL import Image, ImageOps
 
     im = Image.open(io.BytesIO(blob))
     im = ImageOps.exif_transpose(im)
+    pseudo = im.mode in PSEUDOCLASS_MODES
     alpha = im.mode in ("RGBA", "LA", "PA") or (im.mode == "P" and "transparency" in im.info)
     im = im.convert("RGBA" if alpha else "RGB")
-    return np.asarray(im)
+    return np.asarray(im), pseudo
+
+
+def decode(blob: bytes) -> np.ndarray:
+    """decode_ex without the class flag."""
+    return decode_ex(blob)[0]
 
 
 def encode(pixels: np.ndarray, quality: int = 90) -> bytes:
@@ -65,15 +80,18 @@ class CodecPipeline:
     def process(self, blobs: list[bytes], options: list[str]):
         """Returns (encoded outputs, fi_image records); a failed image raises
         ExecFailedException as Processor::execute does."""
-        pixels = list(self.pool.map(decode, blobs))
+        decoded = list(self.pool.map(decode_ex, blobs))
         srcs, ops, quality = [], [], []
-        for img, opts in zip(pixels, options):
+        for (img, pseudo), opts in zip(decoded, options):
             bag = OptionsBag(opts)
             img = ExtractProcessor.extract(bag, img)
             h, w = img.shape[:2]
             q = bag.get_option("quality")
             quality.append(int(q) if not _empty(q) else 90)
-            ops.append(ImageProcessor(bag, w, h).to_op())
+            op = ImageProcessor(bag, w, h).to_op()
+            if pseudo:
+                op.flags |= L.FI_SRC_PSEUDOCLASS
+            ops.append(op)
             srcs.append(np.ascontiguousarray(img))
         outs, recs, rc = self.ctx.process(srcs, ops)
         for i, r in enumerate(recs):

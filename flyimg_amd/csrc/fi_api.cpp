@@ -2174,6 +2174,29 @@ int fi_plan(fi_image *imgs, int32_t n) {
   return first;
 }
 
+int fi_plan_bytes(const fi_image *imgs, int32_t n, int64_t *bytes) {
+  if (n < 0 || (n > 0 && (!imgs || !bytes))) return set_err(FI_EINVAL, "bad arguments");
+  int first = FI_OK;
+  for (int i = 0; i < n; i++) {
+    ImPlan p;
+    const int rc = plan_im(imgs[i], &p);
+    if (rc != FI_OK) {
+      bytes[i] = -1;
+      if (first == FI_OK) first = set_err(rc, "image %d: %s", i, p.err.c_str());
+      continue;
+    }
+    int64_t rows = p.eh;  // no resample: the extent window's rows are copied
+    if (p.resize) {
+      AxisTable t;
+      build_axis(p.filter, p.yf, p.sh, p.th, p.ey0, p.ey0 + p.eh, p.sample, p.H, &t);
+      rows = t.touched;
+    }
+    bytes[i] = rows * (int64_t)p.W * p.C + (int64_t)p.out_w * p.out_h * p.out_c +
+               ((imgs[i].flags & FI_OP_SMARTCROP) ? 16 : 0);
+  }
+  return first;
+}
+
 int fi_process_batch_device(fi_ctx *c, fi_image *imgs, int32_t n) {
   if (!c || n < 0 || (n > 0 && !imgs)) return set_err(FI_EINVAL, "bad arguments");
   if (n == 0) return FI_OK;

@@ -121,9 +121,10 @@ int plan_im(const fi_image &img, ImPlan *p) {
   if (p->resize) {
     p->xf = (double)p->tw / (double)p->sw;
     p->yf = (double)p->th / (double)p->sh;
-    // ResizeImage with the default filter: Mitchell for matte (alpha) images
-    // and enlargements, Lanczos otherwise
-    p->filter = (matte || (p->xf * p->yf) > 1.0) ? kFilterMitchell : kFilterLanczos;
+    // ResizeImage with the default filter (resize.c): Mitchell for PseudoClass
+    // (palette / gray) and matte (alpha) sources and for enlargements, Lanczos otherwise
+    const bool pseudo = (f & FI_SRC_PSEUDOCLASS) != 0;
+    p->filter = (matte || pseudo || (p->xf * p->yf) > 1.0) ? kFilterMitchell : kFilterLanczos;
     p->hfirst = p->xf > p->yf;
   }
   p->ex0 = p->ey0 = 0;

@@ -278,14 +278,17 @@ class ExtractProcessor:
         return image[y:y + h, x:x + w]
 
 
-def process_new_image(ctx, options: str, image):
+def process_new_image(ctx, options: str, image, pseudo_class: bool = False):
     """ImageHandler::processNewImage for the GPU path: ExtractProcessor ->
-    ImageProcessor -> SmartCropProcessor on one decoded RGB8 image.  Returns
-    (pixels, record)."""
+    ImageProcessor -> SmartCropProcessor on one decoded RGB8 image
+    (``pseudo_class``: IM would have read a palette / gray PseudoClass image,
+    codec.decode_ex).  Returns (pixels, record)."""
     bag = OptionsBag(options)
     image = ExtractProcessor.extract(bag, image)
     h, w = image.shape[:2]
     op = ImageProcessor(bag, w, h).to_op()
+    if pseudo_class:
+        op.flags |= L.FI_SRC_PSEUDOCLASS
     outs, recs, rc = ctx.process([image], [op])
     if recs[0].status != L.FI_OK:
         msg = L.lib().fi_last_error()

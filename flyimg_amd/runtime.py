@@ -53,6 +53,20 @@ def plan(width: int, height: int, op: Op):
     return img.out_w, img.out_h, img.out_channels
 
 
+def plan_bytes(sizes_ops):
+    """fi_plan_bytes: SURVEY 8(e) B_img (algorithmic HBM bytes) of each
+    (width, height, Op); -1 where the image does not plan."""
+    n = len(sizes_ops)
+    arr = (L.FiImage * max(n, 1))()
+    for i, (w, h, op) in enumerate(sizes_ops):
+        a = arr[i]
+        a.src_w, a.src_h, a.src_stride, a.src_channels = w, h, w * 3, 3
+        _fill(a, op)
+    out = (ctypes.c_int64 * max(n, 1))()
+    L.lib().fi_plan_bytes(arr, n, out)  # per-image -1 on failure; the caller decides
+    return [int(out[i]) for i in range(n)]
+
+
 class Context:
     def __init__(self, device: int = 0):
         self._lib = L.lib()

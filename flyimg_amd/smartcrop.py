@@ -104,13 +104,20 @@ def main(argv=None) -> int:
     options = parse_argument(argv)
     image = PIL.Image.open(options.inputfile)
     if image.mode not in ("RGB", "RGBA"):
+        # the same note on stderr, without a newline (smartcrop.py:357-362);
+        # SmartCropProcessor runs the command with 2>&1
+        sys.stderr.write("{1} convert from mode='{0}' to mode='RGB' ".format(image.mode, options.inputfile))
         new_image = PIL.Image.new("RGB", image.size)
         new_image.paste(image)
         image = new_image
+    if image.mode == "RGBA":
+        # the reference passes RGBA through and its analysis then fails
+        # (``r, g, b = image.split()``, smartcrop.py:17 / :251)
+        raise ValueError("too many values to unpack (expected 3)")
     arr = np.asarray(image)
-    if arr.ndim != 3 or arr.shape[2] != 3:
-        raise ValueError("smartcrop expects an RGB image")
     w, h = 100, int(options.height / options.width * 100)
+    if h == 0:
+        raise ZeroDivisionError("float division by zero")  # crop(): min(W / width, H / height)
     xywh = (ctypes.c_int32 * 4)()
     score = ctypes.c_double()
     arr = np.ascontiguousarray(arr)

@@ -65,6 +65,10 @@ extern "C" {
 #define FI_OP_UNSHARP (1u << 10)       /* -unsharp RxS+gain+threshold (unsh_)               */
 #define FI_OP_SHARPEN (1u << 11)       /* -sharpen RxS (sh_)                                */
 #define FI_OP_BLUR (1u << 12)          /* -blur RxS (blr_)                                  */
+/* The source is an IM PseudoClass image (palette PNG/GIF, 8-bit gray PNG,
+ * 1-component JPEG -- IM's readers give them a colormap): ResizeImage's
+ * default filter is then Mitchell, not Lanczos (resize.c). */
+#define FI_SRC_PSEUDOCLASS (1u << 13)
 
 /* ImageMagick GravityType values used by -gravity (parameters.yml:99). */
 #define FI_GRAVITY_NORTHWEST 1
@@ -161,6 +165,12 @@ void fi_destroy(fi_ctx *ctx);
 /* Geometry only (no pixel work, no GPU): fills out_w/out_h/out_channels/
  * out_stride for each image; status per image.  Returns FI_OK if all ok. */
 int fi_plan(fi_image *imgs, int32_t n);
+/* Per-image algorithmic HBM bytes of the hot path (SURVEY.md 8(d)/(e)
+ * B_img = R_touched * W_in * C_in + out_w * out_h * out_c + 16 when
+ * FI_OP_SMARTCROP), R_touched = source rows with a non-zero vertical tap
+ * after the ThumbnailImage sample step.  The multi-GPU sharder balances
+ * these (greedy LPT).  bytes[i] = -1 for an image that does not plan. */
+int fi_plan_bytes(const fi_image *imgs, int32_t n, int64_t *bytes);
 
 /* Host buffers: H2D -> kernels -> D2H.  Synchronous. */
 int fi_process_batch(fi_ctx *ctx, fi_image *imgs, int32_t n);

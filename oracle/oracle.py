@@ -159,6 +159,7 @@ def im_gravity_offset(W, H, ew, eh, gravity=5):
 
 FLAG_THUMBNAIL, FLAG_FILL, FLAG_SHRINK, FLAG_EXTENT, FLAG_GRAY, FLAG_ROTATE = 1, 2, 4, 8, 16, 32
 FLAG_MONO = 64  # -monochrome (B7); implies gray
+FLAG_PSEUDOCLASS = 128  # PseudoClass source (palette / gray): ResizeImage's Mitchell rule (resize.c)
 CONV_UNSHARP, CONV_SHARPEN, CONV_BLUR = 1, 2, 4  # forwarded convolutions (ImageProcessor.php:303-315)
 
 

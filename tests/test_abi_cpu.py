@@ -141,3 +141,30 @@ def test_php_ffi_cdef_matches_header():
     for name, proto in pp.items():
         assert proto == hp[name], (proto, hp[name])
     assert pf == hf
+
+
+def test_codec_decode_ex_flags_pseudoclass_modes():
+    """codec.decode_ex: bilevel, 8-bit gray and palette sources are IM
+    PseudoClass images (Mitchell); RGB / RGBA / 16-bit gray are not."""
+    import io
+
+    import numpy as np
+    from PIL import Image
+
+    from flyimg_amd.codec import decode_ex
+
+    rgb = (np.arange(32 * 24 * 3) % 251).astype(np.uint8).reshape(24, 32, 3)
+    im = Image.fromarray(rgb)
+    cases = {"1": True, "L": True, "P": True, "RGB": False, "RGBA": False}
+    for mode, want in cases.items():
+        buf = io.BytesIO()
+        im.convert(mode).save(buf, "PNG")
+        px, pseudo = decode_ex(buf.getvalue())
+        assert pseudo == want, mode
+        assert px.shape[:2] == (24, 32) and px.shape[2] in (3, 4)
+    buf = io.BytesIO()
+    im.convert("L").save(buf, "JPEG")
+    assert decode_ex(buf.getvalue())[1] is True
+    buf = io.BytesIO()
+    Image.fromarray((np.arange(24 * 32) * 60).astype(np.uint16).reshape(24, 32)).save(buf, "PNG")
+    assert decode_ex(buf.getvalue())[1] is False  # 16-bit gray: DirectClass

@@ -133,3 +133,25 @@ def test_im_sample_pre_step_geometry():
         assert orc.lib().or_im_thumbnail_uses_sample(W, H, ow, oh) == 1
     assert orc.im_meta_geometry(1920, 1080, 500, 0, shrink_only=True) == (500, 281)
     assert orc.im_meta_geometry(3840, 2160, 512, 512, fill=True) == (910, 512)
+
+
+def test_pseudoclass_flag_selects_mitchell():
+    """FLAG_PSEUDOCLASS: ResizeImage's filter rule for PseudoClass sources
+    (resize.c): the downscale equals the Mitchell result an enlargement-free
+    matte-free image otherwise never gets, and differs from Lanczos."""
+    import numpy as np
+
+    from flyimg_amd.synth import synth_rgb
+    from oracle import oracle as orc
+
+    src = synth_rgb(320, 240, 9)
+    base = orc.FLAG_THUMBNAIL | orc.FLAG_SHRINK
+    m = orc.im_convert(src, 100, 0, base | orc.FLAG_PSEUDOCLASS)
+    lz = orc.im_convert(src, 100, 0, base)
+    assert m.shape == lz.shape == (75, 100, 3)
+    assert np.abs(m.astype(int) - lz.astype(int)).max() > 1
+    # an RGBA (matte) source already takes Mitchell: the flag changes nothing there
+    rgba = np.dstack([src, np.full(src.shape[:2], 255, np.uint8)])
+    a = orc.im_convert(rgba, 100, 0, base)
+    b = orc.im_convert(rgba, 100, 0, base | orc.FLAG_PSEUDOCLASS)
+    assert np.array_equal(a, b)
