@@ -469,6 +469,7 @@ def run_cfg4(args, rank, world, local_rank, comm):
                 "mean_mpix_per_image": round(mpix / args.steps / n_total, 3),
                 "ops": CFG4_OPS, "batch": B,
                 "parallelism": f"dp{world} (LPT shards by B_img, RCCL gather of result records)",
+                "record_gather": gather.backend,
             },
             "roofline": {
                 "bound": "hbm",

@@ -161,6 +161,7 @@ struct fi_ctx {
   hipStream_t sc_stream = nullptr;  // smartcrop stage + crop apply + readback of a batch (waits for its resample)
   std::mutex mu;
   DevBuf arena, work, io;
+  DevBuf gather;  // RCCL record gather staging
   void *pinned = nullptr;
   size_t pinned_cap = 0;
   bool timing = false;
@@ -2138,7 +2139,7 @@ void fi_destroy(fi_ctx *c) {
   (void)drain(c);
   sync_streams(c);
   if (c->comm) ncclCommDestroy(c->comm);
-  for (DevBuf *b : {&c->arena, &c->work, &c->io})
+  for (DevBuf *b : {&c->arena, &c->work, &c->io, &c->gather})
     if (b->p) (void)hipFree(b->p);
   if (c->pinned) (void)hipHostFree(c->pinned);
   for (Slot &sl : c->slots) {
@@ -2498,20 +2499,24 @@ int fi_rccl_gather_records(fi_ctx *c, const fi_record *send, int32_t count, fi_r
   HIP_TRY(hipSetDevice(c->device));
   const size_t bytes = sizeof(fi_record) * (size_t)count;
   const size_t total = bytes * (1 + (c->rank == 0 ? c->world : 0));
-  int rc = ensure(c, &c->io, total + 256);
+  int rc = ensure(c, &c->gather, total + 256);  // its own buffer: in-flight batches never read it
   if (rc) return rc;
-  uint8_t *sb = (uint8_t *)c->io.p, *rb = sb + bytes;
+  uint8_t *sb = (uint8_t *)c->gather.p, *rb = sb + bytes;
   HIP_TRY(hipMemcpyAsync(sb, send, bytes, hipMemcpyHostToDevice, c->stream));
+  if (c->rank == 0) HIP_TRY(hipMemcpyAsync(rb, sb, bytes, hipMemcpyDeviceToDevice, c->stream));
+  // nothing between ncclGroupStart and ncclGroupEnd may return early: the
+  // group is always closed, then the first error is reported
   ncclResult_t r = ncclGroupStart();
+  if (r != ncclSuccess) return set_err(FI_EDEVICE, "ncclGroupStart: %s", ncclGetErrorString(r));
   if (c->rank == 0) {
-    HIP_TRY(hipMemcpyAsync(rb, sb, bytes, hipMemcpyDeviceToDevice, c->stream));
     for (int p = 1; p < c->world && r == ncclSuccess; p++)
       r = ncclRecv(rb + bytes * p, bytes, ncclUint8, p, c->comm, c->stream);
-  } else if (r == ncclSuccess) {
+  } else {
     r = ncclSend(sb, bytes, ncclUint8, 0, c->comm, c->stream);
   }
-  if (r == ncclSuccess) r = ncclGroupEnd();
-  if (r != ncclSuccess) return set_err(FI_EDEVICE, "RCCL gather: %s", ncclGetErrorString(r));
+  const ncclResult_t re = ncclGroupEnd();
+  if (r != ncclSuccess || re != ncclSuccess)
+    return set_err(FI_EDEVICE, "RCCL gather: %s", ncclGetErrorString(r != ncclSuccess ? r : re));
   if (c->rank == 0 && recv)
     HIP_TRY(hipMemcpyAsync(recv, rb, bytes * c->world, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));

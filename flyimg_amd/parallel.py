@@ -152,8 +152,15 @@ class RecordGather:
                 ok = int(L.lib().fi_rccl_init(ctx.h, comm.rank, comm.world, data) == 0)
             else:
                 ok = 0
-            # every rank takes the same backend: RCCL only if it came up everywhere
-            self.backend = "rccl" if all(comm.allgather_obj(ok)) else "comm"
+            # every rank takes the same decision: a world > 1 run whose RCCL does not
+            # come up everywhere fails (FI_RECORD_GATHER=comm selects the
+            # control-plane gather explicitly) -- no silent fallback
+            oks = comm.allgather_obj(ok)
+            if not all(oks):
+                raise RuntimeError(f"RCCL record gather did not come up on ranks "
+                                   f"{[r for r, o in enumerate(oks) if not o]} (set FI_RECORD_GATHER=comm "
+                                   f"to gather through the control plane)")
+            self.backend = "rccl"
         else:
             self.backend = "comm"
 

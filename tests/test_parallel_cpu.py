@@ -177,3 +177,52 @@ def test_file_comm_close_waits_for_every_rank(tmp_path):
     out = _run(_close_rank, 4, str(tmp_path))
     for r in range(4):
         assert out[r][4] is None, out[r][4]
+
+
+class _StubLib:
+    """fi_rccl_* stand-ins: RCCL comes up on every rank except ``bad``."""
+
+    def __init__(self, rank, bad):
+        self.rank, self.bad = rank, bad
+
+    def fi_rccl_get_unique_id(self, buf):
+        buf.raw = bytes(range(128))
+        return 0
+
+    def fi_rccl_init(self, h, rank, world, data):
+        return -5 if rank == self.bad else 0
+
+
+def _rccl_rank(rank, world, run_id, root, bad, q):
+    try:
+        from flyimg_amd import _lib as L
+
+        L.lib = lambda: _StubLib(rank, bad)  # this spawned process only
+
+        class Ctx:
+            h = None
+
+        comm = FileComm(rank, world, run_id=run_id, root=root, timeout=60)
+        try:
+            g = RecordGather(comm, Ctx())
+            res = g.backend
+        except RuntimeError as e:
+            res = "error: " + str(e)
+        comm.close()
+        q.put((rank, res, None, None, None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, None, None, repr(e)))
+
+
+@pytest.mark.parametrize("bad", [-1, 1])
+def test_record_gather_fails_loudly_when_rccl_is_down(bad):
+    """world > 1 with a context: RCCL on every rank, or every rank raises --
+    never a silent fallback to the control-plane gather."""
+    with tempfile.TemporaryDirectory() as root:
+        out = _run(_rccl_rank, 2, f"r{os.getpid()}{bad}", root, bad)
+    for r in range(2):
+        assert out[r][4] is None, out[r][4]
+        if bad < 0:
+            assert out[r][1] == "rccl"
+        else:
+            assert out[r][1].startswith("error: RCCL record gather did not come up on ranks [1]")
