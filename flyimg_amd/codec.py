@@ -63,7 +63,11 @@ def encode(pixels: np.ndarray, quality: int = 90) -> bytes:
     if ch in (2, 4):  # alpha survives: PNG
         Image.fromarray(pixels, "LA" if ch == 2 else "RGBA").save(buf, "PNG")
     else:
-        Image.fromarray(pixels, "L" if ch == 1 else "RGB").save(buf, "JPEG", quality=int(quality))
+        # IM 6 coders/jpeg.c: without -sampling-factor, quality >= 90 writes 1x1
+        # (4:4:4) chroma and lower qualities 2x2 (4:2:0).  (MozJPEG's cjpeg, the
+        # reference's path when it is installed, always uses 2x2.)
+        Image.fromarray(pixels, "L" if ch == 1 else "RGB").save(
+            buf, "JPEG", quality=int(quality), subsampling=0 if int(quality) >= 90 else 2)
     return buf.getvalue()
 
 

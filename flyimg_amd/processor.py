@@ -197,9 +197,10 @@ class ImageProcessor:
             op.target_w, op.target_h = int(w), int(h)
             op.flags |= L.FI_GEOM_FILL | L.FI_OP_EXTENT
             g = str(o.get_option("gravity"))
-            if g not in L.GRAVITY:
+            code = {k.lower(): v for k, v in L.GRAVITY.items()}.get(g.lower())  # IM: case-insensitive
+            if code is None:
                 raise ExecFailedException(f"unsupported gravity {g!r}")
-            op.gravity = L.GRAVITY[g]
+            op.gravity = code
         elif not _empty(w) or not _empty(h):
             op.target_w = int(w) if not _empty(w) else 0
             op.target_h = int(h) if not _empty(h) else 0

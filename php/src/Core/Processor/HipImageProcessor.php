@@ -17,6 +17,15 @@ use Core\Exception\ExecFailedException;
  * a command line.  Decode/encode stay on the host (djpeg -> PPM -> GPU ->
  * cjpeg, as ImageProcessor.php:204-209 pipes TGA into MozJPEG).
  * Errors raise ExecFailedException, as Processor::execute does.
+ *
+ * Anything the GPU path does not reproduce goes to the parent's convert
+ * pipeline unchanged (gpuEligible): non-JPEG sources (PNG / GIF / WebP,
+ * palette and alpha inputs), JPEGs with an EXIF orientation other than 1
+ * (the parent's -auto-orient, :78), gray (1-component) JPEGs, outputs the
+ * parent would not write with MozJPEG (webp / png / gif, mozjpeg off), and
+ * options IM would honour or reject that the GPU path does not implement
+ * (-background, colorspaces other than sRGB / RGB / Gray, gravities IM
+ * does not know, non-integral -rotate).
  */
 class HipImageProcessor extends ImageProcessor
 {
@@ -65,8 +74,16 @@ class HipImageProcessor extends ImageProcessor
     {
         $this->sourceImageInfo = $outputImage->getInputImage()->sourceImageInfo();
         $this->options = $outputImage->getInputImage()->optionsBag();
+        $path = $this->sourceImageInfo->path();
+        if (!$this->gpuEligible($outputImage, $path)) {
+            return parent::processNewImage($outputImage);
+        }
+        $decoded = $this->decodeRgb($path);
+        if ($decoded === null) {  // not a 3-component JPEG after all
+            return parent::processNewImage($outputImage);
+        }
         $ffi = self::lib();
-        [$w, $h, $rgb] = $this->decodeRgb($this->getSourceImagePath($outputImage));
+        [$w, $h, $rgb] = $decoded;
 
         $img = $ffi->new('fi_image');
         $src = $ffi->new("uint8_t[" . strlen($rgb) . "]", false);
@@ -89,6 +106,87 @@ class HipImageProcessor extends ImageProcessor
         \FFI::free($src);
         \FFI::free($dst);
         return $outputImage;
+    }
+
+    /** Case-insensitive gravity lookup (IM parses -gravity case-insensitively); null = unknown. */
+    private static function gravityCode(string $g): ?int
+    {
+        foreach (self::GRAVITY as $name => $code) {
+            if (strcasecmp($name, $g) === 0) {
+                return $code;
+            }
+        }
+        return null;
+    }
+
+    /** Whether the GPU path reproduces the parent's output for this request. */
+    private function gpuEligible(OutputImage $outputImage, string $path): bool
+    {
+        if (!is_executable(self::MOZJPEG_COMMAND) || !$outputImage->isOutputMozJpeg() ||
+            $outputImage->isOutputWebP()) {
+            return false;                                     // encoder choice of calculateQuality (:195-217)
+        }
+        $head = @file_get_contents($path, false, null, 0, 65536);
+        if (!is_string($head) || strncmp($head, "\xFF\xD8\xFF", 3) !== 0) {
+            return false;                                     // not a JPEG
+        }
+        if (self::jpegOrientation($head) > 1) {
+            return false;                                     // -auto-orient would transform it
+        }
+        if (!empty($this->options->getOption('background'))) {
+            return false;
+        }
+        $clsp = strtolower((string)$outputImage->extractKey('colorspace'));
+        if (!in_array($clsp, ['', 'srgb', 'rgb', 'gray'], true)) {
+            return false;
+        }
+        if (self::gravityCode((string)$this->options->getOption('gravity')) === null) {
+            return false;
+        }
+        $rotate = (string)$this->options->getOption('rotate');
+        if ($rotate !== '' && (!is_numeric($rotate) || fmod((float)$rotate, 90.0) != 0.0)) {
+            return false;
+        }
+        return true;
+    }
+
+    /** EXIF orientation (tag 0x0112 of IFD0 in the APP1 Exif segment) of a JPEG head; 0 = none. */
+    private static function jpegOrientation(string $jpg): int
+    {
+        $n = strlen($jpg);
+        for ($p = 2; $p + 4 <= $n;) {
+            if (ord($jpg[$p]) !== 0xFF) {
+                return 0;
+            }
+            $marker = ord($jpg[$p + 1]);
+            if ($marker === 0xDA || $marker === 0xD9) {
+                return 0;                                     // start of scan: no Exif before it
+            }
+            $len = (ord($jpg[$p + 2]) << 8) | ord($jpg[$p + 3]);
+            if ($marker === 0xE1 && substr($jpg, $p + 4, 6) === "Exif\0\0") {
+                $t = $p + 10;                                 // TIFF header
+                $le = substr($jpg, $t, 2) === 'II';
+                $u16 = function (int $o) use ($jpg, $le): int {
+                    $v = unpack($le ? 'v' : 'n', substr($jpg, $o, 2));
+                    return $v === false ? 0 : $v[1];
+                };
+                $u32 = function (int $o) use ($jpg, $le): int {
+                    $v = unpack($le ? 'V' : 'N', substr($jpg, $o, 4));
+                    return $v === false ? 0 : $v[1];
+                };
+                $ifd = $t + $u32($t + 4);
+                $count = $u16($ifd);
+                for ($i = 0; $i < $count && $ifd + 14 + 12 * $i <= $n; $i++) {
+                    $e = $ifd + 2 + 12 * $i;
+                    if ($u16($e) === 0x0112) {
+                        return $u16($e + 8);
+                    }
+                }
+                return 0;
+            }
+            $p += 2 + $len;
+        }
+        return 0;
     }
 
     /** The fi_image equivalent of generateCommand()'s argv (:66-110). */
@@ -139,16 +237,20 @@ class HipImageProcessor extends ImageProcessor
         $img->target_w = $tw;
         $img->target_h = $th;
         $img->flags = $flags;
-        $img->gravity = self::GRAVITY[$this->options->getOption('gravity')] ?? 5;
+        $img->gravity = self::gravityCode((string)$this->options->getOption('gravity')) ?? 5;
         $img->rotate = $rotate;
         $img->smartcrop_w = 100;                                                // smartcrop.py CLI defaults
         $img->smartcrop_h = 100;
     }
 
-    /** Host decode to packed RGB8 (libjpeg-turbo's djpeg, PPM output). */
-    private function decodeRgb(string $path): array
+    /** Host decode to packed RGB8 (libjpeg-turbo's djpeg, PPM output); null for a
+     *  gray JPEG (PGM: IM reads it as a PseudoClass image -- the parent handles it). */
+    private function decodeRgb(string $path): ?array
     {
         $ppm = shell_exec('/opt/mozjpeg/bin/djpeg -pnm ' . escapeshellarg($path));
+        if (is_string($ppm) && strncmp($ppm, 'P5', 2) === 0) {
+            return null;
+        }
         if (!is_string($ppm) || !preg_match('/^P6\s+(\d+)\s+(\d+)\s+255\s/', $ppm, $m)) {
             throw new ExecFailedException("Command failed.\nThe exit code: decode\nThe last line of output: " . $path);
         }

@@ -168,3 +168,33 @@ def test_codec_decode_ex_flags_pseudoclass_modes():
     buf = io.BytesIO()
     Image.fromarray((np.arange(24 * 32) * 60).astype(np.uint16).reshape(24, 32)).save(buf, "PNG")
     assert decode_ex(buf.getvalue())[1] is False  # 16-bit gray: DirectClass
+
+
+def test_gravity_is_case_insensitive_and_unknown_rejected():
+    """IM parses -gravity case-insensitively (g_north == North); an unknown
+    gravity is an error, as convert's exit status would be."""
+    import pytest
+
+    from flyimg_amd import _lib as L
+    from flyimg_amd.processor import ExecFailedException, ImageProcessor, OptionsBag
+
+    for g in ("north", "NORTH", "North"):
+        op = ImageProcessor(OptionsBag(f"w_200,h_200,c_1,g_{g}"), 800, 500).to_op()
+        assert op.gravity == L.GRAVITY["North"]
+    with pytest.raises(ExecFailedException):
+        ImageProcessor(OptionsBag("w_200,h_200,c_1,g_Upwards"), 800, 500).to_op()
+
+
+def test_jpeg_encoder_chroma_sampling_follows_im_quality_rule():
+    """IM 6 jpeg.c: quality >= 90 -> 4:4:4, below -> 4:2:0 (no -sampling-factor)."""
+    import io
+
+    import numpy as np
+    from PIL import Image, JpegImagePlugin
+
+    from flyimg_amd.codec import encode
+
+    px = (np.arange(64 * 48 * 3) % 253).astype(np.uint8).reshape(48, 64, 3)
+    for q, want in ((90, 0), (95, 0), (89, 2), (75, 2)):
+        im = Image.open(io.BytesIO(encode(px, q)))
+        assert JpegImagePlugin.get_sampling(im) == want, q
