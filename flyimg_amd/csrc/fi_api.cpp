@@ -2122,8 +2122,14 @@ int fi_create(fi_ctx **out, int32_t device) {
   // 0.39 -> 2.06 ms, resize 2.47 -> 2.83 ms).
   bool sc_stream = false;
   if (const char *e = getenv("FI_SC_STREAM")) sc_stream = e[0] == '1';
+  // FI_SC_PRIO=1: the smartcrop stream at the highest priority, so its
+  // workgroups take CU slots as the resample's retire
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  const bool sc_prio = getenv("FI_SC_PRIO") && getenv("FI_SC_PRIO")[0] == '1';
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      (sc_stream && hipStreamCreateWithFlags(&c->sc_stream, hipStreamNonBlocking) != hipSuccess)) {
+      (sc_stream && (sc_prio ? hipStreamCreateWithPriority(&c->sc_stream, hipStreamNonBlocking, prio_hi)
+                             : hipStreamCreateWithFlags(&c->sc_stream, hipStreamNonBlocking)) != hipSuccess)) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return set_err(FI_EDEVICE, "hipStreamCreate failed");
