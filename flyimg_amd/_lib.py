@@ -134,6 +134,8 @@ def lib():
     L.fi_destroy.restype = None
     L.fi_plan.argtypes = [P(FiImage), i32]
     L.fi_plan_bytes.argtypes = [P(FiImage), i32, P(i64)]
+    L.fi_pixelate_regions.argtypes = [vp, vp, i32, i32, i32, i32, P(i32), i32]
+    L.fi_pixelate_regions_device.argtypes = [vp, vp, i32, i32, i32, i32, P(i32), i32]
     L.fi_process_batch.argtypes = [vp, P(FiImage), i32]
     L.fi_process_batch_device.argtypes = [vp, P(FiImage), i32]
     L.fi_submit_batch_device.argtypes = [vp, P(FiImage), i32]

@@ -67,6 +67,8 @@ size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16);
 int vm_read_stamps(uint64_t *out, int slots);
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
+// face-blur pixelation (fi_pixelate.hip)
+int launch_pix(hipStream_t s, int mode, const PixPass &P, const int32_t *ai, const double *ad);
 // fused vertical-first VALU resample (fi_fused.hip)
 int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
                  const int32_t *ai, const float *af, int hw_pitch, int max_taps, int max_nbytes);
@@ -162,6 +164,7 @@ struct fi_ctx {
   std::mutex mu;
   DevBuf arena, work, io;
   DevBuf gather;  // RCCL record gather staging
+  DevBuf pix;     // face-blur pixelation: lists + 10% scratch
   void *pinned = nullptr;
   size_t pinned_cap = 0;
   bool timing = false;
@@ -1944,6 +1947,101 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
 // ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
+// face-blur pixelation (fi_pixelate.hip): per box, the crop's 10% ScaleImage
+// into a Q16 scratch, then its 1000% ScaleImage onto the image at (X, Y).
+static int pixelate_device(fi_ctx *c, uint8_t *img, int w, int h, int64_t stride, int C, const int32_t *boxes,
+                           int nboxes) {
+  if (!img || w <= 0 || h <= 0 || (C != 1 && C != 3) || stride < (int64_t)w * C || nboxes < 0 ||
+      (nboxes > 0 && !boxes))
+    return set_err(FI_EINVAL, "bad pixelate arguments");
+  std::vector<int32_t> ti;
+  std::vector<double> td;
+  struct Box {
+    PixPass down, up;
+  };
+  std::vector<Box> plan;
+  size_t scratch = 0;
+  int first_bad = -1;
+  std::string why;
+  auto put = [&](const ScaleList &L, int32_t *off, int32_t *idx, int32_t *wt) {
+    *off = (int32_t)ti.size();
+    ti.insert(ti.end(), L.off.begin(), L.off.end());
+    *idx = (int32_t)ti.size();
+    ti.insert(ti.end(), L.idx.begin(), L.idx.end());
+    *wt = (int32_t)td.size();
+    td.insert(td.end(), L.w.begin(), L.w.end());
+  };
+  for (int b = 0; b < nboxes; b++) {
+    const int bx = boxes[4 * b], by = boxes[4 * b + 1], bw = boxes[4 * b + 2], bh = boxes[4 * b + 3];
+    if (bw <= 0 || bh <= 0 || bx < 0 || by < 0 || bx >= w || by >= h) {
+      first_bad = b;
+      why = "geometry does not contain image";
+      break;
+    }
+    const int rw = std::min(bw, w - bx), rh = std::min(bh, h - by);  // CropImage clip
+    const int dw = im_percent_size(rw, 10.0), dh = im_percent_size(rh, 10.0);
+    if (dw <= 0 || dh <= 0) {
+      first_bad = b;
+      why = "NegativeOrZeroImageSize (the 10% scale is empty)";
+      break;
+    }
+    const int uw = im_percent_size(dw, 1000.0), uh = im_percent_size(dh, 1000.0);
+    Box B{};
+    ScaleList L;
+    im_scale_rows(rh, dh, &L);
+    put(L, &B.down.yoff, &B.down.yidx, &B.down.yw);
+    im_scale_cols(rw, dw, &L);
+    put(L, &B.down.xoff, &B.down.xidx, &B.down.xw);
+    im_scale_rows(dh, uh, &L);
+    put(L, &B.up.yoff, &B.up.yidx, &B.up.yw);
+    im_scale_cols(dw, uw, &L);
+    put(L, &B.up.xoff, &B.up.xidx, &B.up.xw);
+    B.down.src8 = img + (int64_t)by * stride + (int64_t)bx * C;
+    B.down.sstride = stride;
+    B.down.iw = rw;
+    B.down.ih = rh;
+    B.down.ow = dw;
+    B.down.oh = dh;
+    B.down.C = C;
+    B.down.dst16 = (uint16_t *)(uintptr_t)(scratch + 1);  // tagged: resolved after upload
+    B.up.src16 = B.down.dst16;
+    B.up.iw = dw;
+    B.up.ih = dh;
+    B.up.ow = uw;
+    B.up.oh = uh;
+    B.up.C = C;
+    B.up.dst8 = img + (int64_t)by * stride + (int64_t)bx * C;
+    B.up.dstride = stride;
+    B.up.clip_w = w - bx;  // composite at (X, Y), clipped to the canvas
+    B.up.clip_h = h - by;
+    scratch += ((size_t)dw * dh * C * 2 + 255) / 256 * 256;
+    plan.push_back(B);
+  }
+  const size_t ti_bytes = ti.size() * 4, td_off = (ti_bytes + 255) / 256 * 256;
+  const size_t sc_off = (td_off + td.size() * 8 + 255) / 256 * 256;
+  int rc = ensure(c, &c->pix, sc_off + scratch + 256);
+  if (rc) return rc;
+  uint8_t *pb = (uint8_t *)c->pix.p;
+  rc = ensure_pinned(c, sc_off);
+  if (rc) return rc;
+  memcpy(c->pinned, ti.data(), ti_bytes);
+  memcpy((uint8_t *)c->pinned + td_off, td.data(), td.size() * 8);
+  if (sc_off) HIP_TRY(hipMemcpyAsync(pb, c->pinned, sc_off, hipMemcpyHostToDevice, c->stream));
+  const int32_t *ai = (const int32_t *)pb;
+  const double *ad = (const double *)(pb + td_off);
+  for (Box &B : plan) {
+    fix_ptr(B.down.dst16, pb + sc_off);
+    B.up.src16 = B.down.dst16;
+    launch_pix(c->stream, 0, B.down, ai, ad);
+    launch_pix(c->stream, 1, B.up, ai, ad);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));  // the pinned lists are reused by the next call
+  if (first_bad >= 0) return set_err(FI_EINVAL, "pixelate box %d: %s", first_bad, why.c_str());
+  return FI_OK;
+}
+
+// ---------------------------------------------------------------------------
 extern "C" {
 
 int32_t fi_abi_version(void) { return FI_ABI_VERSION; }
@@ -2145,7 +2243,7 @@ void fi_destroy(fi_ctx *c) {
   (void)drain(c);
   sync_streams(c);
   if (c->comm) ncclCommDestroy(c->comm);
-  for (DevBuf *b : {&c->arena, &c->work, &c->io, &c->gather})
+  for (DevBuf *b : {&c->arena, &c->work, &c->io, &c->gather, &c->pix})
     if (b->p) (void)hipFree(b->p);
   if (c->pinned) (void)hipHostFree(c->pinned);
   for (Slot &sl : c->slots) {
@@ -2179,6 +2277,36 @@ int fi_plan(fi_image *imgs, int32_t n) {
     }
   }
   return first;
+}
+
+int fi_pixelate_regions_device(fi_ctx *c, uint8_t *img, int32_t w, int32_t h, int32_t stride, int32_t channels,
+                               const int32_t *boxes, int32_t nboxes) {
+  if (!c) return set_err(FI_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  return pixelate_device(c, img, w, h, stride, channels, boxes, nboxes);
+}
+
+int fi_pixelate_regions(fi_ctx *c, uint8_t *img, int32_t w, int32_t h, int32_t stride, int32_t channels,
+                        const int32_t *boxes, int32_t nboxes) {
+  if (!c || !img || w <= 0 || h <= 0 || (channels != 1 && channels != 3) || stride < w * channels)
+    return set_err(FI_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  {
+    const int rc0 = drain(c);  // the io buffer may be read by in-flight batches
+    if (rc0) return rc0;
+  }
+  const int64_t pitch = (int64_t)w * channels;
+  int rc = ensure(c, &c->io, (size_t)pitch * h + 256);
+  if (rc) return rc;
+  uint8_t *d = (uint8_t *)c->io.p;
+  HIP_TRY(hipMemcpy2DAsync(d, pitch, img, stride, pitch, h, hipMemcpyHostToDevice, c->stream));
+  rc = pixelate_device(c, d, w, h, pitch, channels, boxes, nboxes);
+  // boxes before a rejected one are applied (each face is its own mogrify run)
+  HIP_TRY(hipMemcpy2DAsync(img, stride, d, pitch, pitch, h, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return rc;
 }
 
 int fi_plan_bytes(const fi_image *imgs, int32_t n, int64_t *bytes) {

@@ -202,6 +202,20 @@ constexpr int kVmOtileBytes = 16 * kVmOtilePitch * 2;
 constexpr int kVmOtile8Pitch = 64 * 3 + 4;     // 8-bit tile row (fast RGB path)
 constexpr int kVmOtile8Bytes = 16 * kVmOtile8Pitch;
 
+// fi_pixelate.hip: one ScaleImage pass of a face box (face-blur pixelation)
+struct PixPass {
+  const uint8_t *src8;    // MODE 0: the crop's first byte in the 8-bit image
+  const uint16_t *src16;  // MODE 1: the 10% image (Q16, pitch iw * C)
+  int64_t sstride;        // MODE 0: image row stride
+  int32_t iw, ih;         // input dims
+  uint16_t *dst16;        // MODE 0: the 10% image
+  uint8_t *dst8;          // MODE 1: the image at (X, Y)
+  int64_t dstride;
+  int32_t ow, oh, C;
+  int32_t clip_w, clip_h;  // MODE 1: writable extent right / below (X, Y)
+  int32_t yoff, yidx, xoff, xidx;  // ai offsets of the row / column lists (fi_plan.h ScaleList)
+  int32_t yw, xw;                  // ad offsets of their weights
+};
 struct ScParamsDev {
   double detail_weight, edge_radius, edge_weight, outside_importance;
   double saturation_bias, saturation_brightness_max, saturation_brightness_min,

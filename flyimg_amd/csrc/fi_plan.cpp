@@ -1021,4 +1021,97 @@ void sc_importance_table(const fi_smartcrop_params &P, double fw, double fh, int
     }
 }
 
+// ---- ScaleImage contribution lists (resize.c ScaleImage; oracle
+// or_im_scale_q16 is the literal loop) ----------------------------------------
+void im_scale_rows(int H, int oh, ScaleList *L) {
+  *L = ScaleList();
+  L->off.push_back(0);
+  if (oh == H) {  // rows copied (scanline = x_vector)
+    for (int y = 0; y < oh; y++) {
+      L->idx.push_back(y);
+      L->w.push_back(1.0);
+      L->off.push_back((int32_t)L->idx.size());
+    }
+    return;
+  }
+  int number_rows = 0, i = 0, cur = -1;
+  bool next_row = true;
+  double span_y = 1.0, scale_y = (double)oh / (double)H;
+  for (int y = 0; y < oh; y++) {
+    while (scale_y < span_y) {
+      if (next_row && number_rows < H) {
+        cur = i++;
+        number_rows++;
+      }
+      L->idx.push_back(cur);
+      L->w.push_back(scale_y);
+      span_y -= scale_y;
+      scale_y = (double)oh / (double)H;
+      next_row = true;
+    }
+    if (next_row && number_rows < H) {
+      cur = i++;
+      number_rows++;
+      next_row = false;
+    }
+    L->idx.push_back(cur);
+    L->w.push_back(span_y);
+    L->off.push_back((int32_t)L->idx.size());
+    scale_y -= span_y;
+    if (scale_y <= 0) {
+      scale_y = (double)oh / (double)H;
+      next_row = true;
+    }
+    span_y = 1.0;
+  }
+}
+
+void im_scale_cols(int W, int ow, ScaleList *L) {
+  *L = ScaleList();
+  std::vector<std::vector<std::pair<int32_t, double>>> col(ow);
+  if (ow == W) {
+    for (int x = 0; x < ow; x++) col[x].push_back({x, 1.0});
+  } else {
+    std::vector<std::pair<int32_t, double>> cur;  // additions to `pixel` since its last reset
+    bool next_column = false;
+    int t = 0;
+    double span_x = 1.0, scale_x = 0;
+    for (int x = 0; x < W; x++) {
+      scale_x = (double)ow / (double)W;
+      while (scale_x >= span_x) {
+        if (next_column) {
+          cur.clear();
+          t++;
+        }
+        cur.push_back({x, span_x});
+        if (t < ow) col[t] = cur;  // scale_scanline[t] = pixel
+        scale_x -= span_x;
+        span_x = 1.0;
+        next_column = true;
+      }
+      if (scale_x > 0) {
+        if (next_column) {
+          cur.clear();
+          next_column = false;
+          t++;
+        }
+        cur.push_back({x, scale_x});
+        span_x -= scale_x;
+      }
+    }
+    if (span_x > 0) cur.push_back({W - 1, span_x});
+    if (!next_column && t < ow) col[t] = cur;
+  }
+  L->off.push_back(0);
+  for (int x = 0; x < ow; x++) {
+    for (auto &e : col[x]) {
+      L->idx.push_back(e.first);
+      L->w.push_back(e.second);
+    }
+    L->off.push_back((int32_t)L->idx.size());
+  }
+}
+
+int im_percent_size(int size, double percent) { return (int)floor(percent * (double)size / 100.0 + 0.5); }
+
 }  // namespace fi

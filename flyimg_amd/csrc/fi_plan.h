@@ -160,4 +160,18 @@ void sc_importance_table(const fi_smartcrop_params &P, double fw, double fh, int
 int pil_coeffs(int in_size, float in0, float in1, int out_size, std::vector<int32_t> *bounds,
                std::vector<int32_t> *kk);
 
+// IM 6 ScaleImage (resize.c) as per-output contribution lists: output o is
+// sum_k w[k] * in[idx[k]], k in [off[o], off[o + 1]), accumulated from 0 in
+// list order -- exactly the additions ScaleImage makes (rows: the y_vector /
+// span.y loop; columns: the pixel / span.x loop, including which partial sums
+// it keeps).  Used by the face-blur pixelation (fi_pixelate.hip).
+struct ScaleList {
+  std::vector<int32_t> off, idx;
+  std::vector<double> w;
+};
+void im_scale_rows(int in_size, int out_size, ScaleList *L);
+void im_scale_cols(int in_size, int out_size, ScaleList *L);
+// ParseMetaGeometry's percentage size: floor(percent * size / 100 + 0.5)
+int im_percent_size(int size, double percent);
+
 }  // namespace fi

@@ -279,6 +279,35 @@ class ExtractProcessor:
         return image[y:y + h, x:x + w]
 
 
+class FaceDetectProcessor:
+    """FaceDetectProcessor.php:45-74 blurFaces: every line ``"x y w h"`` of the
+    facedetect output (face detection itself is out of scope: its output is
+    the input here) becomes one ``mogrify -gravity NorthWest -region WxH+X+Y
+    -scale 10% -scale 1000%`` on the output image -- fi_pixelate_regions, in
+    place, boxes in the output's order; lines that do not split into four
+    fields are skipped as the reference skips them."""
+
+    @staticmethod
+    def boxes(facedetect_output):
+        out = []
+        for line in facedetect_output:
+            g = str(line).split(" ")
+            if len(g) == 4:
+                out.append(tuple(int(v) for v in g))
+        return out
+
+    @staticmethod
+    def blur_faces(ctx, image, facedetect_output):
+        boxes = FaceDetectProcessor.boxes(facedetect_output)
+        if not boxes:
+            return image
+        rc = ctx.pixelate_regions(image, boxes)
+        if rc != L.FI_OK:
+            msg = L.lib().fi_last_error()
+            raise ExecFailedException("Command failed.\nThe exit code: %d\n%s" % (rc, msg.decode() if msg else ""))
+        return image
+
+
 def process_new_image(ctx, options: str, image, pseudo_class: bool = False):
     """ImageHandler::processNewImage for the GPU path: ExtractProcessor ->
     ImageProcessor -> SmartCropProcessor on one decoded RGB8 image

@@ -93,6 +93,19 @@ class Context:
         self.close()
 
     # ---- host batches ----------------------------------------------------
+    def pixelate_regions(self, image: np.ndarray, boxes) -> int:
+        """fi_pixelate_regions: the face-blur mogrify (-region box -scale 10%
+        -scale 1000%) of each (x, y, w, h) box in order, in place on an 8-bit HWC
+        (or HW gray) numpy image.  Returns the C-ABI status (boxes before a
+        rejected one are applied, as consecutive mogrify runs would be)."""
+        assert image.dtype == np.uint8 and image.flags["C_CONTIGUOUS"]
+        h, w = image.shape[:2]
+        ch = image.shape[2] if image.ndim == 3 else 1
+        flat = [int(v) for b in boxes for v in b]
+        arr = (ctypes.c_int32 * max(len(flat), 1))(*flat)
+        return self._lib.fi_pixelate_regions(self.h, image.ctypes.data, w, h, image.strides[0], ch, arr,
+                                             len(flat) // 4)
+
     def process(self, images: list[np.ndarray], ops: list[Op]):
         """Run a batch of RGB8 HWC numpy images; returns (outputs, fi_image records)."""
         n = len(images)

@@ -172,6 +172,19 @@ int fi_plan(fi_image *imgs, int32_t n);
  * these (greedy LPT).  bytes[i] = -1 for an image that does not plan. */
 int fi_plan_bytes(const fi_image *imgs, int32_t n, int64_t *bytes);
 
+/* Face-blur pixelation (FaceDetectProcessor::blurFaces,
+ * FaceDetectProcessor.php:58-74): for each box (x, y, w, h) in order -- the
+ * facedetect output lines "x y w h" -- the effect of
+ *   mogrify -gravity NorthWest -region WxH+X+Y -scale 10% -scale 1000% <img>
+ * on an 8-bit HWC image (channels 1 or 3), in place.  FI_EINVAL for a box
+ * outside the image or whose 10% scale is empty (IM: NegativeOrZeroImageSize);
+ * boxes before it are applied.  Host buffer (synchronous) and device-resident
+ * forms (img on ctx's device, stream-ordered after earlier batches). */
+int fi_pixelate_regions(fi_ctx *ctx, uint8_t *img, int32_t w, int32_t h, int32_t stride, int32_t channels,
+                        const int32_t *boxes, int32_t nboxes);
+int fi_pixelate_regions_device(fi_ctx *ctx, uint8_t *img, int32_t w, int32_t h, int32_t stride, int32_t channels,
+                               const int32_t *boxes, int32_t nboxes);
+
 /* Host buffers: H2D -> kernels -> D2H.  Synchronous. */
 int fi_process_batch(fi_ctx *ctx, fi_image *imgs, int32_t n);
 /* Device-resident buffers (src/dst are device pointers on ctx's device).

@@ -234,6 +234,36 @@ def im_convolve_q16(q16: np.ndarray, conv, ops: int) -> np.ndarray:
     return (((q.astype(np.uint32) + 128) - ((q.astype(np.uint32) + 128) >> 8)) >> 8).astype(np.uint8)
 
 
+def im_scale_q16(q16: np.ndarray, ow: int, oh: int) -> np.ndarray:
+    """or_im_scale_q16: IM 6 ScaleImage of an opaque Q16 HWC image."""
+    q = np.ascontiguousarray(q16, dtype=np.uint16)
+    h, w = q.shape[:2]
+    c = q.shape[2] if q.ndim == 3 else 1
+    out = np.zeros((oh, ow, c), np.uint16)
+    P = ctypes.POINTER(ctypes.c_uint16)
+    rc = lib().or_im_scale_q16(q.ctypes.data_as(P), w, h, c, ow, oh, out.ctypes.data_as(P))
+    if rc:
+        raise ValueError(f"or_im_scale_q16 rc={rc}")
+    return out if q.ndim == 3 else out[:, :, 0]
+
+
+def im_percent_size(size: int, percent: float) -> int:
+    return int(lib().or_im_percent_size(int(size), ctypes.c_double(percent)))
+
+
+def im_pixelate_regions(img: np.ndarray, boxes) -> np.ndarray:
+    """or_im_pixelate_regions: the face-blur mogrify per box, on a copy."""
+    out = np.ascontiguousarray(img, dtype=np.uint8).copy()
+    h, w = out.shape[:2]
+    c = out.shape[2] if out.ndim == 3 else 1
+    flat = [int(v) for b in boxes for v in b]
+    arr = (ctypes.c_int * max(len(flat), 1))(*flat)
+    rc = lib().or_im_pixelate_regions(_u8(out), w, h, w * c, c, arr, len(flat) // 4)
+    if rc:
+        raise ValueError(f"or_im_pixelate_regions rc={rc}")
+    return out
+
+
 def im_resize_q16(src: np.ndarray, ow: int, oh: int, thumbnail=True) -> np.ndarray:
     src = np.ascontiguousarray(src, dtype=np.uint8)
     H, W, C = src.shape

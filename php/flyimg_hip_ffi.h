@@ -24,4 +24,6 @@ const char *fi_last_error(void);
 int fi_create(fi_ctx **out, int32_t device);
 void fi_destroy(fi_ctx *ctx);
 int fi_plan(fi_image *imgs, int32_t n);
+int fi_pixelate_regions(fi_ctx *ctx, uint8_t *img, int32_t w, int32_t h, int32_t stride, int32_t channels,
+                        const int32_t *boxes, int32_t nboxes);
 int fi_process_batch(fi_ctx *ctx, fi_image *imgs, int32_t n);

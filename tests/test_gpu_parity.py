@@ -862,6 +862,47 @@ def test_smartcrop_cli_main_stdout_contract(ctx, capsys, tmp_path, monkeypatch):
     assert capsys.readouterr().out == ""
 
 
+@pytest.mark.parametrize("case", ["rgb", "gray", "clipped", "overlap", "wide", "single_px_blocks"])
+def test_face_blur_pixelate_bit_exact(ctx, case):
+    """FaceDetectProcessor::blurFaces (-region box -scale 10% -scale 1000% per
+    face) on the GPU == the oracle's ScaleImage restatement, bit for bit: RGB
+    and gray outputs, boxes clipped by the image edge (CropImage) and by the
+    composite, overlapping boxes applied in order, boxes whose 10 x 10% size
+    over- or undershoots the box."""
+    from flyimg_amd.processor import FaceDetectProcessor
+
+    rng = np.random.default_rng(len(case))
+    img = synth_rgb(500, 281, 11)
+    if case == "gray":
+        img = np.ascontiguousarray(img[:, :, 1])
+    boxes = {
+        "rgb": [(120, 40, 97, 118)],
+        "gray": [(30, 20, 57, 61), (300, 150, 120, 100)],
+        "clipped": [(450, 230, 90, 80), (0, 0, 33, 35)],
+        "overlap": [(100, 60, 140, 120), (180, 100, 90, 95)],
+        "wide": [(10, 200, 455, 75)],
+        "single_px_blocks": [(200, 100, 15, 14)],
+    }[case]
+    ref = orc.im_pixelate_regions(img, boxes)
+    got = np.ascontiguousarray(img.copy())
+    lines = ["%d %d %d %d" % b for b in boxes] + ["not a box"]
+    FaceDetectProcessor.blur_faces(ctx, got, lines)
+    assert (got != img).any()
+    assert np.array_equal(got, ref), int((got != ref).sum())
+    _ = rng
+
+
+def test_face_blur_rejects_empty_scale(ctx):
+    from flyimg_amd.processor import ExecFailedException, FaceDetectProcessor
+
+    img = synth_rgb(200, 100, 2)
+    got = img.copy()
+    with pytest.raises(ExecFailedException):
+        FaceDetectProcessor.blur_faces(ctx, got, ["10 10 60 50", "0 0 4 40"])  # 10% of 4 px is empty
+    # the first face was applied, as the first mogrify run would have been
+    assert np.array_equal(got, orc.im_pixelate_regions(img, [(10, 10, 60, 50)]))
+
+
 def test_codec_pipeline_auto_orient(ctx):
     """-auto-orient (ImageProcessor.php:78): EXIF orientation 6 is applied
     before the geometry."""

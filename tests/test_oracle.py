@@ -155,3 +155,114 @@ def test_pseudoclass_flag_selects_mitchell():
     a = orc.im_convert(rgba, 100, 0, base)
     b = orc.im_convert(rgba, 100, 0, base | orc.FLAG_PSEUDOCLASS)
     assert np.array_equal(a, b)
+
+
+def _scale_literal(q, ow, oh):
+    """IM 6 ScaleImage (resize.c) in plain Python loops, opaque HWC, f64 --
+    a second restatement the C oracle is checked against (small sizes)."""
+    import numpy as np
+
+    H, W, C = q.shape
+    if ow == W and oh == H:
+        return q.copy()
+    out = np.zeros((oh, ow, C), np.uint16)
+    xv = [[0.0] * C for _ in range(W)]
+    yv = [[0.0] * C for _ in range(W)]
+    clamp = lambda v: 0 if v <= 0.0 else 65535 if v >= 65535.0 else int(v + 0.5)  # noqa: E731
+    nrows, nxt, i = 0, True, 0
+    span_y, scale_y = 1.0, oh / H
+    for y in range(oh):
+        if oh == H:
+            s = [[float(v) for v in q[i, x]] for x in range(W)]
+            i += 1
+        else:
+            while scale_y < span_y:
+                if nxt and nrows < H:
+                    xv = [[float(v) for v in q[i, x]] for x in range(W)]
+                    i += 1
+                    nrows += 1
+                for x in range(W):
+                    for c in range(C):
+                        yv[x][c] += scale_y * xv[x][c]
+                span_y -= scale_y
+                scale_y = oh / H
+                nxt = True
+            if nxt and nrows < H:
+                xv = [[float(v) for v in q[i, x]] for x in range(W)]
+                i += 1
+                nrows += 1
+                nxt = False
+            s = [[yv[x][c] + span_y * xv[x][c] for c in range(C)] for x in range(W)]
+            yv = [[0.0] * C for _ in range(W)]
+            scale_y -= span_y
+            if scale_y <= 0:
+                scale_y = oh / H
+                nxt = True
+            span_y = 1.0
+        if ow == W:
+            out[y] = [[clamp(v) for v in px] for px in s]
+            continue
+        pixel = [0.0] * C
+        nc, t, span_x = False, 0, 1.0
+        sc = [[0.0] * C for _ in range(ow)]
+        for x in range(W):
+            scale_x = ow / W
+            while scale_x >= span_x:
+                if nc:
+                    pixel = [0.0] * C
+                    t += 1
+                pixel = [pixel[c] + span_x * s[x][c] for c in range(C)]
+                sc[t] = list(pixel)
+                scale_x -= span_x
+                span_x = 1.0
+                nc = True
+            if scale_x > 0:
+                if nc:
+                    pixel = [0.0] * C
+                    nc = False
+                    t += 1
+                pixel = [pixel[c] + scale_x * s[x][c] for c in range(C)]
+                span_x -= scale_x
+        if span_x > 0:
+            pixel = [pixel[c] + span_x * s[W - 1][c] for c in range(C)]
+        if not nc and t < ow:
+            sc[t] = list(pixel)
+        out[y] = [[clamp(v) for v in px] for px in sc]
+    return out
+
+
+def test_scale_image_oracle_matches_literal_loops():
+    """or_im_scale_q16 == a plain-Python restatement of ScaleImage on down,
+    up and mixed scales; 1000% of a 10% image is pixel replication."""
+    import numpy as np
+
+    from oracle import oracle as orc
+
+    rng = np.random.default_rng(7)
+    for (W, H), (ow, oh) in [((57, 40), (6, 4)), ((23, 17), (2, 2)), ((6, 4), (60, 40)), ((31, 9), (7, 20)),
+                             ((40, 40), (40, 13)), ((13, 40), (5, 40)), ((9, 9), (1, 1))]:
+        q = (rng.integers(0, 256, (H, W, 3)) * 257).astype(np.uint16)
+        assert np.array_equal(orc.im_scale_q16(q, ow, oh), _scale_literal(q, ow, oh)), (W, H, ow, oh)
+    d = orc.im_scale_q16((rng.integers(0, 256, (40, 57, 3)) * 257).astype(np.uint16), 6, 4)
+    assert np.array_equal(orc.im_scale_q16(d, 60, 40), np.repeat(np.repeat(d, 10, 0), 10, 1))
+
+
+def test_pixelate_regions_oracle_semantics():
+    """-region box -scale 10% -scale 1000%: only the box (and, when 10 x the
+    10% size exceeds the box, up to that many pixels right / below it) changes;
+    the box becomes 10x10 blocks; sizes follow ParseMetaGeometry's rounding."""
+    import numpy as np
+
+    from oracle import oracle as orc
+
+    assert (orc.im_percent_size(57, 10.0), orc.im_percent_size(55, 10.0), orc.im_percent_size(54, 10.0)) == (6, 6, 5)
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (100, 120, 3), dtype=np.uint8)
+    out = orc.im_pixelate_regions(img, [(10, 20, 57, 40)])
+    changed = np.argwhere((out != img).any(axis=2))
+    assert changed[:, 0].min() >= 20 and changed[:, 0].max() < 20 + 40
+    assert changed[:, 1].min() >= 10 and changed[:, 1].max() < 10 + 60  # 10% = 6 -> 60 px wide
+    blk = out[20:60, 10:70]
+    assert np.array_equal(blk, np.repeat(np.repeat(blk[::10, ::10], 10, 0), 10, 1))
+    with pytest.raises(ValueError):
+        orc.im_pixelate_regions(img, [(0, 0, 4, 40)])  # 10% of 4 px is empty
