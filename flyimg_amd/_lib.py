@@ -137,6 +137,10 @@ def lib():
     L.fi_pixelate_regions.argtypes = [vp, vp, i32, i32, i32, i32, P(i32), i32]
     L.fi_pixelate_regions_device.argtypes = [vp, vp, i32, i32, i32, i32, P(i32), i32]
     L.fi_process_batch.argtypes = [vp, P(FiImage), i32]
+    L.fi_submit_batch.argtypes = [vp, P(FiImage), i32]
+    L.fi_host_alloc.argtypes = [vp, ctypes.c_size_t]
+    L.fi_host_alloc.restype = vp
+    L.fi_host_free.argtypes = [vp, vp]
     L.fi_process_batch_device.argtypes = [vp, P(FiImage), i32]
     L.fi_submit_batch_device.argtypes = [vp, P(FiImage), i32]
     L.fi_wait.argtypes = [vp, i32]

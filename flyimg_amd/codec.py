@@ -71,6 +71,41 @@ def encode(pixels: np.ndarray, quality: int = 90) -> bytes:
     return buf.getvalue()
 
 
+class _PinnedSlot:
+    """One in-flight batch's pinned host memory (fi_host_alloc): the decoded
+    sources and the GPU outputs, sliced per image (256-B aligned), grown on
+    demand.  Two slots: batch k+1 decodes into one while batch k's DMA and
+    kernels use the other."""
+
+    def __init__(self, ctx):
+        self.ctx, self.src, self.dst = ctx, None, None
+
+    def _grow(self, which, nbytes):
+        cur = getattr(self, which)
+        if cur is None or cur.nbytes < nbytes:
+            if cur is not None:
+                self.ctx.host_free(cur)
+            setattr(self, which, self.ctx.host_array((max(nbytes, 1 << 20),)))
+        return getattr(self, which)
+
+    @staticmethod
+    def _slices(buf, sizes):
+        out, off = [], 0
+        for n in sizes:
+            out.append(buf[off:off + n])
+            off += (n + 255) // 256 * 256
+        return out
+
+    def sources(self, shapes):
+        sizes = [int(np.prod(s)) for s in shapes]
+        buf = self._grow("src", sum((n + 255) // 256 * 256 for n in sizes))
+        return [v.reshape(s) for v, s in zip(self._slices(buf, sizes), shapes)]
+
+    def outputs(self, sizes):
+        buf = self._grow("dst", sum((n + 255) // 256 * 256 for n in sizes))
+        return self._slices(buf, sizes)
+
+
 class CodecPipeline:
     """Batches of encoded images through decode -> GPU -> encode."""
 
@@ -105,3 +140,72 @@ class CodecPipeline:
                     r.status, msg.decode() if msg else f"image {i}"))
         encoded = list(self.pool.map(lambda a: encode(a[0], a[1]), zip(outs, quality)))
         return encoded, recs
+
+    def _prepare(self, slot, blobs, options):
+        """Decode (thread pool) straight into the slot's pinned sources; ops."""
+        decoded = list(self.pool.map(decode_ex, blobs))
+        views, ops, quality = [], [], []
+        for (img, pseudo), opts in zip(decoded, options):
+            bag = OptionsBag(opts)
+            img = ExtractProcessor.extract(bag, img)
+            h, w = img.shape[:2]
+            q = bag.get_option("quality")
+            quality.append(int(q) if not _empty(q) else 90)
+            op = ImageProcessor(bag, w, h).to_op()
+            if pseudo:
+                op.flags |= L.FI_SRC_PSEUDOCLASS
+            ops.append(op)
+            views.append(img)
+        pins = slot.sources([v.shape for v in views])
+        list(self.pool.map(lambda a: np.copyto(a[0], a[1]), zip(pins, views)))
+        return pins, ops, quality
+
+    def process_batches(self, batches):
+        """Pipelined form of ``process`` over an iterable of (blobs, options)
+        batches: batch k+1 is decoded into pinned memory and submitted
+        (fi_submit_batch) while batch k's DMA and kernels run, and batch k is
+        encoded while batch k+1 runs.  Yields (encoded outputs, records) per
+        batch, in order; the ``stats`` attribute holds the host time spent
+        decoding, blocked on the GPU, and encoding."""
+        from .runtime import plan as fi_plan
+
+        slots = [_PinnedSlot(self.ctx), _PinnedSlot(self.ctx)]
+        self.stats = {"s_decode": 0.0, "s_gpu_wait": 0.0, "s_encode": 0.0}
+        import time
+
+        prev = None
+        for k, (blobs, options) in enumerate(batches):
+            t0 = time.perf_counter()
+            slot = slots[k % 2]
+            srcs, ops, quality = self._prepare(slot, blobs, options)
+            sizes = []
+            for src, op in zip(srcs, ops):
+                ow, oh, oc = fi_plan(src.shape[1], src.shape[0], op)
+                sizes.append(max(ow * oh * oc, 1))
+            outs = slot.outputs(sizes)
+            arr, outs = self.ctx.submit(srcs, ops, outs)
+            t1 = time.perf_counter()
+            self.stats["s_decode"] += t1 - t0
+            if prev is not None:
+                yield self._finish(prev, keep=1)
+            prev = (arr, outs, quality, srcs)
+        if prev is not None:
+            yield self._finish(prev, keep=0)
+
+    def _finish(self, batch, keep):
+        import time
+
+        arr, outs, quality, _ = batch
+        t0 = time.perf_counter()
+        self.ctx.wait(keep)  # that batch is final (its failures are in its records)
+        t1 = time.perf_counter()
+        for i in range(len(outs)):
+            if arr[i].status != L.FI_OK:
+                msg = L.lib().fi_last_error()
+                raise ExecFailedException("Command failed.\nThe exit code: %d\n%s" % (
+                    arr[i].status, msg.decode() if msg else f"image {i}"))
+        views = self.ctx.views(arr, outs)
+        encoded = list(self.pool.map(lambda a: encode(np.ascontiguousarray(a[0]), a[1]), zip(views, quality)))
+        self.stats["s_gpu_wait"] += t1 - t0
+        self.stats["s_encode"] += time.perf_counter() - t1
+        return encoded, arr

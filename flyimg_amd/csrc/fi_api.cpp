@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -120,7 +121,17 @@ struct StripTab {
   std::vector<int32_t> starts;  // [nx]
   std::vector<float> wT;        // [htaps][nx]
 };
-// One in-flight batch (fi_submit_batch_device): what fi_wait needs to fill
+// A host-buffer batch (fi_submit_batch / fi_process_batch): the caller's
+// records, the device-side records run_batch fills, and where each output
+// goes -- straight into a pinned caller dst, or through the slot's pinned
+// staging (pageable dst) with one memcpy at fi_wait.
+struct HostIo {
+  fi_image *user = nullptr;
+  std::vector<fi_image> dev;
+  std::vector<size_t> dev_dst_off;  // per image: its device dst in the slot's hio buffer
+  std::vector<int64_t> pin_off;     // per image: offset in the slot's pinned staging, -1 = dst is pinned
+};
+// One in-flight batch (fi_submit_batch[_device]): what fi_wait needs to fill
 // the caller's fi_image records once the stream has drained.
 struct PendingBatch {
   fi_image *imgs = nullptr;
@@ -136,6 +147,7 @@ struct PendingBatch {
   size_t nres = 0;              // ScResult records in the slot's pinned readback
   bool any_apply = false;
   std::vector<TimedRange> timers;  // this batch's HIP-event ranges
+  std::shared_ptr<HostIo> host;    // host-buffer batches only
 };
 // Pinned host staging of one in-flight batch: the upload blob and the result
 // readback.  Two slots: batch k+1 is planned and uploaded while batch k runs.
@@ -152,6 +164,11 @@ struct Slot {
   // slot, because batch k+1's upload and resample run while batch k's
   // smartcrop stage still reads its own.
   DevBuf arena, work;
+  // host-buffer batches: device copies of the sources / outputs, and the pinned
+  // staging of pageable sources and outputs
+  DevBuf hio;
+  void *hpin = nullptr;
+  size_t hpin_cap = 0;
 };
 constexpr int kSlots = 2;
 struct fi_ctx {
@@ -1665,8 +1682,21 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
 
 // Per-image result records into the slot's pinned readback; the batch joins
 // the in-flight list (finalize_front fills the caller's records).
-static int queue_readback(fi_ctx *c, BatchPlan &Bp, int slot, uint8_t *wb, double t_start) {
+static int queue_readback(fi_ctx *c, BatchPlan &Bp, int slot, uint8_t *wb, double t_start,
+                          std::shared_ptr<HostIo> host) {
   Slot &S = c->slots[slot];
+  if (host) {
+    // outputs to the host, behind the batch's last kernel on sc_stream: the
+    // planned (pre-apply) bytes cover the applied crop, which is never larger
+    for (int i = 0; i < Bp.n; i++) {
+      const fi_image &d = Bp.imgs[i];
+      if (Bp.status[i] != FI_OK || !host->user[i].dst) continue;
+      const size_t bytes = (size_t)d.out_stride * d.out_h;
+      uint8_t *to = host->pin_off[i] < 0 ? host->user[i].dst : (uint8_t *)S.hpin + host->pin_off[i];
+      HIP_TRY(hipMemcpyAsync(to, (uint8_t *)S.hio.p + host->dev_dst_off[i], bytes, hipMemcpyDeviceToHost,
+                             c->sc_stream));
+    }
+  }
   uint8_t *rp = (uint8_t *)S.res;
   const size_t res_bytes = sizeof(ScResult) * Bp.sitems.size();
   const size_t outwh_bytes = sizeof(int32_t) * 2 * (size_t)Bp.n;
@@ -1694,13 +1724,14 @@ static int queue_readback(fi_ctx *c, BatchPlan &Bp, int slot, uint8_t *wb, doubl
   pb.nres = Bp.sitems.size();
   pb.any_apply = !Bp.apply.empty();
   pb.timers.swap(c->pending);  // waited for when this batch is finalized
+  pb.host = std::move(host);
   c->inflight.push_back(std::move(pb));
   return FI_OK;
 }
 
 static int drain(fi_ctx *c);
 static int wait_slot(fi_ctx *c, int slot);
-static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
+static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async, std::shared_ptr<HostIo> host = nullptr) {
   const double t_start = now_ms();
   Exec E;
   E.c = c;
@@ -1742,7 +1773,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
     if (c->heap_retry) return set_err(FI_ENOMEM, "batch tables exceed the device table heap");
     heap_reset(c);
     c->heap_retry = true;
-    const int rrc = run_batch(c, imgs, n, async);
+    const int rrc = run_batch(c, imgs, n, async, host);
     c->heap_retry = false;
     return rrc;
   }
@@ -1769,7 +1800,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async) {
   if (rc) return rc;
   rc = launch_batch(c, E, Bp, K, ab, wb, S);
   if (rc) return rc;
-  rc = queue_readback(c, Bp, slot, wb, t_start);
+  rc = queue_readback(c, Bp, slot, wb, t_start, host);
   if (rc) return rc;
   host_stat(c, "host_launch", now_ms() - t_planned);
   if (async) return FI_OK;
@@ -1824,6 +1855,22 @@ static int finalize_front(fi_ctx *c) {
     if (pb.status[i] != FI_OK && first_bad == FI_OK) {
       first_bad = pb.status[i];
       first_err = "image " + std::to_string(i) + ": " + pb.errs[i];
+    }
+    if (pb.host) {  // host-buffer batch: the caller's record, and its staged output
+      fi_image &o = pb.host->user[i];
+      o.out_w = im.out_w;
+      o.out_h = im.out_h;
+      o.out_channels = im.out_channels;
+      o.out_stride = im.out_stride;
+      o.crop_x = im.crop_x;
+      o.crop_y = im.crop_y;
+      o.crop_w = im.crop_w;
+      o.crop_h = im.crop_h;
+      o.crop_score = im.crop_score;
+      o.status = im.status;
+      o.n_candidates = im.n_candidates;
+      if (im.status == FI_OK && o.dst && pb.host->pin_off[i] >= 0)
+        memcpy(o.dst, (const uint8_t *)S.hpin + pb.host->pin_off[i], (size_t)im.out_stride * im.out_h);
     }
   }
   host_stat(c, "host_total", now_ms() - pb.t_start);
@@ -2249,9 +2296,10 @@ void fi_destroy(fi_ctx *c) {
   for (Slot &sl : c->slots) {
     if (sl.blob) (void)hipHostFree(sl.blob);
     if (sl.res) (void)hipHostFree(sl.res);
+    if (sl.hpin) (void)hipHostFree(sl.hpin);
     if (sl.done) (void)hipEventDestroy(sl.done);
     if (sl.rs_done) (void)hipEventDestroy(sl.rs_done);
-    for (DevBuf *b : {&sl.arena, &sl.work})
+    for (DevBuf *b : {&sl.arena, &sl.work, &sl.hio})
       if (b->p) (void)hipFree(b->p);
   }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
@@ -2360,71 +2408,123 @@ int fi_wait(fi_ctx *c, int32_t keep) {
   return first;
 }
 
+// Host-buffer batch, asynchronous: sources into the batch slot's device
+// buffer (pinned sources DMA directly; pageable ones through the slot's pinned
+// staging), run_batch, outputs back behind the batch (queue_readback).  The
+// slot's previous batch is finalized first, so two host batches are in flight.
+static bool host_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky "invalid value" of a pageable pointer
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+static int submit_host(fi_ctx *c, fi_image *imgs, int32_t n) {
+  const int slot = c->next_slot;
+  {
+    const int rc0 = wait_slot(c, slot);  // per-image failures of that batch stay in its records
+    if (rc0 == FI_EDEVICE) return rc0;
+  }
+  Slot &S = c->slots[slot];
+  auto host = std::make_shared<HostIo>();
+  host->user = imgs;
+  host->dev.assign(imgs, imgs + n);
+  host->dev_dst_off.assign(n, 0);
+  host->pin_off.assign(n, -1);
+  std::vector<size_t> soff(n, 0);
+  std::vector<int64_t> spin(n, -1);  // pageable source: offset of its packed rows in the staging
+  std::vector<uint8_t> src_pinned(n, 0);
+  size_t total = 0, pin_total = 0;
+  for (int i = 0; i < n; i++) {
+    const fi_image &im = imgs[i];
+    const int C = im.src_channels == 4 ? 4 : 3;
+    const int64_t sstride = ((int64_t)im.src_w * C + 15) / 16 * 16;
+    soff[i] = total;
+    total += (size_t)std::max<int64_t>(sstride * im.src_h, 0);
+    total = (total + 255) / 256 * 256;
+    host->dev_dst_off[i] = total;
+    total += (size_t)std::max<int64_t>(im.dst_capacity, 0);
+    total = (total + 255) / 256 * 256;
+    host->dev[i].src_stride = (int32_t)sstride;
+    const bool ok = im.src && im.src_w > 0 && im.src_h > 0 && (im.src_channels == 3 || im.src_channels == 4) &&
+                    im.src_stride >= im.src_w * im.src_channels;
+    if (ok && !(src_pinned[i] = host_pinned(im.src))) {
+      spin[i] = (int64_t)pin_total;
+      pin_total += ((size_t)im.src_w * im.src_channels * im.src_h + 255) / 256 * 256;
+    }
+    if (im.dst && im.dst_capacity > 0 && !host_pinned(im.dst)) {
+      host->pin_off[i] = (int64_t)pin_total;
+      pin_total += ((size_t)im.dst_capacity + 255) / 256 * 256;
+    }
+  }
+  int rc = ensure(c, &S.hio, total + 256);
+  if (rc) return rc;
+  rc = ensure_pinned_buf(&S.hpin, &S.hpin_cap, pin_total + 256);
+  if (rc) return rc;
+  uint8_t *io = (uint8_t *)S.hio.p;
+  for (int i = 0; i < n; i++) {
+    const fi_image &im = imgs[i];
+    fi_image &d = host->dev[i];
+    const int C = im.src_channels;
+    const bool ok = im.src && im.src_w > 0 && im.src_h > 0 && (C == 3 || C == 4) && im.src_stride >= im.src_w * C;
+    d.dst = im.dst ? io + host->dev_dst_off[i] : nullptr;
+    if (!ok) {
+      d.src = nullptr;
+      continue;
+    }
+    const size_t row = (size_t)im.src_w * C;
+    const uint8_t *from = im.src;
+    int64_t from_stride = im.src_stride;
+    if (!src_pinned[i]) {  // pageable: pack the rows into the pinned staging first
+      uint8_t *pin = (uint8_t *)S.hpin + spin[i];
+      for (int y = 0; y < im.src_h; y++) memcpy(pin + (size_t)y * row, im.src + (int64_t)y * im.src_stride, row);
+      from = pin;
+      from_stride = (int64_t)row;
+    }
+    HIP_TRY(hipMemcpy2DAsync(io + soff[i], d.src_stride, from, from_stride, row, im.src_h, hipMemcpyHostToDevice,
+                             c->stream));
+    d.src = io + soff[i];
+  }
+  return run_batch(c, host->dev.data(), n, true, host);
+}
+
+int fi_submit_batch(fi_ctx *c, fi_image *imgs, int32_t n) {
+  if (!c || n < 0 || (n > 0 && !imgs)) return set_err(FI_EINVAL, "bad arguments");
+  if (n == 0) return FI_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  return submit_host(c, imgs, n);
+}
+
 int fi_process_batch(fi_ctx *c, fi_image *imgs, int32_t n) {
   if (!c || n < 0 || (n > 0 && !imgs)) return set_err(FI_EINVAL, "bad arguments");
   if (n == 0) return FI_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   {
-    const int rc0 = drain(c);  // the io buffer may be read by in-flight batches
-    if (rc0) return rc0;
+    const int rc0 = drain(c);  // synchronous call: earlier batches complete first
+    if (rc0 == FI_EDEVICE) return rc0;
   }
-  // stage host images into device memory with 16-byte aligned rows
-  std::vector<fi_image> dev(imgs, imgs + n);
-  std::vector<size_t> soff(n), doff(n);
-  size_t total = 0;
-  for (int i = 0; i < n; i++) {
-    fi_image p = imgs[i];
-    ImPlan pl;
-    plan_im(p, &pl);
-    const int C = imgs[i].src_channels == 4 ? 4 : 3;
-    const int64_t sstride = ((int64_t)imgs[i].src_w * C + 15) / 16 * 16;
-    soff[i] = total;
-    total += (size_t)std::max<int64_t>(sstride * imgs[i].src_h, 0);
-    total = (total + 255) / 256 * 256;
-    doff[i] = total;
-    total += (size_t)std::max<int64_t>(imgs[i].dst_capacity, 0);
-    total = (total + 255) / 256 * 256;
-    dev[i].src_stride = (int32_t)sstride;
+  const int rc = submit_host(c, imgs, n);
+  const int rd = drain(c);
+  return rc != FI_OK ? rc : rd;
+}
+
+void *fi_host_alloc(fi_ctx *c, size_t bytes) {
+  if (!c || bytes == 0) return nullptr;
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    set_err(FI_ENOMEM, "hipHostMalloc(%zu) failed", bytes);
+    return nullptr;
   }
-  int rc = ensure(c, &c->io, total + 256);
-  if (rc) return rc;
-  uint8_t *io = (uint8_t *)c->io.p;
-  for (int i = 0; i < n; i++) {
-    const int C = imgs[i].src_channels;
-    if (!imgs[i].src || imgs[i].src_w <= 0 || imgs[i].src_h <= 0 || (C != 3 && C != 4) ||
-        imgs[i].src_stride < imgs[i].src_w * C) {
-      dev[i].src = nullptr;
-      continue;
-    }
-    HIP_TRY(hipMemcpy2DAsync(io + soff[i], dev[i].src_stride, imgs[i].src, imgs[i].src_stride,
-                             (size_t)imgs[i].src_w * C, imgs[i].src_h, hipMemcpyHostToDevice, c->stream));
-    dev[i].src = io + soff[i];
-    dev[i].dst = imgs[i].dst ? io + doff[i] : nullptr;
-  }
-  rc = run_batch(c, dev.data(), n, false);
-  for (int i = 0; i < n; i++) {
-    fi_image &o = imgs[i];
-    const fi_image &d = dev[i];
-    o.out_w = d.out_w;
-    o.out_h = d.out_h;
-    o.out_channels = d.out_channels;
-    o.out_stride = d.out_stride;
-    o.crop_x = d.crop_x;
-    o.crop_y = d.crop_y;
-    o.crop_w = d.crop_w;
-    o.crop_h = d.crop_h;
-    o.crop_score = d.crop_score;
-    o.status = d.status;
-    o.n_candidates = d.n_candidates;
-    if (d.status == FI_OK && o.dst) {
-      const size_t bytes = (size_t)d.out_stride * d.out_h;
-      if (hipMemcpyAsync(o.dst, io + doff[i], bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-        return set_err(FI_EDEVICE, "D2H of image %d failed", i);
-    }
-  }
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return rc;
+  return p;
+}
+
+int fi_host_free(fi_ctx *c, void *p) {
+  if (!c) return set_err(FI_EINVAL, "bad arguments");
+  if (p) HIP_TRY(hipHostFree(p));
+  return FI_OK;
 }
 
 void fi_smartcrop_default_params(fi_smartcrop_params *p) {

@@ -77,6 +77,10 @@ class Context:
 
     def close(self):
         if self.h:
+            for ptr in list(getattr(self, "_pinned", {})):
+                self._lib.fi_host_free(self.h, ptr)
+        self._pinned = {}
+        if self.h:
             self._lib.fi_destroy(self.h)
             self.h = None
 
@@ -138,6 +142,64 @@ class Context:
             else:
                 results.append(None)
         return results, arr, rc
+
+    # ---- pinned host buffers + asynchronous host batches ----------------------
+    def host_array(self, shape, dtype=np.uint8) -> np.ndarray:
+        """A numpy array over pinned host memory (fi_host_alloc): sources and
+        outputs there are copied by DMA directly, overlapping earlier batches.
+        Freed with the context (or ``host_free``)."""
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        ptr = self._lib.fi_host_alloc(self.h, max(nbytes, 1))
+        if not ptr:
+            raise MemoryError(L.lib().fi_last_error().decode())
+        buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(ptr)
+        arr = np.frombuffer(buf, dtype=np.uint8, count=nbytes).view(dtype).reshape(shape)
+        self._pinned = getattr(self, "_pinned", {})
+        self._pinned[ptr] = arr
+        return arr
+
+    def host_free(self, arr: np.ndarray):
+        ptr = arr.ctypes.data
+        if ptr in getattr(self, "_pinned", {}):
+            del self._pinned[ptr]
+            L.check(self._lib.fi_host_free(self.h, ptr))
+
+    def submit(self, images: list[np.ndarray], ops: list[Op], outs: list[np.ndarray] | None = None):
+        """fi_submit_batch: queue a batch of host images; returns (FiImage array,
+        output buffers) whose contents are final after ``wait()``.  Buffers from
+        ``host_array`` go by DMA directly; others through the library's pinned
+        staging.  ``images`` / ``outs`` must stay alive until then."""
+        n = len(images)
+        arr = (L.FiImage * n)()
+        for i, (src, op) in enumerate(zip(images, ops)):
+            img = arr[i]
+            img.src = src.ctypes.data
+            img.src_h, img.src_w = src.shape[:2]
+            img.src_stride = src.strides[0]
+            img.src_channels = src.shape[2] if src.ndim == 3 else 1
+            _fill(img, op)
+        L.lib().fi_plan(arr, n)
+        if outs is None:
+            outs = [np.zeros(max(arr[i].out_w * arr[i].out_h * max(arr[i].out_channels, 1), 1), np.uint8)
+                    for i in range(n)]
+        for i in range(n):
+            arr[i].dst = outs[i].ctypes.data
+            arr[i].dst_capacity = outs[i].nbytes
+        L.check(self._lib.fi_submit_batch(self.h, arr, n))
+        return arr, outs
+
+    @staticmethod
+    def views(arr, outs):
+        """Per image: the HWC (or HW) output view of a finished batch, or None."""
+        res = []
+        for i in range(len(outs)):
+            a = arr[i]
+            if a.status != L.FI_OK:
+                res.append(None)
+                continue
+            o = outs[i].reshape(-1)[: a.out_h * a.out_stride].reshape(a.out_h, a.out_w, a.out_channels)
+            res.append(o[:, :, 0] if a.out_channels == 1 else o)
+        return res
 
     # ---- smartcrop (smartcrop.py SmartCrop().crop) ---------------------------
     def smartcrop_ex(self, rgb: np.ndarray, width: int, height: int, params=None, options=None,

@@ -33,6 +33,7 @@
 #ifndef FLYIMG_HIP_H
 #define FLYIMG_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -187,6 +188,17 @@ int fi_pixelate_regions_device(fi_ctx *ctx, uint8_t *img, int32_t w, int32_t h, 
 
 /* Host buffers: H2D -> kernels -> D2H.  Synchronous. */
 int fi_process_batch(fi_ctx *ctx, fi_image *imgs, int32_t n);
+/* Asynchronous form of fi_process_batch: sources are staged to the device
+ * and the batch is queued; outputs and records are final after fi_wait.
+ * Two batches can be in flight (the next one's staging and upload overlap the
+ * previous one's kernels).  Sources and outputs in pinned memory
+ * (fi_host_alloc) are copied by DMA directly; pageable ones go through the
+ * library's pinned staging.  imgs and the buffers must stay valid until
+ * fi_wait returns for this batch. */
+int fi_submit_batch(fi_ctx *ctx, fi_image *imgs, int32_t n);
+/* Pinned host memory for decode targets and outputs of fi_submit_batch. */
+void *fi_host_alloc(fi_ctx *ctx, size_t bytes);
+int fi_host_free(fi_ctx *ctx, void *p);
 /* Device-resident buffers (src/dst are device pointers on ctx's device).
  * Synchronous; the timed kernels are recorded in fi_kernel_stats. */
 int fi_process_batch_device(fi_ctx *ctx, fi_image *imgs, int32_t n);

@@ -903,6 +903,66 @@ def test_face_blur_rejects_empty_scale(ctx):
     assert np.array_equal(got, orc.im_pixelate_regions(img, [(10, 10, 60, 50)]))
 
 
+def test_async_host_batches_match_synchronous(ctx):
+    """fi_submit_batch with pinned and pageable sources / outputs, two batches
+    in flight, equals fi_process_batch image for image (records and pixels)."""
+    from flyimg_amd.processor import ImageProcessor, OptionsBag
+
+    opts = ["w_500,smc_1", "w_300,h_250,c_1", "w_200,clsp_Gray,r_90", "w_320", "w_150,h_150,c_1,smc_1"]
+    srcs = [synth_rgb(960 + 64 * k, 540 + 32 * k, 300 + k) for k in range(len(opts))]
+    ops = [ImageProcessor(OptionsBag(o), s.shape[1], s.shape[0]).to_op() for o, s in zip(opts, srcs)]
+    ref, rrecs, rc = ctx.process(srcs, ops)
+    assert rc == 0
+    pinned = []
+    for s in srcs[:3]:
+        p = ctx.host_array(s.shape)
+        p[...] = s
+        pinned.append(p)
+    batch_a = (pinned + srcs[3:], ops)            # pinned and pageable sources
+    batch_b = (srcs, ops)
+    a1, o1 = ctx.submit(*batch_a)
+    outs_pinned = [ctx.host_array((max(o.nbytes, 1),)) for o in o1]
+    a2, o2 = ctx.submit(*batch_b, outs=outs_pinned)   # pinned outputs
+    assert ctx.wait(0) == 0
+    for arr, outs in ((a1, o1), (a2, o2)):
+        views = ctx.views(arr, outs)
+        for i in range(len(opts)):
+            assert arr[i].status == 0
+            assert (arr[i].crop_x, arr[i].crop_y, arr[i].crop_w, arr[i].crop_h) == \
+                   (rrecs[i].crop_x, rrecs[i].crop_y, rrecs[i].crop_w, rrecs[i].crop_h)
+            assert np.array_equal(views[i], ref[i]), opts[i]
+    for p in pinned + outs_pinned:
+        ctx.host_free(p)
+
+
+def test_codec_process_batches_pipelined(ctx):
+    """CodecPipeline.process_batches (pinned decode slots, fi_submit_batch,
+    encode overlapped) yields what process() returns, batch by batch."""
+    import io
+
+    from PIL import Image
+
+    from flyimg_amd.codec import CodecPipeline, decode
+
+    blobs = []
+    for k in range(5):
+        b = io.BytesIO()
+        Image.fromarray(synth_rgb(800 + 16 * k, 600, 40 + k)).save(b, "JPEG", quality=92)
+        blobs.append(b.getvalue())
+    opts = ["w_300,smc_1,q_90", "w_200,h_200,c_1", "w_250", "w_120,clsp_Gray", "w_400,q_85"]
+    pipe = CodecPipeline(ctx, threads=4)
+    try:
+        want = [pipe.process([b], [o])[0][0] for b, o in zip(blobs, opts)]
+        got = []
+        for enc, recs in pipe.process_batches([(blobs[:2], opts[:2]), (blobs[2:4], opts[2:4]), (blobs[4:], opts[4:])]):
+            got += enc
+    finally:
+        pipe.close()
+    assert len(got) == 5
+    for g, w in zip(got, want):
+        assert np.array_equal(decode(g), decode(w))
+
+
 def test_codec_pipeline_auto_orient(ctx):
     """-auto-orient (ImageProcessor.php:78): EXIF orientation 6 is applied
     before the geometry."""
