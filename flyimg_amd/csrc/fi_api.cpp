@@ -47,6 +47,7 @@ int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, 
                 const ScParamsDev &P);
 int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
                  const ScParamsDev &P);
+int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P);
 int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, int max_px, const DevCrop *crops,
                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P);
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
@@ -200,6 +201,7 @@ struct fi_ctx {
   bool vm_rs = true;     // FI_DISABLE_VM_RS=1: no k_rs_vm (streaming MFMA resample, the default)
   bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
   bool sc_vq = true;        // FI_DISABLE_SC_VQ=1: k_sc_vmaps (VALU vertical pass) instead of k_sc_vq
+  bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
@@ -760,6 +762,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.hmC = T.hmC;
     d.hmS0 = T.hmS0;
     d.vq = prep && P.vq_ok && c->sc_vq ? 1 : 0;
+    d.fz = d.hm && d.vq && P.fz_ok && c->sc_fz ? 1 : 0;
     d.vqA = T.vqA;
     d.vqC = T.vqC;
     d.vqK0 = T.vqK0;
@@ -768,7 +771,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     // workspace (offsets; converted to pointers after allocation)
     auto take = [&](size_t n) { return (uint8_t *)(uintptr_t)(E.work.take(n) + 1); };
     if (P.fx > 1 || P.fy > 1) d.red = take((size_t)P.rw * P.rh * 3);
-    if (P.thumb && P.need_h)  // generic kernels: pitch aw*3; k_sc_hrows: pitch apitch
+    if (P.thumb && P.need_h && !d.fz)  // generic kernels: pitch aw*3; k_sc_hrows: pitch apitch
       d.hbuf = take((size_t)(prep ? (P.aw * 3 + 15) / 16 * 16 : P.aw * 3) * std::max(P.hrows, 1));
     if (P.thumb && (!prep || want_pre)) d.pre = take((size_t)P.aw * P.ah * 3);
     d.maps = (uint32_t *)take((size_t)P.aw * P.ah * 4);
@@ -816,6 +819,8 @@ struct ScLaunches {
   Launch red, hp, vp, maps;        // generic (fi_kernels.hip)
   size_t prep_off = 0, hv_off = 0, hm_off = 0, vq_off = 0;  // k_sc_vmaps / k_sc_hrows / k_sc_hmfma / k_sc_vq
   int nprep = 0, nhv = 0, nhm = 0, h_chunks = 0, h_lds = 0, hm_chunks = 0, hm_lds = 0, v_chunks = 0, v_lds = 0;
+  size_t fz_off = 0;  // k_sc_fz
+  int nfz = 0, fz_lds = 0;
   int nvq = 0, vq_chunks = 0, vq_lds = 0;
   size_t sl_off = 0, sg_off = 0;   // k_sc_score2 with maps in LDS / global
   int nsl = 0, nsg = 0, sl_px = 0;
@@ -824,13 +829,16 @@ struct ScLaunches {
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> prep, hv, hm, sl, sg, vq;
+  std::vector<ScDesc> prep, hv, hm, sl, sg, vq, fz;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
     const ScDesc &d = SL.descs[k];
     const ScPlan &P = *SL.plans[k];
     if (d.red) sred.push_back((int)k);
-    if (d.prep) {
+    if (d.fz) {
+      fz.push_back(d);
+      X->fz_lds = std::max(X->fz_lds, P.fz_lds);
+    } else if (d.prep) {
       if (d.vq) {
         vq.push_back(d);
         X->vq_chunks = std::max(X->vq_chunks, P.vq_chunks);
@@ -875,6 +883,8 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->nhm = (int)hm.size();
   X->vq_off = B.addv(vq);
   X->nvq = (int)vq.size();
+  X->fz_off = B.addv(fz);
+  X->nfz = (int)fz.size();
   X->sl_off = B.addv(sl);
   X->nsl = (int)sl.size();
   X->sg_off = B.addv(sg);
@@ -892,7 +902,8 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
     if (launch_sc_h(st, true, (const ScDesc *)(ab + X.hm_off), X.nhm, X.hm_chunks, X.hm_lds, ai) != 0 ||
         launch_sc_h(st, false, (const ScDesc *)(ab + X.hv_off), X.nhv, X.h_chunks, X.h_lds, ai) != 0 ||
         launch_sc_v(st, (const ScDesc *)(ab + X.prep_off), X.nprep, X.v_chunks, X.v_lds, ai, PD) != 0 ||
-        launch_sc_vq(st, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0)
+        launch_sc_vq(st, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0 ||
+        launch_sc_fz(st, (const ScDesc *)(ab + X.fz_off), X.nfz, X.fz_lds, ai, PD) != 0)
       return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d)", X.hm_lds, X.h_lds, X.v_lds);
     if (X.hp.tiles)
       hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, st, desc(X.hp), pre(X.hp), X.hp.n, ai);
@@ -2259,6 +2270,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
   if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');
+  if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_MFMA")) c->sc_mfma = !(e[0] == '1');
   // FI_SC_STREAM=1: the smartcrop stage of batch k on its own stream, beside

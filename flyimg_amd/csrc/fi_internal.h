@@ -122,6 +122,7 @@ struct ScDesc {
   int32_t hm_rows, hm_ks, hm_pitch, hm_nb;
   int32_t hmB, hmC, hmS0;  // arena offsets (int32 units; hmB 16-B aligned)
   int32_t vq;              // 1: vertical pass + maps by k_sc_vq (tables below)
+  int32_t fz;              // 1: both passes + maps by k_sc_fz (hm + vq tables, one workgroup per image)
   int32_t vqA, vqC, vqK0;  // arena offsets (int32 units; vqA 16-B aligned)
   uint8_t *red;        // reduce scratch rw*rh*3
   uint8_t *hbuf;       // H-pass scratch aw*hrows*3
@@ -141,6 +142,10 @@ struct ScDesc {
 constexpr int kPrepRows = 16;
 constexpr int kVqRows = 14;  // k_sc_vq: analysed rows per workgroup (16 prescaled rows with the edge halo)
 constexpr int kPrepMaxLds = 64 * 1024;
+// k_sc_fz (fi_smartcrop.hip): the fused per-image prescale + maps; LDS =
+// kFzRing (80) H-stage rows + max(3 source planes of 16 rows, 16 prescaled rows
+// + luma); <= 80 KB keeps two workgroups per CU
+constexpr int kFzMaxLds = 80 * 1024;
 // k_sc_score2: maps resident in LDS when aw*ah*4 <= this; crops per image.
 constexpr int kScoreLdsMaps = 112 * 1024;
 constexpr int kScoreMaxCrops = 1024;

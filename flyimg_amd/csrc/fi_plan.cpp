@@ -992,6 +992,17 @@ void plan_sc_prep(ScPlan *p) {
   p->v_lds = (int)vmax;
   p->prep_ok = true;
   plan_sc_vq(p);
+  // k_sc_fz: both MFMA passes in one per-image workgroup (no reduce step; the
+  // source block's items fit the kernel's 4 register slots per thread)
+  p->fz_ok = false;
+  if (p->hm_ok && p->vq_ok && !reduced && p->hm_pitch <= 1024) {
+    const int64_t lpitch = (p->aw + 3) / 4 * 4;
+    const int64_t lds = 80 * apitch + std::max<int64_t>(3 * 16 * (int64_t)p->hm_pitch, 16 * apitch + 16 * lpitch);
+    if (lds <= kFzMaxLds) {
+      p->fz_lds = (int)lds;
+      p->fz_ok = true;
+    }
+  }
 }
 
 static double thirds(double x) {

@@ -147,6 +147,8 @@ struct ScPlan {
   // 16-row MFMA block), its H-stage window starts at vqK0[chunk] (<= 64 rows)
   bool vq_ok = false;
   int vq_chunks = 0, vq_lds = 0;
+  bool fz_ok = false;  // k_sc_fz (fused per-image prescale + maps)
+  int fz_lds = 0;
   std::vector<int32_t> vqA;   // [chunk][3 limbs] fragments of 64 lanes x 16 B (256 int32)
   std::vector<int32_t> vqC;   // [ah] 2^21 + 128 * sum_j k[y][j]
   std::vector<int32_t> vqK0;  // [chunk] first H-stage row of the window

@@ -433,6 +433,230 @@ __global__ __launch_bounds__(kPrepThreads) void k_sc_vq(const ScDesc *__restrict
   }
 }
 
+// ---- k_sc_fz: the whole prescale + maps of ONE image per workgroup (k_sc_hmfma
+// and k_sc_vq fused; no H-stage round trip through HBM).  The image's source
+// rows stream through in blocks of 16 (one MFMA row block of the horizontal
+// pass); their H-stage rows (p - 128 bytes) go to an LDS ring of kFzRing rows;
+// each chunk of kVqRows analysed rows runs as soon as the ring holds its
+// 64-row window (k_sc_vq's vertical MFMA, luma, edge / skin / saturation).
+// Two workgroups per CU overlap one's loads with the other's MFMAs.  LDS: ring kFzRing x apitch, then one region shared by the
+// source planes (horizontal phase) and the prescaled rows + luma (vertical).
+// Arithmetic is k_sc_hmfma's and k_sc_vq's: Pillow's int32 accumulators bit
+// for bit.
+constexpr int kFzRing = 80;  // a 64-row window at any 16-row block alignment
+#ifndef FI_FZ_THREADS
+#define FI_FZ_THREADS 512
+#endif
+constexpr int kFzThreads = FI_FZ_THREADS;  // 8 waves; two workgroups per CU (LDS)
+__global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restrict__ descs,
+                                                        const int32_t *__restrict__ ai, const ScParamsDev P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const ScDesc &D = descs[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int aw = D.aw, ah = D.ah, hrows = D.hrows, yoff = D.ybox_first;
+  const int apitch = (aw * 3 + 15) & ~15, lpitch = (aw + 3) & ~3;
+  const int PP = D.hm_pitch, KS = D.hm_ks, nb = D.hm_nb;
+  const uint8_t *src = D.img;
+  const int64_t sstride = D.stride;
+  const int sC = D.C, sW = D.W, nch = sC == 3 ? 3 : 1;
+  uint8_t *ring = lds8;                                   // [kFzRing][apitch] H-stage rows, p - 128
+  uint8_t *shared = lds8 + kFzRing * apitch;              // source planes [c][16][PP] | prer + lum
+  uint8_t *prer = shared, *lum = shared + 16 * apitch;    // [16][apitch] prescaled rows, [16][lpitch] luma
+  typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+  typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+  const int ng = PP >> 4;                                 // 16-pixel groups per plane row
+  const int nitem = 16 * ng;                              // items of one 16-row block
+  const bool a4 = (((uintptr_t)src | (uintptr_t)sstride) & 3) == 0;
+  // one block of 16 source rows -> planes of (p - 128): items of 16 pixels of a
+  // row, two per thread at a time (six 16-byte loads in flight, then the
+  // deinterleave); row tails and narrow rows byte by byte
+  auto stage_block = [&](int r0) {
+#pragma unroll 1
+    for (int base = 0; base < nitem; base += 2 * kFzThreads) {
+      u32x4a q[2][3];
+      bool fast[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int it = base + u * kFzThreads + tid;
+        const int rr = it / ng, g = it - rr * ng;
+        fast[u] = it < nitem && r0 + rr < hrows && sC == 3 && a4 && 16 * g + 16 <= sW;
+        if (fast[u]) {
+          const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride;
+#pragma unroll
+          for (int k = 0; k < 3; k++) q[u][k] = *reinterpret_cast<const u32x4a *>(s + 48 * g + 16 * k);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int it = base + u * kFzThreads + tid;
+        if (it >= nitem) break;
+        const int rr = it / ng, g = it - rr * ng;
+        const bool rowok = r0 + rr < hrows;
+        const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride;
+        u32x4s w0, w1, w2;
+        if (fast[u]) {
+          const uint32_t d[12] = {q[u][0].x, q[u][0].y, q[u][0].z, q[u][0].w, q[u][1].x, q[u][1].y,
+                                  q[u][1].z, q[u][1].w, q[u][2].x, q[u][2].y, q[u][2].z, q[u][2].w};
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint32_t a0 = d[3 * k], a1 = d[3 * k + 1], a2 = d[3 * k + 2];
+            w0[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00060300u), 0x05020100u) ^ 0x80808080u;
+            w1[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00070401u), 0x06020100u) ^ 0x80808080u;
+            w2[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00000502u), 0x07040100u) ^ 0x80808080u;
+          }
+        } else {
+#pragma unroll 1
+          for (int k = 0; k < 4; k++) {
+            uint32_t a = 0, b = 0, c = 0;
+#pragma unroll 1
+            for (int j = 0; j < 4; j++) {
+              const int x = 16 * g + 4 * k + j;
+              const bool ok = rowok && x < sW;
+              uint32_t vr, vg, vb;
+              if (sC == 3) {
+                vr = ok ? s[3 * x] : 128u;
+                vg = ok ? s[3 * x + 1] : 128u;
+                vb = ok ? s[3 * x + 2] : 128u;
+              } else {
+                vr = vg = vb = ok ? s[x] : 128u;
+              }
+              a |= vr << (8 * j);
+              b |= vg << (8 * j);
+              c |= vb << (8 * j);
+            }
+            w0[k] = a ^ 0x80808080u;
+            w1[k] = b ^ 0x80808080u;
+            w2[k] = c ^ 0x80808080u;
+          }
+        }
+        *reinterpret_cast<u32x4s *>(shared + (0 * 16 + rr) * PP + 16 * g) = w0;
+        if (nch == 3) {
+          *reinterpret_cast<u32x4s *>(shared + (1 * 16 + rr) * PP + 16 * g) = w1;
+          *reinterpret_cast<u32x4s *>(shared + (2 * 16 + rr) * PP + 16 * g) = w2;
+        }
+      }
+    }
+  };
+  const int32_t *hmS0 = ai + D.hmS0, *hmC = ai + D.hmC;
+  const i32x4 *hmB = reinterpret_cast<const i32x4 *>(ai + D.hmB);
+  const int k0l = mfma_i8_k(lane, 0), k8l = mfma_i8_k(lane, 8);
+  auto hpass = [&](int r0) {  // the staged block -> H-stage rows r0 .. r0 + 15 into the ring
+#pragma unroll 1
+    for (int b = wave; b < nb; b += kFzThreads / 64) {
+      const int s0 = hmS0[b];
+      i32x4 Bf[2][3];
+#pragma unroll
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int qq = 0; qq < 3; qq++) Bf[t][qq] = t < KS ? hmB[((b * KS + t) * 3 + qq) * 64 + lane] : i32x4{0, 0, 0, 0};
+      const int x = 16 * b + (lane & 15);
+      const int32_t cx = x < aw ? hmC[x] : 0;
+#pragma unroll 1
+      for (int c = 0; c < nch; c++) {
+        i32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+          if (t < KS) {
+            const uint8_t *base = shared + (c * 16 + (lane & 15)) * PP + s0 + 64 * t;
+            const i32x2 lo = *reinterpret_cast<const i32x2 *>(base + k0l);
+            const i32x2 hi = *reinterpret_cast<const i32x2 *>(base + k8l);
+            const i32x4 a = {lo.x, lo.y, hi.x, hi.y};
+            acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, Bf[t][0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, Bf[t][1], acc1, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, Bf[t][2], acc2, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int row = r0 + 4 * (lane >> 4) + i;
+          if (x < aw && row < hrows) {
+            const uint32_t v = (uint32_t)acc0[i] + ((uint32_t)acc1[i] << 8) + ((uint32_t)acc2[i] << 16) + (uint32_t)cx;
+            const uint8_t o = (uint8_t)(pil_clip8((int32_t)v) ^ 0x80u);
+            uint8_t *dst = ring + (row % kFzRing) * apitch + 3 * x;
+            if (nch == 3) {
+              dst[c] = o;
+            } else {
+              dst[0] = dst[1] = dst[2] = o;
+            }
+          }
+        }
+      }
+    }
+  };
+  // ---- stream the H stage, run each analysed-row chunk once its window is in
+  const int chunks = (ah + kVqRows - 1) / kVqRows;
+  int produced = 0;  // H-stage rows in the ring: [produced - ring span, produced)
+  const int rA = 16 * (lane >> 4) + ((lane & 15) >> 1);
+  const int nq = apitch >> 4, nbytes = 3 * aw;
+#pragma unroll 1
+  for (int c = 0; c < chunks; c++) {
+    const int k0 = ai[D.vqK0 + c];
+    const int need = min(k0 + 64, hrows);
+    while (produced < need) {
+      __syncthreads();  // the shared region's previous readers (vertical phase) are done
+      stage_block(produced);
+      __syncthreads();
+      hpass(produced);
+      produced += 16;
+    }
+    __syncthreads();  // ring rows of the window complete; the shared region is free
+    const int y0 = kVqRows * c, y1 = min(y0 + kVqRows, ah), pa = max(0, y0 - 1), pe = min(ah, pa + 16);
+    const i32x4 *af = reinterpret_cast<const i32x4 *>(ai + D.vqA) + (size_t)c * 3 * 64;
+    const i32x4 A0 = af[lane], A1 = af[64 + lane], A2 = af[128 + lane];
+    int32_t cy[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) cy[i] = ai[D.vqC + min(pa + 4 * (lane >> 4) + i, ah - 1)];
+    // window row r lives in ring row (k0 + r) % kFzRing
+    const uint8_t *pA = ring + ((k0 + rA) % kFzRing) * apitch + 8 * (lane & 1);
+    const uint8_t *pB = ring + ((k0 + rA + 8) % kFzRing) * apitch + 8 * (lane & 1);
+#pragma unroll 1
+    for (int t = wave; t < nq; t += kFzThreads / 64) {
+      const i32x2 lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pA + 16 * t));
+      const i32x2 hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pB + 16 * t));
+      const i32x4 B = {lo.x, lo.y, hi.x, hi.y};
+      const i32x4 d2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+      const i32x4 d1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, B, d2 << 8, 0, 0, 0);
+      const i32x4 d0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+      const int col = 16 * t + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int m = 4 * (lane >> 4) + i;
+        const int32_t sv = (int32_t)((uint32_t)d0[i] + ((uint32_t)d1[i] << 8) + (uint32_t)cy[i]);
+        if (col < nbytes && pa + m < pe) prer[m * apitch + col] = pil_clip8(sv);
+      }
+    }
+    __syncthreads();
+    const int nr = pe - pa;
+#pragma unroll 1
+    for (int it = tid; it < nr * aw; it += kFzThreads) {
+      const int m = it / aw, x = it - m * aw;
+      const uint8_t *qq = prer + m * apitch + 3 * x;
+      lum[m * lpitch + x] = (uint8_t)sc_luma(qq[0], qq[1], qq[2]);
+      const int y = pa + m;
+      if (D.pre && y >= y0 && y < y1) {
+        uint8_t *o = D.pre + ((int64_t)y * aw + x) * 3;
+        o[0] = qq[0];
+        o[1] = qq[1];
+        o[2] = qq[2];
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int it = tid; it < (y1 - y0) * aw; it += kFzThreads) {
+      const int yr = it / aw, x = it - yr * aw, y = y0 + yr, m = y - pa;
+      const uint8_t *lrow = lum + m * lpitch;
+      const uint32_t L = lrow[x];
+      uint32_t E = L;
+      if (aw >= 3 && ah >= 3 && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
+        const int v = 4 * (int)L - (int)lrow[x - lpitch] - (int)lrow[x + lpitch] - (int)lrow[x - 1] - (int)lrow[x + 1] + 1;
+        E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
+      }
+      const uint8_t *qq = prer + m * apitch + 3 * x;
+      D.maps[(int64_t)y * aw + x] = sc_skin_sat(qq[0], qq[1], qq[2], L, P) | (E << 8);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 constexpr int kScoreThreads = 1024;
 constexpr int kScoreWaves = kScoreThreads / 64;
@@ -720,6 +944,12 @@ int launch_sc_h(hipStream_t s, bool mfma, const ScDesc *descs, int n, int chunks
     hipLaunchKernelGGL(k_sc_hmfma, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai);
   else
     hipLaunchKernelGGL(k_sc_hrows, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai);
+  return 0;
+}
+int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P) {
+  if (n <= 0) return 0;
+  if (lds > kFzMaxLds) return -1;
+  hipLaunchKernelGGL(k_sc_fz, dim3(n), dim3(kFzThreads), lds, s, descs, ai, P);
   return 0;
 }
 int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,

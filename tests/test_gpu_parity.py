@@ -45,10 +45,12 @@ def _context_with(env):
 
 
 _ENV = {"FI_DISABLE_FUSED": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0",
-        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0"}
+        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0", "FI_DISABLE_SC_FZ": "0"}
 PATHS = {
-    # default kernels: k_rs_vm streaming MFMA resample; k_sc_hmfma + k_sc_vq prescale; k_sc_score2
+    # default kernels: k_rs_vm streaming MFMA resample; k_sc_fz fused prescale + maps; k_sc_score2
     "vm": dict(_ENV),
+    # the unfused MFMA prescale: k_sc_hmfma + k_sc_vq (H-stage rows through HBM)
+    "nofz": dict(_ENV, FI_DISABLE_SC_FZ="1"),
     # VALU fused resample (k_rs_fused); VALU vertical prescale + maps (k_sc_vmaps)
     "valu": dict(_ENV, FI_DISABLE_VM_RS="1", FI_DISABLE_SC_VQ="1"),
     # default resample with the VALU horizontal prescale (k_sc_hrows)
@@ -67,7 +69,8 @@ def rctx(request):
     c.close()
 
 
-EXPECTED_PATH = {"vm": "path_vm", "schrows": "path_vm", "valu": "path_fused", "generic": "path_generic_v"}
+EXPECTED_PATH = {"vm": "path_vm", "nofz": "path_vm", "schrows": "path_vm", "valu": "path_fused",
+                 "generic": "path_generic_v"}
 
 
 @pytest.mark.parametrize("W,H,opts", [
