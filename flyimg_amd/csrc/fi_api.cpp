@@ -69,6 +69,10 @@ size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16);
 int vm_read_stamps(uint64_t *out, int slots);
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
+// streaming exact-integer MFMA resample, horizontal first (fi_hv.hip)
+size_t hv_lds_bytes(int pp, int nocb);
+int launch_hv(hipStream_t s, const HvDesc *descs, const HvStripD *strips, const HvTile *tiles, int ntiles,
+              const int32_t *ai, size_t lds);
 // face-blur pixelation (fi_pixelate.hip)
 int launch_pix(hipStream_t s, int mode, const PixPass &P, const int32_t *ai, const double *ad);
 // fused vertical-first VALU resample (fi_fused.hip)
@@ -199,11 +203,14 @@ struct fi_ctx {
   std::map<const AxisTable *, std::vector<StripTab>> strip_cache;
   bool fused = true;    // FI_DISABLE_FUSED=1 forces the generic two-pass resample
   bool vm_rs = true;     // FI_DISABLE_VM_RS=1: no k_rs_vm (streaming MFMA resample, the default)
+  bool hv_rs = true;     // FI_DISABLE_HV_RS=1: horizontal-first geometries take the generic two-pass kernels
   bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
   bool sc_vq = true;        // FI_DISABLE_SC_VQ=1: k_sc_vmaps (VALU vertical pass) instead of k_sc_vq
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
+  std::map<const AxisTable *, HvV> hvv_cache;  // ok iff nblk > 0
+  std::map<const AxisTable *, HvH> hvh_cache;  // ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
   // Device-resident table heaps: every per-geometry table (tap tables, MFMA
   // fragments, Pillow coefficients, importance tables) is uploaded once and
@@ -229,6 +236,8 @@ struct fi_ctx {
   std::map<const StripTab *, std::pair<int32_t, int32_t>> strip_at;
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
   std::map<const MfmaH *, std::array<int32_t, 4>> mh_at;  // wsum, frag, s0, lut
+  std::map<const HvV *, std::array<int32_t, 3>> hvv_at;   // k0ks, frag, wsum
+  std::map<const HvH *, std::array<int32_t, 3>> hvh_at;   // w128, frag, s0
   int32_t mono_wts_at = -1;
   bool heap_retry = false;
   bool sc_mfma = true;  // FI_DISABLE_SC_MFMA=1: VALU horizontal pass (k_sc_hrows) instead of k_sc_hmfma
@@ -426,6 +435,8 @@ static void heap_reset(fi_ctx *c) {
   c->strip_at.clear();
   c->vv_at.clear();
   c->mh_at.clear();
+  c->hvv_at.clear();
+  c->hvh_at.clear();
   c->mono_wts_at = -1;
 }
 // Before a batch places anything: evict oversized host caches (only here, so
@@ -440,6 +451,8 @@ static int heap_prepare(fi_ctx *c, Exec &E) {
     c->strip_cache.clear();
     c->vmv_cache.clear();
     c->vmh_cache.clear();
+    c->hvv_cache.clear();
+    c->hvh_cache.clear();
     c->sc_cache.clear();
     c->imp_cache.clear();
     heap_reset(c);
@@ -976,6 +989,10 @@ struct BatchPlan {
   std::vector<int> vm_img;
   std::vector<const VmV *> vm_v;
   std::vector<const MfmaH *> vm_h;
+  std::vector<int> hv_img;
+  std::vector<const HvV *> hv_v;
+  std::vector<const HvH *> hv_h;
+  std::vector<int32_t> hv_W;  // source widths
   int h_tile_pitch = 0;  // k_rs_h_tile: max staged row bytes over the mode-2 images
   int h_tile_taps = 0;   // k_rs_h_tile: max horizontal window over the mode-2 images
   std::vector<size_t> res_off;    // per image: resized buffer in the workspace (smartcrop apply)
@@ -998,10 +1015,15 @@ struct BatchPlan {
   std::vector<MStrip> vstrips;
   std::vector<VTile> vtiles;
   size_t vm_lds = 0;
+  std::vector<HvDesc> hdescs;
+  std::vector<HvStripD> hstrips;
+  std::vector<HvTile> htiles;
+  size_t hv_lds = 0;
 };
 // Blob offsets and launch lists of a packed batch.
 struct Packed {
   size_t all_rd_off = 0, vdesc_off = 0, vstrip_off = 0, vtile_off = 0, apply_off = 0, mono_off = 0;
+  size_t hdesc_off = 0, hstrip_off = 0, htile_off = 0;
   size_t ai_off = 0, af_off = 0, ad_off = 0, mono_wts = 0;
   Launch L0, L1a, L2a, L2b, Q0, Q1a, Q2a, Q2b, CL[6];
   bool h_tiled = false;
@@ -1067,6 +1089,33 @@ static int64_t plan_resample(fi_ctx *c, Exec &E, BatchPlan &Bp, const ImPlan &P,
       Bp.vm_v.push_back(&vit->second);
       Bp.vm_h.push_back(hh);
       return strip_bytes;
+    }
+  }
+  // horizontal first: contiguous tap ranges (no sample pre-step), 16-byte aligned rows
+  if (fast_ok && P.hfirst && !P.sample && c->fused && c->hv_rs && aligned16) {
+    auto vit = c->hvv_cache.find(vt);
+    if (vit == c->hvv_cache.end()) {
+      HvV m;
+      if (!build_hv_v(*vt, &m)) m = HvV();
+      vit = c->hvv_cache.emplace(vt, std::move(m)).first;
+    }
+    auto hit = c->hvh_cache.find(ht);
+    if (hit == c->hvh_cache.end()) {
+      HvH m;
+      if (!build_hv_h(*ht, &m)) m = HvH();
+      for (const HvStrip &st : m.strips)
+        if (hv_lds_bytes(st.pp, st.nocb) > kVmMaxLds) m = HvH();
+      hit = c->hvh_cache.emplace(ht, std::move(m)).first;
+    }
+    if (vit->second.nblk > 0 && !hit->second.strips.empty()) {
+      d.mode = 6;  // streaming exact-integer MFMA, horizontal first
+      Bp.hv_img.push_back((int)Bp.rd.size());
+      Bp.hv_v.push_back(&vit->second);
+      Bp.hv_h.push_back(&hit->second);
+      Bp.hv_W.push_back(P.W);
+      int64_t cols = 0;
+      for (const HvStrip &st : hit->second.strips) cols += std::min(st.pp, P.W - st.px0);
+      return (int64_t)vit->second.nrows * cols * 3;
     }
   }
   if (vfirst_fast && !P.mono && d.h.maxtaps <= 64) {
@@ -1236,8 +1285,8 @@ static void plan_image(fi_ctx *c, Exec &E, BatchPlan &Bp, int i) {
     src_bytes = plan_resample(c, E, Bp, P, im, d);
   }
   Bp.resize_bytes += (double)src_bytes + (double)need;
-  static const char *kPath[6] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_none",
-                                 "path_vm"};
+  static const char *kPath[7] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_none",
+                                 "path_vm", "path_hv"};
   c->stats[kPath[d.mode]].launches += 1;  // images per resample path (fi_kernel_stats)
   Bp.rd_of[i] = (int)Bp.rd.size();
   Bp.rd.push_back(d);
@@ -1549,6 +1598,103 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
       if (i < q8[x].size()) Bp.vtiles.push_back(q8[x][i]);
 }
 
+// k_rs_hv workgroups: (image, strip, band of output blocks); bands only when
+// the horizontal-first images alone would not fill the chip (each band
+// re-produces the intermediate rows of its first block's window).
+static void build_hv_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
+  auto align4 = [&]() {
+    while (E.ai.size() % 4) E.ai.push_back(0);
+  };
+  auto put = [&](const std::vector<int32_t> &v) {
+    const int32_t o = E.oi();
+    E.ai.insert(E.ai.end(), v.begin(), v.end());
+    return o;
+  };
+  std::map<const HvH *, int32_t> splaced;  // first strip in Bp.hstrips
+  struct Work1 {
+    int32_t img, first_strip, nstrips, nblk;
+  };
+  std::vector<Work1> work;
+  for (size_t q = 0; q < Bp.hv_img.size(); q++) {
+    const ResizeDesc &d = Bp.rd[Bp.hv_img[q]];
+    const HvV &V = *Bp.hv_v[q];
+    const HvH &H = *Bp.hv_h[q];
+    auto vp = c->hvv_at.find(&V);
+    if (vp == c->hvv_at.end()) {
+      std::array<int32_t, 3> o;
+      o[0] = put(V.k0ks);
+      align4();
+      o[1] = put(V.frag);
+      o[2] = put(V.wsum);
+      vp = c->hvv_at.emplace(&V, o).first;
+    }
+    auto hp = c->hvh_at.find(&H);
+    if (hp == c->hvh_at.end()) {
+      std::array<int32_t, 3> o;
+      o[0] = put(H.w128);
+      align4();
+      o[1] = put(H.frag);
+      o[2] = put(H.s0);
+      hp = c->hvh_at.emplace(&H, o).first;
+    }
+    auto sp = splaced.find(&H);
+    if (sp == splaced.end()) {
+      const int32_t first = (int32_t)Bp.hstrips.size();
+      for (const HvStrip &st : H.strips) {
+        HvStripD m{};
+        m.x0 = st.x0;
+        m.x1 = st.x1;
+        m.px0 = st.px0;
+        m.pp = st.pp;
+        m.nocb = st.nocb;
+        m.frag = hp->second[1] + (int32_t)st.frag;
+        m.s0 = hp->second[2] + (int32_t)st.s0;
+        Bp.hstrips.push_back(m);
+        Bp.hv_lds = std::max(Bp.hv_lds, hv_lds_bytes(st.pp, st.nocb));
+      }
+      sp = splaced.emplace(&H, first).first;
+    }
+    HvDesc m{};
+    m.src = d.src;
+    m.src_stride = d.src_stride;
+    m.dst = d.dst;
+    m.dst_stride = d.dst_stride;
+    m.ew = d.ew;
+    m.eh = d.eh;
+    m.rot = d.rot;
+    m.gray = d.gray;
+    m.row0 = V.row0;
+    m.nrows = V.nrows;
+    m.nblk = V.nblk;
+    m.vk = vp->second[0];
+    m.vfrag = vp->second[1];
+    m.vws = vp->second[2];
+    m.hw128 = hp->second[0];
+    m.W = Bp.hv_W[q];
+    work.push_back({(int32_t)Bp.hdescs.size(), sp->second, (int32_t)H.strips.size(), V.nblk});
+    Bp.hdescs.push_back(m);
+  }
+  int64_t nst = 0;
+  for (const Work1 &w : work) nst += w.nstrips;
+  std::vector<std::vector<HvTile>> q8(8);  // XCD-aware order, as build_vm_tiles
+  for (size_t k = 0; k < work.size(); k++) {
+    const Work1 &w = work[k];
+    static const int64_t target = getenv("FI_HV_WGS") ? atoi(getenv("FI_HV_WGS")) : 8192;  // tuning
+    int bands = nst > 0 ? (int)((target + nst - 1) / nst) : 1;
+    bands = std::max(1, std::min(bands, w.nblk / 6));
+    for (int bnd = 0; bnd < bands; bnd++) {
+      const int b0 = (int)((int64_t)w.nblk * bnd / bands), b1 = (int)((int64_t)w.nblk * (bnd + 1) / bands);
+      if (b1 <= b0) continue;
+      for (int st = 0; st < w.nstrips; st++) q8[k % 8].push_back(HvTile{w.img, w.first_strip + st, b0, b1});
+    }
+  }
+  size_t mx = 0;
+  for (auto &q : q8) mx = std::max(mx, q.size());
+  for (size_t i = 0; i < mx; i++)
+    for (int x = 0; x < 8; x++)
+      if (i < q8[x].size()) Bp.htiles.push_back(q8[x][i]);
+}
+
 // Pack descriptors, tiles, launch lists and the batch's new heap tables into
 // the upload blob E.blob.
 static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
@@ -1565,6 +1711,9 @@ static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
   K.vdesc_off = B.addv(Bp.vdescs);
   K.vstrip_off = B.addv(Bp.vstrips);
   K.vtile_off = B.addv(Bp.vtiles);
+  K.hdesc_off = B.addv(Bp.hdescs);
+  K.hstrip_off = B.addv(Bp.hstrips);
+  K.htile_off = B.addv(Bp.htiles);
   for (auto &g : Bp.fgroups) g.second.off = B.addv(g.second.tiles);
   auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
   auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
@@ -1628,6 +1777,12 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
         launch_vm(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
                   (const VTile *)(ab + K.vtile_off), (int)Bp.vtiles.size(), ai, Bp.vm_lds) != 0)
       return set_err(FI_EDEVICE, "streaming MFMA resample launch rejected (LDS %zu)", Bp.vm_lds);
+    // (k_rs_hv on a stream of its own beside k_rs_vm was measured: cfg4 102.1
+    // vs 102.5 ms/step -- k_rs_vm's LDS leaves no CU room to overlap into)
+    if (!Bp.htiles.empty() &&
+        launch_hv(c->stream, (const HvDesc *)(ab + K.hdesc_off), (const HvStripD *)(ab + K.hstrip_off),
+                  (const HvTile *)(ab + K.htile_off), (int)Bp.htiles.size(), ai, Bp.hv_lds) != 0)
+      return set_err(FI_EDEVICE, "horizontal-first MFMA resample launch rejected (LDS %zu)", Bp.hv_lds);
     for (auto &g : Bp.fgroups) {
       const FusedGroup &G = g.second;
       if (G.tiles.empty()) continue;
@@ -1776,6 +1931,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async, std::shar
   build_fused_tiles(c, E, Bp);
   const double t_tiles0 = now_ms();
   build_vm_tiles(c, E, Bp);
+  build_hv_tiles(c, E, Bp);
   const double t_tiles = now_ms();
   Packed K;
   pack_batch(c, E, Bp, K);
@@ -2268,6 +2424,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   c->device = device;
   if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
+  if (const char *e = getenv("FI_DISABLE_HV_RS")) c->hv_rs = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
   if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');

@@ -207,6 +207,33 @@ constexpr int kVmOtileBytes = 16 * kVmOtilePitch * 2;
 constexpr int kVmOtile8Pitch = 64 * 3 + 4;     // 8-bit tile row (fast RGB path)
 constexpr int kVmOtile8Bytes = 16 * kVmOtile8Pitch;
 
+// k_rs_hv (fi_hv.hip): streaming exact-integer MFMA resample, horizontal first
+// (fi_plan.h HvH / HvV).
+struct HvDesc {               // one image
+  const uint8_t *src;
+  int64_t src_stride;
+  uint8_t *dst;
+  int64_t dst_stride;
+  int32_t ew, eh, rot, gray;
+  int32_t W;                  // source width (the staging's right edge)
+  int32_t row0, nrows, nblk;  // source rows [row0, row0 + nrows); 16-row output blocks
+  int32_t vk;                 // ai offset: per block (K0, ks)
+  int32_t vfrag;              // ai offset (16-B aligned): A fragments [block][t][limb][64 lanes][16 B]
+  int32_t vws;                // ai offset (16-B aligned): weight sum per output row
+  int32_t hw128;              // ai offset: 128 * horizontal weight sum per output px
+};
+struct HvStripD {             // fi_plan.h HvStrip placed in the arena
+  int32_t x0, x1, px0, pp, nocb;
+  int32_t frag, s0, pad;      // ai offsets (frag 16-B aligned)
+};
+struct HvTile {               // one workgroup: image x strip x output blocks [b0, b1)
+  int32_t img, strip, b0, b1;
+};
+constexpr int kHvThreads = 512;
+constexpr int kHvRing = 144;          // intermediate rows: a 128-row window at any production phase
+constexpr int kHvOpitch = 144;        // ring row bytes (48 px x 3 channels; 9 16-byte groups, odd)
+constexpr int kHvOtPitch = 48 * 3 + 4;  // Q16 output tile row, u16 units
+
 // fi_pixelate.hip: one ScaleImage pass of a face box (face-blur pixelation)
 struct PixPass {
   const uint8_t *src8;    // MODE 0: the crop's first byte in the 8-bit image

@@ -578,6 +578,124 @@ bool build_vm_v(const AxisTable &v, VmV *m) {
   return true;
 }
 
+// source-index range [a, e] of output o's non-zero taps (false: none)
+static bool src_range(const AxisTable &t, int o, int *a, int *e) {
+  *a = 1 << 30;
+  *e = -1;
+  for (int j = 0; j < t.count[o]; j++)
+    if (t.w[t.woff[o] + j] != 0.0f) {
+      *a = std::min(*a, t.start[o] + j);
+      *e = std::max(*e, t.start[o] + j);
+    }
+  return *e >= *a;
+}
+// quantized weight of output o at source index s (0 if not a tap)
+static int32_t tap_w_src(const AxisTable &t, int o, int s) {
+  const int j = s - t.start[o];
+  return (j < 0 || j >= t.count[o]) ? 0 : quant_w(t.w[t.woff[o] + j]);
+}
+// per-output tap ranges, monotone in o (false otherwise)
+static bool monotone_ranges(const AxisTable &t, std::vector<int> *lo, std::vector<int> *hi) {
+  const int n = (int)t.start.size();
+  lo->resize(n);
+  hi->resize(n);
+  for (int o = 0; o < n; o++) {
+    if (!src_range(t, o, &(*lo)[o], &(*hi)[o])) return false;
+    if (o > 0 && ((*lo)[o] < (*lo)[o - 1] || (*hi)[o] < (*hi)[o - 1])) return false;
+  }
+  return true;
+}
+
+bool build_hv_h(const AxisTable &h, HvH *m) {
+  *m = HvH();
+  const int nx = (int)h.start.size();
+  std::vector<int> lo, hi;
+  if (nx == 0 || !monotone_ranges(h, &lo, &hi)) return false;
+  m->w128.assign(nx, 0);
+  for (int x = 0; x < nx; x++)
+    for (int j = 0; j < h.count[x]; j++) m->w128[x] += 128 * quant_w(h.w[h.woff[x] + j]);
+  m->col0 = lo[0];
+  // strip [x0, x1): window starts / k-steps per 16-px block (false: a block
+  // needs more than 2 k-steps or the window more than kHvMaxPP px)
+  auto try_strip = [&](int x0, int x1, HvStrip *S, std::vector<int32_t> *s0) {
+    S->x0 = x0;
+    S->x1 = x1;
+    S->px0 = lo[x0] / 16 * 16;
+    S->nocb = (x1 - x0 + 15) / 16;
+    int pp = 0;
+    s0->clear();
+    for (int ob = 0; ob < S->nocb; ob++) {
+      const int xa = x0 + 16 * ob, xb = std::min(x1, xa + 16);
+      const int w0 = (lo[xa] - S->px0) / 8 * 8;
+      const int ks = (hi[xb - 1] + 1 - S->px0 - w0 + 63) / 64;
+      if (ks > 2) return false;
+      s0->push_back(w0);
+      s0->push_back(ks);
+      pp = std::max(pp, w0 + 64 * ks);
+    }
+    S->pp = (pp + 15) / 16 * 16;
+    return S->pp <= kHvMaxPP;
+  };
+  for (int x0 = 0; x0 < nx;) {
+    HvStrip S{};
+    std::vector<int32_t> s0;
+    int x1 = std::min(nx, x0 + kHvMaxNx);
+    while (!try_strip(x0, x1, &S, &s0)) {
+      if (x1 - x0 <= 16) return false;
+      x1 = x0 + (x1 - x0 - 1) / 16 * 16;
+    }
+    S.s0 = m->s0.size();
+    m->s0.insert(m->s0.end(), s0.begin(), s0.end());
+    S.frag = m->frag.size();
+    m->frag.resize(m->frag.size() + (size_t)S.nocb * 2 * 3 * 256, 0);
+    for (int ob = 0; ob < S.nocb; ob++)
+      for (int t = 0; t < 2; t++)
+        for (int l = 0; l < 64; l++)
+          for (int j = 0; j < 16; j++) {
+            const int x = x0 + 16 * ob + (l & 15);
+            const int s = S.px0 + s0[2 * ob] + 64 * t + mfma_i8_k(l, j);
+            int32_t limb[3];
+            limbs3(t < s0[2 * ob + 1] && x < x1 ? tap_w_src(h, x, s) : 0, limb);
+            put_frag(m->frag, S.frag + (size_t)(ob * 2 + t) * 3 * 256, l, j, limb);
+          }
+    m->strips.push_back(S);
+    x0 = x1;
+  }
+  return true;
+}
+
+bool build_hv_v(const AxisTable &v, HvV *m) {
+  *m = HvV();
+  const int ny = (int)v.start.size();
+  std::vector<int> lo, hi;
+  if (ny == 0 || !monotone_ranges(v, &lo, &hi)) return false;
+  m->row0 = lo[0];
+  m->nrows = hi[ny - 1] + 1 - m->row0;
+  m->nblk = (ny + 15) / 16;
+  m->frag.assign((size_t)m->nblk * 2 * 3 * 256, 0);
+  m->wsum.assign((size_t)16 * m->nblk, 0);
+  for (int b = 0; b < m->nblk; b++) {
+    const int ye = std::min(ny, 16 * b + 16);
+    const int K0 = lo[16 * b] - m->row0;
+    const int ks = (hi[ye - 1] + 1 - m->row0 - K0 + 63) / 64;
+    if (ks > 2) return false;
+    m->k0ks.push_back(K0);
+    m->k0ks.push_back(ks);
+    for (int t = 0; t < ks; t++)
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int y = 16 * b + (l & 15);
+          const int s = m->row0 + K0 + 64 * t + mfma_i8_k(l, j);
+          int32_t limb[3];
+          limbs3(y < ny ? tap_w_src(v, y, s) : 0, limb);
+          put_frag(m->frag, (size_t)(b * 2 + t) * 3 * 256, l, j, limb);
+        }
+  }
+  for (int y = 0; y < ny; y++)
+    for (int j = 0; j < v.count[y]; j++) m->wsum[y] += quant_w(v.w[v.woff[y] + j]);
+  return true;
+}
+
 
 bool build_ring(const AxisTable &v, RingTable *rt) {
   *rt = RingTable();

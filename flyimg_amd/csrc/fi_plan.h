@@ -109,6 +109,38 @@ struct VmV {
 };
 bool build_vm_v(const AxisTable &v, VmV *m);
 
+// Tables of k_rs_hv (fi_hv.hip): the horizontal-first streaming kernel.  Both
+// axes must touch a contiguous range of source rows / columns (always the case
+// without the ThumbnailImage sample pre-step, and a horizontal-first geometry
+// never has one: the sampled factors are equal).
+//   horizontal  column strips of <= kHvMaxNx output px; the strip's source
+//               window [px0, px0 + pp) starts on a 16-px boundary (48 bytes:
+//               whole pixels, 16-byte aligned loads); per 16-px output block a
+//               window start w0 (8-aligned, relative to px0) and <= 2 k-steps
+//               of 64 columns, B fragments [block][t][limb] (t < 2, zero past ks);
+//   vertical    per 16-row output block a window start K0 (touched-row list
+//               index, nondecreasing) and <= 2 k-steps of 64 rows, A fragments
+//               [block][t][limb], and the weight sum of every output row.
+constexpr int kHvMaxNx = 48;     // output px per strip: 3 16-px blocks (32-px strips measured slower: 21.7 vs 18.7 ms, cfg4 8192-image run)
+constexpr int kHvMaxPP = 256;    // source px of a strip window
+struct HvStrip {
+  int32_t x0, x1, px0, pp, nocb;
+  size_t frag, s0;               // offsets into HvH::frag / s0
+};
+struct HvH {
+  int32_t col0 = 0;              // touched columns = [col0, col0 + ncols)
+  std::vector<HvStrip> strips;
+  std::vector<int32_t> frag, s0, w128;  // w128: 128 * weight sum per output px
+};
+bool build_hv_h(const AxisTable &h, HvH *m);
+struct HvV {
+  int32_t row0 = 0, nrows = 0, nblk = 0;
+  std::vector<int32_t> k0ks;     // per block: K0, ks
+  std::vector<int32_t> frag;     // [block][t < 2][limb][256]
+  std::vector<int32_t> wsum;     // [16 nblk] weight sum per output row
+};
+bool build_hv_v(const AxisTable &v, HvV *m);
+
 // Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)
 // to `out_size`; taps mapped back to the `in_src` source indices through the
 // SampleImage offsets (identity when !sample) and merged.

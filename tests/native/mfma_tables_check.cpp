@@ -164,6 +164,81 @@ static void check_h(const AxisTable &h, const char *name) {
   printf("  %s: horizontal %zu strips ok\n", name, m.strips.size());
 }
 
+// k_rs_hv: the horizontal pass over each strip's plane window and the
+// vertical pass over each block's ring window, with the kernel's algebra
+// (H: sum W (p - 128) + 128 sum W; V: 256 sum W (Vh - 128) + sum W (Vl - 128)
+// + 32896 sum W) against sum(quant(w) * value).
+static void check_hv(const AxisTable &h, const AxisTable &v, const char *name) {
+  HvH mh;
+  HvV mv;
+  if (!build_hv_h(h, &mh) || !build_hv_v(v, &mv)) {
+    printf("  %s: horizontal-first tables not built, skipped\n", name);
+    CHECK(!g_required, "%s: horizontal-first tables required", name);
+    return;
+  }
+  std::mt19937 rng(77);
+  std::vector<int> P(h.src_hi + kHvMaxPP), V(v.src_hi);
+  for (auto &x : P) x = (int)(rng() & 255);
+  for (auto &x : V) x = (int)(rng() % 65536);
+  const int nx = (int)h.start.size(), ny = (int)v.start.size();
+  int covered = 0;
+  for (const HvStrip &S : mh.strips) {
+    CHECK(S.px0 % 16 == 0 && S.pp % 16 == 0 && S.pp <= kHvMaxPP && S.x1 - S.x0 <= kHvMaxNx, "%s: strip", name);
+    for (int ob = 0; ob < S.nocb; ob++) {
+      const int w0 = mh.s0[S.s0 + 2 * ob], ks = mh.s0[S.s0 + 2 * ob + 1];
+      CHECK(w0 % 8 == 0 && ks >= 1 && ks <= 2 && w0 + 64 * ks <= S.pp, "%s: horizontal window", name);
+      for (int n = 0; n < 16; n++) {
+        const int x = S.x0 + 16 * ob + n;
+        if (x >= S.x1) continue;
+        covered++;
+        int64_t acc = mh.w128[x];
+        for (int t = 0; t < 2; t++)
+          for (int l = 0; l < 64; l++) {
+            if ((l & 15) != n) continue;
+            for (int j = 0; j < 16; j++) {
+              const int64_t w = limb_w(mh.frag, S.frag + (size_t)(ob * 2 + t) * 3 * 256, l, j);
+              if (w == 0) continue;
+              CHECK(t < ks, "%s: horizontal weight past ks", name);
+              acc += w * (P[S.px0 + w0 + 64 * t + mfma_i8_k(l, j)] - 128);
+            }
+          }
+        int64_t ref = 0;
+        for (int j = 0; j < h.count[x]; j++) ref += (int64_t)qw(h.w[h.woff[x] + j]) * P[h.start[x] + j];
+        CHECK(acc == ref, "%s: hv horizontal x=%d %lld != %lld", name, x, (long long)acc, (long long)ref);
+      }
+    }
+  }
+  CHECK(covered == nx, "%s: hv strips cover %d of %d px", name, covered, nx);
+  for (int b = 0; b < mv.nblk; b++) {
+    const int K0 = mv.k0ks[2 * b], ks = mv.k0ks[2 * b + 1];
+    CHECK(ks >= 1 && ks <= 2 && (b == 0 || K0 >= mv.k0ks[2 * b - 2]), "%s: vertical window %d", name, b);
+    for (int n = 0; n < 16; n++) {
+      const int y = 16 * b + n;
+      if (y >= ny) continue;
+      int64_t sh = 0, sl = 0;
+      for (int t = 0; t < 2; t++)
+        for (int l = 0; l < 64; l++) {
+          if ((l & 15) != n) continue;
+          for (int j = 0; j < 16; j++) {
+            const int64_t w = limb_w(mv.frag, (size_t)(b * 2 + t) * 3 * 256, l, j);
+            if (w == 0) continue;
+            const int k = K0 + 64 * t + mfma_i8_k(l, j);
+            CHECK(t < ks && k < mv.nrows, "%s: vertical weight outside the window", name);
+            const int val = V[mv.row0 + k];
+            sh += w * ((val >> 8) - 128);
+            sl += w * ((val & 255) - 128);
+          }
+        }
+      const int64_t s = 256 * sh + sl + 32896 * (int64_t)mv.wsum[y];
+      int64_t ref = 0;
+      for (int j = 0; j < v.count[y]; j++) ref += (int64_t)qw(v.w[v.woff[y] + j]) * V[v.start[y] + j];
+      CHECK(s == ref, "%s: hv vertical y=%d %lld != %lld", name, y, (long long)s, (long long)ref);
+      CHECK(llabs(sh) < (1ll << 31) && llabs(sl) < (1ll << 31), "%s: vertical limb sum exceeds int32", name);
+    }
+  }
+  printf("  %s: horizontal-first %zu strips, %d blocks ok\n", name, mh.strips.size(), mv.nblk);
+}
+
 static void check_pillow(int W, int H, int tw, int th, const char *name) {
   fi_smartcrop_options o;
   o.prescale = 1;
@@ -221,8 +296,13 @@ static void geometry(int W, int H, int tw, int th, uint32_t flags, const char *n
   AxisTable v, h;
   build_axis(P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &v);
   build_axis(P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &h);
-  check_h(h, name);
-  check_vm(v, name);
+  if (P.hfirst) {
+    CHECK(!P.sample, "%s: horizontal-first with the sample pre-step", name);
+    check_hv(h, v, name);
+  } else {
+    check_h(h, name);
+    check_vm(v, name);
+  }
 }
 
 int main() {
@@ -241,6 +321,18 @@ int main() {
   geometry(4000, 3000, 0, 300, T | S, "h_300 on 4000x3000");
   geometry(1600, 1200, 400, 400, T | F | X, "1600x1200 400x400 c_1");
   geometry(6000, 400, 60, 0, T | S, "factor 0.01 no sample");
+  // horizontal-first (tests/test_gpu_parity.py HV_CASES): k_rs_hv tables required
+  const uint32_t R = FI_OP_RESIZE;
+  g_required = true;
+  geometry(1000, 702, 640, 0, R | S, "hv 1000x702 -> 640");
+  geometry(1500, 1000, 500, 0, R | S, "hv 1500x1000 -> 500 (1/3)");
+  geometry(2000, 1497, 500, 0, R | S, "hv 2000x1497 -> 500 (1/4)");
+  geometry(2500, 1497, 500, 0, R | S, "hv 2500x1497 -> 500 (1/5)");
+  geometry(901, 600, 250, 300, R | F | X, "hv fill 901x600 250x300");
+  geometry(125, 91, 300, 0, T, "hv enlarge 125x91 -> 300");
+  geometry(4000, 702, 2600, 0, R | S, "hv 4000x702 -> 2600");
+  g_required = false;
+  geometry(3000, 2001, 450, 0, R | S, "hv 3000x2001 -> 450 (0.15: two-pass)");
   check_pillow(500, 281, 100, 100, "smartcrop 500x281");
   check_pillow(400, 400, 100, 100, "smartcrop 400x400");
   check_pillow(512, 512, 100, 100, "smartcrop 512x512");

@@ -45,14 +45,14 @@ def _context_with(env):
 
 
 _ENV = {"FI_DISABLE_FUSED": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0",
-        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0", "FI_DISABLE_SC_FZ": "0"}
+        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0", "FI_DISABLE_SC_FZ": "0", "FI_DISABLE_HV_RS": "0"}
 PATHS = {
-    # default kernels: k_rs_vm streaming MFMA resample; k_sc_fz fused prescale + maps; k_sc_score2
+    # default kernels: k_rs_vm / k_rs_hv streaming MFMA resample; k_sc_fz fused prescale + maps; k_sc_score2
     "vm": dict(_ENV),
     # the unfused MFMA prescale: k_sc_hmfma + k_sc_vq (H-stage rows through HBM)
     "nofz": dict(_ENV, FI_DISABLE_SC_FZ="1"),
     # VALU fused resample (k_rs_fused); VALU vertical prescale + maps (k_sc_vmaps)
-    "valu": dict(_ENV, FI_DISABLE_VM_RS="1", FI_DISABLE_SC_VQ="1"),
+    "valu": dict(_ENV, FI_DISABLE_VM_RS="1", FI_DISABLE_HV_RS="1", FI_DISABLE_SC_VQ="1"),
     # default resample with the VALU horizontal prescale (k_sc_hrows)
     "schrows": dict(_ENV, FI_DISABLE_SC_MFMA="1"),
     # generic kernels: two-pass resample; per-row prescale/maps kernels
@@ -278,6 +278,63 @@ def test_resize_edge_geometries(rctx, case):
     assert np.abs(out.astype(np.int16) - ref.astype(np.int16)).max() <= 1
 
 
+R_ = F.FI_OP_RESIZE | F.FI_GEOM_SHRINK_ONLY
+HV_CASES = [
+    # (name, W, H, target_w, target_h, flags, rotate, gravity, takes k_rs_hv): horizontal-first
+    # geometries (x_factor > y_factor after ParseMetaGeometry's rounding)
+    ("hv_0.64", 1000, 702, 640, 0, R_, 0, "Center", True),             # 1 k-step, right-edge tail group
+    ("hv_thumb_0.64", 1000, 702, 640, 0, F.FI_OP_THUMBNAIL | F.FI_GEOM_SHRINK_ONLY, 0, "Center", True),
+    ("hv_third", 1500, 1000, 500, 0, R_, 0, "Center", True),           # windows of 1 and 2 k-steps
+    ("hv_quarter", 2000, 1497, 500, 0, R_, 0, "Center", True),         # 2 k-steps both passes
+    ("hv_fifth", 2500, 1497, 500, 0, R_, 0, "Center", True),           # 32-px strips (48 px exceed the window)
+    ("hv_fill_rot270", 901, 600, 250, 300, F.FI_OP_RESIZE | F.FI_GEOM_FILL | F.FI_OP_EXTENT | F.FI_OP_ROTATE,
+     270, "Center", True),
+    ("hv_fill_north", 1003, 700, 300, 300, F.FI_OP_RESIZE | F.FI_GEOM_FILL | F.FI_OP_EXTENT, 0, "North", True),
+    ("hv_gray_rot90", 1000, 702, 640, 0, R_ | F.FI_OP_GRAY | F.FI_OP_ROTATE, 90, "Center", True),
+    ("hv_gray_rot180", 640, 481, 317, 0, R_ | F.FI_OP_GRAY | F.FI_OP_ROTATE, 180, "Center", True),
+    ("hv_enlarge_mitchell", 125, 91, 300, 0, F.FI_OP_THUMBNAIL, 0, "Center", True),
+    ("hv_wide_bands", 4000, 702, 2600, 0, R_, 0, "Center", True),      # 55 strips x bands of blocks
+    ("hv_tall", 640, 2999, 317, 0, R_, 0, "Center", True),
+    ("hv_0.15_generic", 3000, 2001, 450, 0, R_, 0, "Center", False),  # windows > 2 k-steps: two-pass kernels
+]
+
+
+@pytest.mark.parametrize("case", HV_CASES, ids=[c[0] for c in HV_CASES])
+def test_horizontal_first_within_one_lsb_of_oracle(rctx, case):
+    """Horizontal-first geometries (IM runs HorizontalFilter first): the
+    streaming k_rs_hv on the default path, the two-pass kernels on the others
+    -- +-1 LSB of the oracle, exact-match fraction >= 0.98 -- and the path
+    actually taken is the one named."""
+    name, W, H, tw, th, flags, rot, grav, hv = case
+    src = synth_rgb(W, H, 31 + W + H)
+    g = L.GRAVITY[grav]
+    before = {p: rctx.stats(p)[1] for p in ("path_hv", "path_generic_h")}
+    outs, recs, rc = rctx.process([src], [Op(tw, th, flags, g, rot)])
+    assert rc == 0 and recs[0].status == 0, L.lib().fi_last_error()
+    want = "path_hv" if hv and rctx.path_name in ("vm", "nofz", "schrows") else "path_generic_h"
+    assert rctx.stats(want)[1] == before[want] + 1, (want, {p: rctx.stats(p)[1] - before[p] for p in before})
+    ref = orc.im_convert(src, tw, th, _oracle_flags(flags), gravity=g, rotate=rot)
+    _cmp(outs[0], ref, name)
+
+
+def test_horizontal_first_monochrome(ctx):
+    """-monochrome on a horizontal-first geometry: k_rs_hv's Q16 gray epilogue
+    feeds fi_mono.hip (the error diffusion is chaotic in its +-1 LSB input:
+    its invariants, as test_monochrome_pipeline_resized)."""
+    from flyimg_amd.processor import ImageProcessor, OptionsBag
+
+    src = synth_rgb(1000, 702, 5)
+    op = ImageProcessor(OptionsBag("w_640,mnchr_1"), 1000, 702).to_op()
+    before = ctx.stats("path_hv")[1]
+    outs, recs, rc = ctx.process([src], [op])
+    assert rc == 0 and recs[0].status == 0
+    assert ctx.stats("path_hv")[1] == before + 1
+    ref = orc.im_convert(src, op.target_w, op.target_h, _oracle_flags(op.flags) | orc.FLAG_MONO)
+    out = outs[0]
+    assert out.shape == ref.shape and set(np.unique(out)) <= {0, 255}
+    assert abs(out.mean() - ref.mean()) / 255 < 0.01
+
+
 def test_mixed_batch_one_call(rctx):
     ctx = rctx
     imgs, ops, refs = [], [], []
@@ -370,11 +427,11 @@ def test_cfg4_slice_one_batch(ctx):
         smc.append(bool(op.flags & L.FI_OP_SMARTCROP))
         ops.append(Op(op.target_w, op.target_h, op.flags & ~L.FI_OP_SMARTCROP_APPLY, op.gravity, op.rotate,
                       100, 100))
-    h_before = ctx.stats("path_generic_h")[1]
+    h_before = ctx.stats("path_hv")[1]
     vm_before = ctx.stats("path_vm")[1]
     outs, recs, rc = ctx.process(srcs, ops)
     assert rc == 0, L.lib().fi_last_error()
-    assert ctx.stats("path_generic_h")[1] > h_before, "no horizontal-first geometry in the slice"
+    assert ctx.stats("path_hv")[1] > h_before, "no horizontal-first geometry in the slice"
     assert ctx.stats("path_vm")[1] > vm_before
 
     def check(j):
@@ -997,7 +1054,7 @@ def test_mixed_batch_every_path_one_call(ctx):
 
     cases = [
         (synth_rgb(1920, 1080, 1), "w_500"),                       # vm
-        (synth_rgb(900, 300, 2), "w_120"),                         # H-first generic
+        (synth_rgb(900, 300, 2), "w_120"),                         # H-first (k_rs_hv)
         (_rgba(640, 480, 3), "w_150,h_150,c_1,r_180"),             # RGBA
         (synth_rgb(900, 600, 4), "w_300,h_200,c_1,r_270,clsp_Gray,sh_3"),  # conv, gray, rotate
         (synth_rgb(1280, 720, 5), "w_500,blr_1x2"),                # conv
