@@ -90,6 +90,13 @@ __device__ __forceinline__ int32_t vm_fold3(int32_t d0, int32_t d1, int32_t d2) 
 }
 
 // per-workgroup phase sums of MODE 9 (read by fi_debug_vm_stamps)
+// Channel-plane stride = 16 vpitch + kVmPlanePad bytes, 44 (mod 64) dwords: the
+// plane writes of a block (lane = byte column (px, channel) x 4-row group)
+// put the 16 (column, channel) pairs of a tile on 16 distinct bank quads, key
+// = ci + 11 channel (mod 16), at every pixel phase of the tile's first byte.
+// Without it (stride = 0 mod 64 dwords) the three channels of a pixel hit one
+// bank: 62 M of k_rs_vm's 79 M LDS bank-conflict cycles (PMC, ablation 5).
+constexpr int kVmPlanePad = 176;
 constexpr int kVmStampSlots = 4096;
 constexpr int kVmStampN = 12;  // phase sums + piece count per workgroup
 __device__ uint64_t g_vm_stamps[kVmStampSlots * (kVmStampN + 1)];
@@ -122,7 +129,7 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
   //                     [output tile: 8-bit or Q16][horizontal fragments]
   uint8_t *apl = lds + kVmChunkBytes;
   uint8_t *vpl = apl + kVmABytes;
-  const int plane = 16 * S.vpitch;  // one limb plane of one channel
+  const int plane = 16 * S.vpitch + kVmPlanePad;  // one limb plane of one channel
   uint16_t *otile = reinterpret_cast<uint16_t *>(vpl + 6 * plane);  // [16][kVmOtilePitch] Q16
   uint8_t *otile8 = vpl + 6 * plane;                                 // [16][kVmOtile8Pitch]
   i32x4 *hbl = reinterpret_cast<i32x4 *>(vpl + 6 * plane + (fast8 ? kVmOtile8Bytes : kVmOtileBytes));  // [nocb][ks][3][64]
@@ -487,7 +494,8 @@ int vm_read_stamps(uint64_t *out, int slots) {
 
 // piece buffer + A fragments + Q16 planes + output tile + the strip's horizontal fragments
 size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16) {
-  return (size_t)kVmChunkBytes + kVmABytes + (size_t)6 * 16 * vpitch + (q16 ? kVmOtileBytes : kVmOtile8Bytes) +
+  return (size_t)kVmChunkBytes + kVmABytes + (size_t)6 * (16 * vpitch + kVmPlanePad) +
+         (q16 ? kVmOtileBytes : kVmOtile8Bytes) +
          (size_t)nocb * ks * 3 * 1024;
 }
 
