@@ -448,7 +448,7 @@ constexpr int kFzRing = 80;  // a 64-row window at any 16-row block alignment
 #define FI_FZ_THREADS 512
 #endif
 constexpr int kFzThreads = FI_FZ_THREADS;  // 8 waves; two workgroups per CU (LDS)
-__global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restrict__ descs,
+__global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restrict__ descs,
                                                         const int32_t *__restrict__ ai, const ScParamsDev P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
   const ScDesc &D = descs[blockIdx.x];
@@ -537,69 +537,6 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
       }
     }
   };
-  // One item per thread (nitem <= kFzThreads: source rows of <= 512 px): the
-  // next block's three 16-byte loads are issued before the current block's
-  // horizontal pass (pf_load) and deinterleaved after it (pf_store); wider rows
-  // take stage_block.
-  const bool pf = nitem <= kFzThreads;
-  const int prr = tid / ng, pg = tid - prr * ng;
-  u32x4a pq[3];
-  bool pfast = false;
-  auto pf_load = [&](int r0) {
-    pfast = tid < nitem && r0 + prr < hrows && sC == 3 && a4 && 16 * pg + 16 <= sW;
-    if (pfast) {
-      const uint8_t *s = src + (int64_t)(r0 + prr + yoff) * sstride;
-#pragma unroll
-      for (int k = 0; k < 3; k++) pq[k] = *reinterpret_cast<const u32x4a *>(s + 48 * pg + 16 * k);
-    }
-  };
-  auto pf_store = [&](int r0) {
-    if (tid >= nitem) return;
-    const int rr = prr, g = pg;
-    const bool rowok = r0 + rr < hrows;
-    const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride;
-    u32x4s w0, w1, w2;
-    if (pfast) {
-      const uint32_t d[12] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y,
-                              pq[1].z, pq[1].w, pq[2].x, pq[2].y, pq[2].z, pq[2].w};
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t a0 = d[3 * k], a1 = d[3 * k + 1], a2 = d[3 * k + 2];
-        w0[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00060300u), 0x05020100u) ^ 0x80808080u;
-        w1[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00070401u), 0x06020100u) ^ 0x80808080u;
-        w2[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00000502u), 0x07040100u) ^ 0x80808080u;
-      }
-    } else {
-#pragma unroll 1
-      for (int k = 0; k < 4; k++) {
-        uint32_t a = 0, b = 0, c = 0;
-#pragma unroll 1
-        for (int j = 0; j < 4; j++) {
-          const int x = 16 * g + 4 * k + j;
-          const bool ok = rowok && x < sW;
-          uint32_t vr, vg, vb;
-          if (sC == 3) {
-            vr = ok ? s[3 * x] : 128u;
-            vg = ok ? s[3 * x + 1] : 128u;
-            vb = ok ? s[3 * x + 2] : 128u;
-          } else {
-            vr = vg = vb = ok ? s[x] : 128u;
-          }
-          a |= vr << (8 * j);
-          b |= vg << (8 * j);
-          c |= vb << (8 * j);
-        }
-        w0[k] = a ^ 0x80808080u;
-        w1[k] = b ^ 0x80808080u;
-        w2[k] = c ^ 0x80808080u;
-      }
-    }
-    *reinterpret_cast<u32x4s *>(shared + (0 * 16 + rr) * PP + 16 * g) = w0;
-    if (nch == 3) {
-      *reinterpret_cast<u32x4s *>(shared + (1 * 16 + rr) * PP + 16 * g) = w1;
-      *reinterpret_cast<u32x4s *>(shared + (2 * 16 + rr) * PP + 16 * g) = w2;
-    }
-  };
   const int32_t *hmS0 = ai + D.hmS0, *hmC = ai + D.hmC;
   const i32x4 *hmB = reinterpret_cast<const i32x4 *>(ai + D.hmB);
   const int k0l = mfma_i8_k(lane, 0), k8l = mfma_i8_k(lane, 8);
@@ -655,16 +592,9 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
   for (int c = 0; c < chunks; c++) {
     const int k0 = ai[D.vqK0 + c];
     const int need = min(k0 + 64, hrows);
-    bool have = false;  // this block's loads already issued (prefetch within the chunk)
     while (produced < need) {
-      if (pf && !have) pf_load(produced);
       __syncthreads();  // the shared region's previous readers (vertical phase) are done
-      if (pf)
-        pf_store(produced);
-      else
-        stage_block(produced);
-      have = pf && produced + 16 < need;
-      if (have) pf_load(produced + 16);
+      stage_block(produced);
       __syncthreads();
       hpass(produced);
       produced += 16;
