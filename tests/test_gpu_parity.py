@@ -295,6 +295,9 @@ HV_CASES = [
     ("hv_enlarge_mitchell", 125, 91, 300, 0, F.FI_OP_THUMBNAIL, 0, "Center", True),
     ("hv_wide_bands", 4000, 702, 2600, 0, R_, 0, "Center", True),      # 55 strips x bands of blocks
     ("hv_tall", 640, 2999, 317, 0, R_, 0, "Center", True),
+    ("hv_tiny", 40, 23, 30, 0, R_, 0, "Center", True),                 # one block, one 16-px group, tail path
+    ("hv_fill_rows_cropped", 700, 1002, 300, 300, F.FI_OP_RESIZE | F.FI_GEOM_FILL | F.FI_OP_EXTENT, 0, "South",
+     True),                                                             # extent window offset in y
     ("hv_0.15_generic", 3000, 2001, 450, 0, R_, 0, "Center", False),  # windows > 2 k-steps: two-pass kernels
 ]
 
