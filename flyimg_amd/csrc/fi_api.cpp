@@ -634,13 +634,6 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     L->plans.push_back(&P);
     ScDesc d{};
     d.result = it.result;
-    if (P.status == FI_OK && (int)P.crops.size() > kScoreMaxCrops) {
-      (*status)[k] = FI_EUNSUPPORTED;
-      (*errs)[k] = "smartcrop: " + std::to_string(P.crops.size()) + " crop windows (max " +
-                   std::to_string(kScoreMaxCrops) + ")";
-      L->descs.push_back(d);
-      continue;
-    }
     if (P.status != FI_OK) {
       (*status)[k] = P.status;
       (*errs)[k] = P.err;

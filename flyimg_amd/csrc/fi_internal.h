@@ -146,7 +146,8 @@ constexpr int kPrepMaxLds = 64 * 1024;
 // kFzRing (80) H-stage rows + max(3 source planes of 16 rows, 16 prescaled rows
 // + luma); <= 80 KB keeps two workgroups per CU
 constexpr int kFzMaxLds = 80 * 1024;
-// k_sc_score2: maps resident in LDS when aw*ah*4 <= this; crops per image.
+// k_sc_score2: maps resident in LDS when aw*ah*4 <= this; crops whose totals /
+// bounds / candidate list stay in LDS (more: the image's CropScore slots).
 constexpr int kScoreLdsMaps = 112 * 1024;
 constexpr int kScoreMaxCrops = 1024;
 

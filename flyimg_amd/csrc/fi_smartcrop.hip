@@ -674,10 +674,15 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
   __shared__ double s_tot[kScoreMaxCrops];
   __shared__ double s_bnd[kScoreMaxCrops];
   __shared__ int32_t cand[kScoreMaxCrops];
-  __shared__ int32_t ncand_s;
+  __shared__ int32_t ncand_s, first_cand_s;
   const ScDesc &D = descs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ncrops = D.ncrops;
+  // more crops than the LDS arrays hold (analysed images beyond ~14:1, or a
+  // small step): totals, bounds and the candidate marks live in the image's
+  // CropScore slots instead (exact = 2 marks a candidate until re-scored)
+  const bool big = ncrops > kScoreMaxCrops;
+  CropScore *const sco = scores + D.score0;
   const int W = D.aw, H = D.ah, npx = W * H;
   const uint32_t *maps = D.maps;
   if (LDS_MAPS) {
@@ -765,9 +770,11 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
       const double mag = fabs(wd) * (fabs(Fd) + Ed) + fabs(ws) * (fabs(Fs) + Es) + fabs(wt) * (fabs(Ft) + Et);
       const double B = ((fabs(wd) * Ed + fabs(ws) * Es + fabs(wt) * Et) * (1.0 + 16.0 * u) + 16.0 * u * mag) /
                        area * 1.01;
-      s_tot[c] = tot;
-      s_bnd[c] = B;
-      CropScore &o = scores[D.score0 + c];
+      if (!big) {
+        s_tot[c] = tot;
+        s_bnd[c] = B;
+      }
+      CropScore &o = sco[c];
       o.detail = Fd;
       o.saturation = Ft;
       o.skin = Fs;
@@ -778,21 +785,32 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
   }
   __syncthreads();
   // candidates: every crop whose interval reaches the best lower bound
+  auto tot_of = [&](int c) { return big ? sco[c].total : s_tot[c]; };
+  auto bnd_of = [&](int c) { return big ? sco[c].bound : s_bnd[c]; };
   if (tid == 0) {
     double best_lo = -1.0e308;
-    for (int c = 0; c < ncrops; c++) best_lo = fmax(best_lo, s_tot[c] - s_bnd[c]);
-    int k = 0;
+    for (int c = 0; c < ncrops; c++) best_lo = fmax(best_lo, tot_of(c) - bnd_of(c));
+    int k = 0, first = -1;
     for (int c = 0; c < ncrops; c++)
-      if (D.exact_all || s_tot[c] + s_bnd[c] >= best_lo) cand[k++] = c;
+      if (D.exact_all || tot_of(c) + bnd_of(c) >= best_lo) {
+        if (first < 0) first = c;
+        if (big)
+          sco[c].exact = 2;
+        else
+          cand[k] = c;
+        k++;
+      }
     ncand_s = k;
+    first_cand_s = first;
   }
   __syncthreads();
   const int ncand = ncand_s;
   const bool need_exact = D.exact_all || ncand > 1;
   if (need_exact) {
     // exact re-score: one lane per candidate, the reference's row-major order
-    for (int k = tid; k < ncand; k += kScoreThreads) {
-      const int c = cand[k];
+    for (int k = tid; k < (big ? ncrops : ncand); k += kScoreThreads) {
+      if (big && sco[k].exact != 2) continue;
+      const int c = big ? k : cand[k];
       const DevCrop cr = crops[D.crop0 + c];
       const double *tab = ad + cr.table;
       double skin = 0, detail = 0, sat = 0;
@@ -813,8 +831,8 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
         }
       }
       const double tot = (detail * wd + skin * ws + sat * wt) / (cr.fw * cr.fh);
-      s_tot[c] = tot;
-      CropScore &o = scores[D.score0 + c];
+      if (!big) s_tot[c] = tot;
+      CropScore &o = sco[c];
       o.detail = detail;
       o.saturation = sat;
       o.skin = skin;
@@ -825,18 +843,22 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
     __syncthreads();
   }
   if (tid == 0) {
-    int top = cand[0];
-    double best = s_tot[top];
+    int top = first_cand_s;
+    double best = tot_of(top);
     if (need_exact) {
       best = -9223372036854775807.0;  // -sys.maxsize; strict > keeps the first max
-      for (int k = 0; k < ncand; k++) {
-        const double v = s_tot[cand[k]];
+      // candidates in crop order (the re-scored ones carry exact = 1)
+      for (int k = 0; k < (big ? ncrops : ncand); k++) {
+        const int c = big ? k : cand[k];
+        if (big && sco[c].exact != 1) continue;
+        const double v = tot_of(c);
         if (v > best) {
           best = v;
-          top = cand[k];
+          top = c;
         }
       }
     }
+    if (big && !need_exact) sco[top].exact = 0;  // the one candidate's mark (fast score kept)
     results[D.result].top = top;
     results[D.result].n_candidates = ncand;
     results[D.result].total = best;

@@ -206,7 +206,11 @@ class Context:
                      want_images: bool = False):
         rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
         h, w = rgb.shape[:2]
-        cap = 2 * ((w + 7) // 8 + 1) * ((h + 7) // 8 + 1) + 16
+        step, nsc = 8, 2
+        if options is not None:  # crops() positions per scale x scales
+            step = max(int(options.step), 1)
+            nsc = int((options.max_scale - options.min_scale) / max(options.scale_step, 1e-9) + 1.5) + 1
+        cap = nsc * ((w + step - 1) // step + 1) * ((h + step - 1) // step + 1) + 16
         crops = (L.FiCropScore * cap)()
         n, top = ctypes.c_int32(), ctypes.c_int32()
         awh = (ctypes.c_int32 * 2)()

@@ -184,6 +184,37 @@ def test_smartcrop_reference_fixture(sctx):
     assert f"{t.width}x{t.height}" == "674x674"
 
 
+@pytest.mark.parametrize("exact_all", [True, False])
+def test_smartcrop_more_crops_than_lds_slots(ctx, exact_all):
+    """More than kScoreMaxCrops (1024) crop windows (step 1 on 240x120: 1588
+    windows over two scales): k_sc_score2 keeps totals, bounds and candidate marks in the
+    image's CropScore slots -- every crop's scores bit-exact vs the oracle
+    (exact_all), the same top crop on the bound-and-verify path."""
+    src = synth_rgb(240, 120, 0x51)
+    o = _opts(exact_all)
+    o.step = 1
+    r = ctx.smartcrop_ex(src, 100, 100, options=o)
+    ref = orc.sc_crop(src, 100, 100, step=1)
+    assert r["n"] == len(ref["crops"]) > 1024
+    for c, g in zip(r["crops"], ref["crops"]):
+        assert [c.x, c.y, c.width, c.height] == [g["x"], g["y"], g["width"], g["height"]]
+        if c.exact:
+            assert c.total.hex() == g["score"]["total"].hex()
+            assert [c.detail.hex(), c.saturation.hex(), c.skin.hex()] == \
+                [g["score"]["detail"].hex(), g["score"]["saturation"].hex(), g["score"]["skin"].hex()]
+        else:
+            assert abs(c.total - g["score"]["total"]) <= 1e-9 * max(1.0, abs(g["score"]["total"]))
+    assert all(c.exact in (0, 1) for c in r["crops"])
+    if exact_all:
+        assert all(c.exact == 1 for c in r["crops"])
+    assert r["top_index"] == ref["top_index"]
+    t = r["crops"][r["top_index"]]
+    if t.exact:
+        assert t.total.hex() == ref["top_crop"]["score"]["total"].hex()
+    else:  # a single candidate: its fast total, within its bound of the exact one
+        assert abs(t.total - ref["top_crop"]["score"]["total"]) <= 1e-9 * max(1.0, abs(t.total))
+
+
 def test_smartcrop_dropin_module(ctx):
     from flyimg_amd.smartcrop import SmartCrop
 
