@@ -161,8 +161,10 @@ struct Slot {
   size_t blob_cap = 0;
   void *res = nullptr;
   size_t res_cap = 0;
-  hipEvent_t done = nullptr;  // recorded (on sc_stream) after the batch's last readback
+  hipEvent_t done = nullptr;  // recorded (on rb_stream) after the batch's last readback
   hipEvent_t rs_done = nullptr;  // resample stage of the batch done (main stream)
+  hipEvent_t up_done = nullptr;  // the batch's sources / blob uploaded (up_stream)
+  hipEvent_t sc_end = nullptr;   // the batch's last kernel done (sc_stream)
   bool busy = false;
   // device buffers of the in-flight batch: the uploaded blob (descriptors) and
   // the workspace (intermediates, smartcrop scratch, scores, results).  Per
@@ -182,7 +184,11 @@ struct fi_ctx {
   int next_slot = 0;
   std::vector<PendingBatch> inflight;  // submission order
   hipStream_t stream = nullptr;     // upload, resample, mono
-  hipStream_t sc_stream = nullptr;  // smartcrop stage + crop apply + readback of a batch (waits for its resample)
+  hipStream_t sc_stream = nullptr;  // smartcrop stage + crop apply of a batch (waits for its resample)
+  // copies off the kernel streams: batch k+1's uploads run during batch k's
+  // kernels, batch k's readback during batch k+1's (the main stream waits for
+  // up_done, the readback for sc_end; one slot's buffers per batch)
+  hipStream_t up_stream = nullptr, rb_stream = nullptr;
   std::mutex mu;
   DevBuf arena, work, io;
   DevBuf gather;  // RCCL record gather staging
@@ -246,6 +252,8 @@ struct fi_ctx {
 static void sync_streams(fi_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->sc_stream != c->stream) (void)hipStreamSynchronize(c->sc_stream);
+  if (c->up_stream) (void)hipStreamSynchronize(c->up_stream);
+  if (c->rb_stream) (void)hipStreamSynchronize(c->rb_stream);
 }
 static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
   if (b->cap >= bytes) return FI_OK;
@@ -1844,6 +1852,9 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
 static int queue_readback(fi_ctx *c, BatchPlan &Bp, int slot, uint8_t *wb, double t_start,
                           std::shared_ptr<HostIo> host) {
   Slot &S = c->slots[slot];
+  if (!S.sc_end) HIP_TRY(hipEventCreateWithFlags(&S.sc_end, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(S.sc_end, c->sc_stream));
+  HIP_TRY(hipStreamWaitEvent(c->rb_stream, S.sc_end, 0));
   if (host) {
     // outputs to the host, behind the batch's last kernel on sc_stream: the
     // planned (pre-apply) bytes cover the applied crop, which is never larger
@@ -1853,18 +1864,18 @@ static int queue_readback(fi_ctx *c, BatchPlan &Bp, int slot, uint8_t *wb, doubl
       const size_t bytes = (size_t)d.out_stride * d.out_h;
       uint8_t *to = host->pin_off[i] < 0 ? host->user[i].dst : (uint8_t *)S.hpin + host->pin_off[i];
       HIP_TRY(hipMemcpyAsync(to, (uint8_t *)S.hio.p + host->dev_dst_off[i], bytes, hipMemcpyDeviceToHost,
-                             c->sc_stream));
+                             c->rb_stream));
     }
   }
   uint8_t *rp = (uint8_t *)S.res;
   const size_t res_bytes = sizeof(ScResult) * Bp.sitems.size();
   const size_t outwh_bytes = sizeof(int32_t) * 2 * (size_t)Bp.n;
   if (!Bp.sitems.empty())
-    HIP_TRY(hipMemcpyAsync(rp, wb + Bp.results_off, res_bytes, hipMemcpyDeviceToHost, c->sc_stream));
+    HIP_TRY(hipMemcpyAsync(rp, wb + Bp.results_off, res_bytes, hipMemcpyDeviceToHost, c->rb_stream));
   if (!Bp.apply.empty())
-    HIP_TRY(hipMemcpyAsync(rp + res_bytes, wb + Bp.outwh_off, outwh_bytes, hipMemcpyDeviceToHost, c->sc_stream));
+    HIP_TRY(hipMemcpyAsync(rp + res_bytes, wb + Bp.outwh_off, outwh_bytes, hipMemcpyDeviceToHost, c->rb_stream));
   if (!S.done) HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(S.done, c->sc_stream));
+  HIP_TRY(hipEventRecord(S.done, c->rb_stream));
   S.busy = true;
   c->next_slot = (slot + 1) % kSlots;
   PendingBatch pb;
@@ -1946,7 +1957,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async, std::shar
   rc = ensure_pinned_buf(&S.res, &S.res_cap, sizeof(ScResult) * Bp.sitems.size() + sizeof(int32_t) * 2 * (size_t)n + 64);
   if (rc) return rc;
   memcpy(S.blob, B.b.data(), B.b.size());
-  HIP_TRY(hipMemcpyAsync(S.arena.p, S.blob, B.b.size(), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(S.arena.p, S.blob, B.b.size(), hipMemcpyHostToDevice, c->up_stream));
+  if (!S.up_done) HIP_TRY(hipEventCreateWithFlags(&S.up_done, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(S.up_done, c->up_stream));
+  HIP_TRY(hipStreamWaitEvent(c->stream, S.up_done, 0));
   const double t_planned = now_ms();
   host_stat(c, "host_plan", t_planned - t_start);
   host_stat(c, "host_plan_images", t_images - t_start);
@@ -2442,6 +2456,11 @@ int fi_create(fi_ctx **out, int32_t device) {
     return set_err(FI_EDEVICE, "hipStreamCreate failed");
   }
   if (!sc_stream) c->sc_stream = c->stream;
+  if (hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking) != hipSuccess) {
+    fi_destroy(c);
+    return set_err(FI_EDEVICE, "hipStreamCreate failed");
+  }
   *out = c;
   return FI_OK;
 }
@@ -2461,12 +2480,16 @@ void fi_destroy(fi_ctx *c) {
     if (sl.hpin) (void)hipHostFree(sl.hpin);
     if (sl.done) (void)hipEventDestroy(sl.done);
     if (sl.rs_done) (void)hipEventDestroy(sl.rs_done);
+    if (sl.up_done) (void)hipEventDestroy(sl.up_done);
+    if (sl.sc_end) (void)hipEventDestroy(sl.sc_end);
     for (DevBuf *b : {&sl.arena, &sl.work, &sl.hio})
       if (b->p) (void)hipFree(b->p);
   }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   if (c->sc_stream != c->stream) (void)hipStreamDestroy(c->sc_stream);
+  if (c->up_stream) (void)hipStreamDestroy(c->up_stream);
+  if (c->rb_stream) (void)hipStreamDestroy(c->rb_stream);
   delete c;
 }
 
@@ -2645,7 +2668,7 @@ static int submit_host(fi_ctx *c, fi_image *imgs, int32_t n) {
       from_stride = (int64_t)row;
     }
     HIP_TRY(hipMemcpy2DAsync(io + soff[i], d.src_stride, from, from_stride, row, im.src_h, hipMemcpyHostToDevice,
-                             c->stream));
+                             c->up_stream));
     d.src = io + soff[i];
   }
   return run_batch(c, host->dev.data(), n, true, host);
