@@ -58,6 +58,7 @@ constexpr int kVmWaves = kVmThreads / 64;
 constexpr int kVmTiles = 512 / 16 / kVmWaves;         // 16-byte column tiles per wave
 constexpr int kVmLoads = 64 * 512 / 16 / kVmThreads;  // 16-byte loads per lane per piece
 static_assert(kVmTiles == 4 && kVmLoads == 4, "k_rs_vm lane maps assume 8 waves");
+static_assert(2 * kVmWaves == 16 && 3 * 64 + 3 <= 4 * 64, "fast8 stores: two block rows per wave, one dword per lane");
 
 __device__ __forceinline__ i32x2 vm_tr8(const uint8_t *p) {
   return __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2v *)(p));
@@ -69,8 +70,12 @@ __device__ __forceinline__ i32x4 vm_mfma(i32x4 a, i32x4 b, i32x4 c) {
 // 16-column groups, so the two 8-column groups of a transposing half-wave read
 // (columns 16 apart) land 32 banks apart
 __device__ __forceinline__ int vm_col_off(int ci) { return (ci * 16) ^ (((ci >> 4) & 1) << 7); }
-__device__ __forceinline__ uint32_t vm_q16_to_u8(uint32_t q) {  // ScaleQuantumToChar
-  return ((q + 128u) - ((q + 128u) >> 8)) >> 8;
+__device__ __forceinline__ uint32_t vm_q16_to_u8(uint32_t q) {
+  // ScaleQuantumToChar ((q + 128) - ((q + 128) >> 8)) >> 8 = (q + 128) / 257
+  // = ((q + 128) * 65281) >> 24 for every q in [0, 65535] (checked
+  // exhaustively): one 24-bit multiply-high instead of four ops
+  // (q < 2^16: the mask is free, v_add_u32_sdwa WORD_0; v_mul_hi_u32_u24)
+  return (uint32_t)(((uint64_t)((q & 0xFFFFu) + 128u) * (65281ull << 8)) >> 32);
 }
 __device__ __forceinline__ uint32_t vm_gray(uint32_t r, uint32_t g, uint32_t b) {
   // -colorspace Gray: Rec709Luma on gamma-encoded Q16, ClampToQuantum
@@ -261,21 +266,25 @@ __global__ __launch_bounds__(kVmThreads, 4) void k_rs_vm(const VDesc *__restrict
       return;
     }
     if (fast8) {
-      // items = (row, destination dword): interior dwords copied from the
-      // shifted 8-bit tile as one dword, the partial first/last dword byte by byte
-      const int ndw = (nb + 3) / 4 + 1;
-      const float inv = 1.0f / (float)ndw;
-      for (int it = tid; it < rows_here * ndw; it += kVmThreads) {
-        const int yl = (int)(((float)it + 0.5f) * inv), d = it - yl * ndw;
+      // wave w copies rows 2w and 2w + 1 (wave-uniform row address and shift),
+      // lane d the destination dword d of the row: interior dwords as one
+      // dword from the shifted 8-bit tile, the partial first/last dword byte by
+      // byte (nb + 3 <= 195 bytes: 49 dwords <= 64 lanes)
+#pragma unroll 1
+      for (int r = 0; r < 2; r++) {
+        const int yl = 2 * wv + r;
+        if (yl >= rows_here) break;
         const int sh = row_sh(16 * b + yl);
-        const int k0 = 4 * d - sh;  // segment byte of the dword's first byte
-        if (k0 >= nb) continue;
+        const int k0 = 4 * lane - sh;  // segment byte of the dword's first byte
         uint8_t *a0 = D.dst + (int64_t)(16 * b + yl) * D.dst_stride + (int64_t)S.x0 * 3;
         const uint8_t *o = otile8 + yl * kVmOtile8Pitch;
         if (k0 >= 0 && k0 + 4 <= nb) {
-          *(g_u32v *)(a0 + k0) = *reinterpret_cast<const uint32_t *>(o + 4 * d);
-        } else {
-          for (int k = max(k0, 0); k < min(k0 + 4, nb); k++) *(g_u8v *)(a0 + k) = o[sh + k];
+          *(g_u32v *)(a0 + k0) = *reinterpret_cast<const uint32_t *>(o + 4 * lane);
+        } else if (k0 < nb && k0 + 4 > 0) {
+          const uint32_t w = *reinterpret_cast<const uint32_t *>(o + 4 * lane);
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (k0 + j >= 0 && k0 + j < nb) *(g_u8v *)(a0 + k0 + j) = (uint8_t)(w >> (8 * j));
         }
       }
       return;
