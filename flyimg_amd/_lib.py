@@ -164,6 +164,7 @@ def lib():
     L.fi_rccl_gather_records.argtypes = [vp, P(FiRecord), i32, P(FiRecord)]
     L.fi_debug_monochrome.argtypes = [vp, vp, i32, i32, i32, vp, i32]
     L.fi_debug_convolve.argtypes = [vp, vp, i32, i32, i32, vp, ctypes.c_uint32, vp]
+    L.fi_debug_skinsat.argtypes = [vp, vp, vp]
     _lib = L
     return L
 

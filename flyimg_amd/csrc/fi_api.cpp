@@ -47,7 +47,9 @@ int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, 
                 const ScParamsDev &P);
 int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
                  const ScParamsDev &P);
-int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P);
+int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
+                 const uint16_t *skinsat);
+int launch_sc_skinsat(hipStream_t s, uint16_t *table, const ScParamsDev &P);
 int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, int max_px, const DevCrop *crops,
                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P);
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
@@ -213,6 +215,9 @@ struct fi_ctx {
   bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
   bool sc_vq = true;        // FI_DISABLE_SC_VQ=1: k_sc_vmaps (VALU vertical pass) instead of k_sc_vq
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
+  bool sc_skinsat = true;   // FI_DISABLE_SC_SKINSAT=1: k_sc_fz evaluates skin / saturation per pixel (f64)
+  DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
+  std::string skinsat_key;
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   std::map<const AxisTable *, HvV> hvv_cache;  // ok iff nblk > 0
@@ -909,6 +914,20 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
                       const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &PD) {
   auto desc = [&](const Launch &L) { return (const ScDesc *)(ab + L.desc_off); };
   auto pre = [&](const Launch &L) { return (const int32_t *)(ab + L.prefix_off); };
+  // the skin / saturation table of this parameter set (k_sc_fz<true>), built
+  // on the stream that reads it, so batches queued before a parameter change
+  // have read the old table first
+  const uint16_t *skinsat = nullptr;
+  if (X.nfz > 0 && c->sc_skinsat) {
+    const std::string key(reinterpret_cast<const char *>(&PD), offsetof(ScParamsDev, pad));
+    if (!c->skinsat.p || c->skinsat_key != key) {
+      const int rc = ensure(c, &c->skinsat, (size_t)2 << 24);
+      if (rc != FI_OK) return rc;
+      launch_sc_skinsat(st, (uint16_t *)c->skinsat.p, PD);
+      c->skinsat_key = key;
+    }
+    skinsat = (const uint16_t *)c->skinsat.p;
+  }
   {
     Timer t(c, "sc_prep", 0, st, st);
     if (X.red.tiles)
@@ -917,7 +936,7 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
         launch_sc_h(st, false, (const ScDesc *)(ab + X.hv_off), X.nhv, X.h_chunks, X.h_lds, ai) != 0 ||
         launch_sc_v(st, (const ScDesc *)(ab + X.prep_off), X.nprep, X.v_chunks, X.v_lds, ai, PD) != 0 ||
         launch_sc_vq(st, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0 ||
-        launch_sc_fz(st, (const ScDesc *)(ab + X.fz_off), X.nfz, X.fz_lds, ai, PD) != 0)
+        launch_sc_fz(st, (const ScDesc *)(ab + X.fz_off), X.nfz, X.fz_lds, ai, PD, skinsat) != 0)
       return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d)", X.hm_lds, X.h_lds, X.v_lds);
     if (X.hp.tiles)
       hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, st, desc(X.hp), pre(X.hp), X.hp.n, ai);
@@ -2273,6 +2292,26 @@ int fi_debug_vm_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   return vm_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
 }
+// Test hook: the skin / saturation table of k_sc_fz<true> for `params`
+int fi_debug_skinsat(fi_ctx *c, const fi_smartcrop_params *params, uint16_t *out) {
+  if (!c || !out) return set_err(FI_EINVAL, "bad arguments");
+  fi_smartcrop_params p;
+  if (params)
+    p = *params;
+  else
+    fi_smartcrop_default_params(&p);
+  HIP_TRY(hipSetDevice(c->device));
+  sync_streams(c);  // batches in flight may read the table
+  const int rc = ensure(c, &c->skinsat, (size_t)2 << 24);
+  if (rc != FI_OK) return rc;
+  const ScParamsDev PD = to_dev(p);
+  launch_sc_skinsat(c->stream, (uint16_t *)c->skinsat.p, PD);
+  c->skinsat_key.clear();  // built on c->stream, not the smartcrop stream: rebuilt before the next use
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, c->skinsat.p, (size_t)2 << 24, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return FI_OK;
+}
 // Test hook: the -monochrome kernels (fi_mono.hip) on a caller-supplied Q16
 // gray image (host buffers), so the parity tests can feed the oracle the
 // identical input; out is w x h (rot 0/180) or h x w (rot 90/270), 8-bit.
@@ -2435,6 +2474,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
   if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
+  if (const char *e = getenv("FI_DISABLE_SC_SKINSAT")) c->sc_skinsat = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_MFMA")) c->sc_mfma = !(e[0] == '1');
   // FI_SC_STREAM=1: the smartcrop stage of batch k on its own stream, beside
@@ -2471,7 +2511,7 @@ void fi_destroy(fi_ctx *c) {
   (void)drain(c);
   sync_streams(c);
   if (c->comm) ncclCommDestroy(c->comm);
-  for (DevBuf *b : {&c->arena, &c->work, &c->io, &c->gather, &c->pix})
+  for (DevBuf *b : {&c->arena, &c->work, &c->io, &c->gather, &c->pix, &c->skinsat})
     if (b->p) (void)hipFree(b->p);
   if (c->pinned) (void)hipHostFree(c->pinned);
   for (Slot &sl : c->slots) {

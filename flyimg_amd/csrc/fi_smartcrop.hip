@@ -448,8 +448,21 @@ constexpr int kFzRing = 80;  // a 64-row window at any 16-row block alignment
 #define FI_FZ_THREADS 512
 #endif
 constexpr int kFzThreads = FI_FZ_THREADS;  // 8 waves; two workgroups per CU (LDS)
+constexpr int kFzGather = 4;                // skin/saturation table reads in flight per thread
+// skin | saturation << 8 of every 24-bit colour (sc_skin_sat of the colour and
+// its luma): built once per parameter set, a gather replaces ~200 f64 VALU
+// instructions per analysed pixel in k_sc_fz<true>; bit-identical by construction.
+__global__ __launch_bounds__(256) void k_sc_skinsat(uint16_t *__restrict__ t, const ScParamsDev P) {
+  const uint32_t c = blockIdx.x * 256u + threadIdx.x;  // (r << 16) | (g << 8) | b
+  const uint32_t r = c >> 16, g = (c >> 8) & 255u, b = c & 255u;
+  const uint32_t v = sc_skin_sat(r, g, b, sc_luma(r, g, b), P);
+  t[c] = (uint16_t)((v & 255u) | ((v >> 16) << 8));
+}
+
+template <bool LUT>
 __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restrict__ descs,
-                                                        const int32_t *__restrict__ ai, const ScParamsDev P) {
+                                                        const int32_t *__restrict__ ai, const ScParamsDev P,
+                                                        const uint16_t *__restrict__ skinsat) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
   const ScDesc &D = descs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -641,18 +654,47 @@ __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restric
       }
     }
     __syncthreads();
+    // maps of the chunk's rows: detect_edge (ImagingFilter3x3 interior,
+    // border copies L), skin and saturation (LUT: kFzGather table reads in
+    // flight per thread before they are used)
+    const int nit = (y1 - y0) * aw;
+    constexpr int kG = LUT ? kFzGather : 1;
 #pragma unroll 1
-    for (int it = tid; it < (y1 - y0) * aw; it += kFzThreads) {
-      const int yr = it / aw, x = it - yr * aw, y = y0 + yr, m = y - pa;
-      const uint8_t *lrow = lum + m * lpitch;
-      const uint32_t L = lrow[x];
-      uint32_t E = L;
-      if (aw >= 3 && ah >= 3 && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
-        const int v = 4 * (int)L - (int)lrow[x - lpitch] - (int)lrow[x + lpitch] - (int)lrow[x - 1] - (int)lrow[x + 1] + 1;
-        E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
+    for (int base = tid; base < nit; base += kG * kFzThreads) {
+      uint32_t sv[kG];
+      if (LUT) {
+#pragma unroll
+        for (int u = 0; u < kG; u++) {
+          const int it = base + u * kFzThreads;
+          sv[u] = 0;
+          if (it < nit) {
+            const int yr = it / aw, x = it - yr * aw;
+            const uint8_t *qq = prer + (y0 + yr - pa) * apitch + 3 * x;
+            sv[u] = skinsat[((uint32_t)qq[0] << 16) | ((uint32_t)qq[1] << 8) | qq[2]];
+          }
+        }
       }
-      const uint8_t *qq = prer + m * apitch + 3 * x;
-      D.maps[(int64_t)y * aw + x] = sc_skin_sat(qq[0], qq[1], qq[2], L, P) | (E << 8);
+#pragma unroll
+      for (int u = 0; u < kG; u++) {
+        const int it = base + u * kFzThreads;
+        if (it >= nit) break;
+        const int yr = it / aw, x = it - yr * aw, y = y0 + yr, m = y - pa;
+        const uint8_t *lrow = lum + m * lpitch;
+        const uint32_t L = lrow[x];
+        uint32_t E = L;
+        if (aw >= 3 && ah >= 3 && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
+          const int v = 4 * (int)L - (int)lrow[x - lpitch] - (int)lrow[x + lpitch] - (int)lrow[x - 1] - (int)lrow[x + 1] + 1;
+          E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
+        }
+        uint32_t st;
+        if (LUT) {
+          st = (sv[u] & 255u) | ((sv[u] >> 8) << 16);
+        } else {
+          const uint8_t *qq = prer + m * apitch + 3 * x;
+          st = sc_skin_sat(qq[0], qq[1], qq[2], L, P);
+        }
+        D.maps[(int64_t)y * aw + x] = st | (E << 8);
+      }
     }
   }
 }
@@ -968,10 +1010,18 @@ int launch_sc_h(hipStream_t s, bool mfma, const ScDesc *descs, int n, int chunks
     hipLaunchKernelGGL(k_sc_hrows, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai);
   return 0;
 }
-int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P) {
+int launch_sc_skinsat(hipStream_t s, uint16_t *table, const ScParamsDev &P) {
+  hipLaunchKernelGGL(k_sc_skinsat, dim3(1u << 16), dim3(256), 0, s, table, P);
+  return 0;
+}
+int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
+                 const uint16_t *skinsat) {
   if (n <= 0) return 0;
   if (lds > kFzMaxLds) return -1;
-  hipLaunchKernelGGL(k_sc_fz, dim3(n), dim3(kFzThreads), lds, s, descs, ai, P);
+  if (skinsat)
+    hipLaunchKernelGGL((k_sc_fz<true>), dim3(n), dim3(kFzThreads), lds, s, descs, ai, P, skinsat);
+  else
+    hipLaunchKernelGGL((k_sc_fz<false>), dim3(n), dim3(kFzThreads), lds, s, descs, ai, P, skinsat);
   return 0;
 }
 int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,

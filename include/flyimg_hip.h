@@ -274,6 +274,11 @@ int fi_debug_convolve(fi_ctx *ctx, const uint16_t *q16, int32_t w, int32_t h, in
                       uint32_t ops, uint8_t *out);
 int fi_debug_monochrome(fi_ctx *ctx, const uint16_t *gray, int32_t w, int32_t h, int32_t rot, uint8_t *out,
                         int32_t out_stride);
+/* Test hook (not a reference interface): the skin / saturation table k_sc_fz
+ * reads (2^24 entries, index (r << 16) | (g << 8) | b, value skin | sat << 8)
+ * built for `params` (NULL: defaults) and copied to out, so a test can compare
+ * every colour with the oracle's detect_skin / detect_saturation. */
+int fi_debug_skinsat(fi_ctx *ctx, const fi_smartcrop_params *params, uint16_t *out);
 
 #ifdef __cplusplus
 }

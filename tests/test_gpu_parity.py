@@ -45,12 +45,15 @@ def _context_with(env):
 
 
 _ENV = {"FI_DISABLE_FUSED": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0",
-        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0", "FI_DISABLE_SC_FZ": "0", "FI_DISABLE_HV_RS": "0"}
+        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0", "FI_DISABLE_SC_FZ": "0", "FI_DISABLE_HV_RS": "0",
+        "FI_DISABLE_SC_SKINSAT": "0"}
 PATHS = {
     # default kernels: k_rs_vm / k_rs_hv streaming MFMA resample; k_sc_fz fused prescale + maps; k_sc_score2
     "vm": dict(_ENV),
     # the unfused MFMA prescale: k_sc_hmfma + k_sc_vq (H-stage rows through HBM)
     "nofz": dict(_ENV, FI_DISABLE_SC_FZ="1"),
+    # k_sc_fz evaluating skin / saturation per pixel in f64 instead of the colour table
+    "fzf64": dict(_ENV, FI_DISABLE_SC_SKINSAT="1"),
     # VALU fused resample (k_rs_fused); VALU vertical prescale + maps (k_sc_vmaps)
     "valu": dict(_ENV, FI_DISABLE_VM_RS="1", FI_DISABLE_HV_RS="1", FI_DISABLE_SC_VQ="1"),
     # default resample with the VALU horizontal prescale (k_sc_hrows)
@@ -69,7 +72,7 @@ def rctx(request):
     c.close()
 
 
-EXPECTED_PATH = {"vm": "path_vm", "nofz": "path_vm", "schrows": "path_vm", "valu": "path_fused",
+EXPECTED_PATH = {"vm": "path_vm", "nofz": "path_vm", "fzf64": "path_vm", "schrows": "path_vm", "valu": "path_fused",
                  "generic": "path_generic_v"}
 
 
@@ -345,7 +348,7 @@ def test_horizontal_first_within_one_lsb_of_oracle(rctx, case):
     before = {p: rctx.stats(p)[1] for p in ("path_hv", "path_generic_h")}
     outs, recs, rc = rctx.process([src], [Op(tw, th, flags, g, rot)])
     assert rc == 0 and recs[0].status == 0, L.lib().fi_last_error()
-    want = "path_hv" if hv and rctx.path_name in ("vm", "nofz", "schrows") else "path_generic_h"
+    want = "path_hv" if hv and rctx.path_name in ("vm", "nofz", "fzf64", "schrows") else "path_generic_h"
     assert rctx.stats(want)[1] == before[want] + 1, (want, {p: rctx.stats(p)[1] - before[p] for p in before})
     ref = orc.im_convert(src, tw, th, _oracle_flags(flags), gravity=g, rotate=rot)
     _cmp(outs[0], ref, name)
@@ -567,6 +570,33 @@ def test_monochrome_kernels_bit_exact(ctx, name, g, rot):
     gpu = ctx.monochrome_q16(g, rot)
     assert gpu.shape == ref.shape
     assert np.array_equal(gpu, ref), f"{name}: {(gpu != ref).sum()} of {gpu.size} pixels differ"
+
+
+@pytest.mark.parametrize("overrides", [{}, {"skin_threshold": 0.7, "saturation_threshold": 0.3,
+                                             "skin_brightness_min": 0.1, "skin_color": (0.7, 0.6, 0.4)}],
+                         ids=["defaults", "custom"])
+def test_skinsat_table_every_colour(ctx, overrides):
+    """k_sc_fz's skin / saturation table against the oracle's detect_skin /
+    detect_saturation (smartcrop.py:234-274, luma of the same colour) for all
+    2^24 colours: the gather replaces the per-pixel f64 evaluation bit for bit."""
+    import ctypes
+
+    p = L.FiSmartcropParams()
+    L.lib().fi_smartcrop_default_params(p)
+    op = orc.default_params(**overrides)
+    for k, v in overrides.items():
+        if k == "skin_color":
+            for j in range(3):
+                p.skin_color[j] = v[j]
+        else:
+            setattr(p, k, v)
+    tab = np.zeros(1 << 24, np.uint16)
+    L.check(L.lib().fi_debug_skinsat(ctx.h, ctypes.byref(p), tab.ctypes.data))
+    c = np.arange(1 << 24, dtype=np.uint32)
+    rgb = np.stack([c >> 16, (c >> 8) & 255, c & 255], axis=-1).astype(np.uint8).reshape(4096, 4096, 3)
+    _, _, skin, sat = orc.sc_maps(rgb, op)
+    assert np.array_equal(tab & 255, skin.reshape(-1)), int(((tab & 255) != skin.reshape(-1)).sum())
+    assert np.array_equal(tab >> 8, sat.reshape(-1)), int(((tab >> 8) != sat.reshape(-1)).sum())
 
 
 MONO_CASES = [
