@@ -50,6 +50,10 @@ int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds,
 int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
                  const uint16_t *skinsat);
 int launch_sc_skinsat(hipStream_t s, uint16_t *table, const ScParamsDev &P);
+int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c);
+int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *len, int n, uint8_t *const *dst,
+                      const int64_t *dst_stride, int32_t *status, void *(*alloc)(void *, int, size_t), void *actx,
+                      std::string *err);
 int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, int max_px, const DevCrop *crops,
                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P);
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
@@ -217,6 +221,7 @@ struct fi_ctx {
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   bool sc_skinsat = true;   // FI_DISABLE_SC_SKINSAT=1: k_sc_fz evaluates skin / saturation per pixel (f64)
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
+  DevBuf jpeg[3];           // GPU JPEG decode: compressed input, tables + descriptors, coefficients + planes
   std::string skinsat_key;
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
@@ -2292,6 +2297,38 @@ int fi_debug_vm_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   return vm_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
 }
+// GPU JPEG decode (fi_jpeg.hip): the decode half of the host codec pipeline
+// (ImageProcessor's `convert` reads the source with libjpeg) on the device
+int fi_jpeg_info(const uint8_t *data, size_t len, int32_t *w, int32_t *h, int32_t *channels) {
+  if (!data || !w || !h || !channels) return set_err(FI_EINVAL, "bad arguments");
+  int W = 0, H = 0, C = 0;
+  const int rc = jpeg_info(data, len, &W, &H, &C);
+  if (rc) return set_err(rc, rc == FI_EUNSUPPORTED ? "JPEG stream the GPU decoder does not handle" : "malformed JPEG");
+  *w = W;
+  *h = H;
+  *channels = C;
+  return FI_OK;
+}
+static void *jpeg_alloc(void *actx, int which, size_t bytes) {
+  fi_ctx *c = static_cast<fi_ctx *>(actx);
+  return ensure(c, &c->jpeg[which], bytes) == FI_OK ? c->jpeg[which].p : nullptr;
+}
+int fi_jpeg_decode_device(fi_ctx *c, const uint8_t *const *data, const size_t *len, int32_t n, uint8_t *const *dst,
+                          const int64_t *dst_stride, int32_t *status) {
+  if (!c || n < 0 || (n > 0 && (!data || !len || !dst || !dst_stride || !status)))
+    return set_err(FI_EINVAL, "bad arguments");
+  if (n == 0) return FI_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  std::lock_guard<std::mutex> lk(c->mu);
+  std::string err;
+  const int rc = jpeg_decode_batch(c->stream, data, len, n, dst, dst_stride, status, jpeg_alloc, c, &err);
+  if (rc) return set_err(rc, "%s", err.c_str());
+  for (int i = 0; i < n; i++)  // the others are decoded; the caller decodes these on the host
+    if (status[i])
+      return set_err(status[i], "image %d: %s", i,
+                     status[i] == FI_EUNSUPPORTED ? "JPEG stream the GPU decoder does not handle" : "malformed JPEG");
+  return FI_OK;
+}
 // Test hook: the skin / saturation table of k_sc_fz<true> for `params`
 int fi_debug_skinsat(fi_ctx *c, const fi_smartcrop_params *params, uint16_t *out) {
   if (!c || !out) return set_err(FI_EINVAL, "bad arguments");
@@ -2511,7 +2548,8 @@ void fi_destroy(fi_ctx *c) {
   (void)drain(c);
   sync_streams(c);
   if (c->comm) ncclCommDestroy(c->comm);
-  for (DevBuf *b : {&c->arena, &c->work, &c->io, &c->gather, &c->pix, &c->skinsat})
+  for (DevBuf *b : {&c->arena, &c->work, &c->io, &c->gather, &c->pix, &c->skinsat, &c->jpeg[0], &c->jpeg[1],
+                    &c->jpeg[2]})
     if (b->p) (void)hipFree(b->p);
   if (c->pinned) (void)hipHostFree(c->pinned);
   for (Slot &sl : c->slots) {

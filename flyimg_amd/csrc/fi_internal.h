@@ -302,4 +302,33 @@ struct CropScore {  // per crop (batch-global index)
   int32_t pad;
 };
 
+// ---- GPU JPEG decode (fi_jpeg.hip): baseline sequential Huffman, 8-bit, one
+// scan (gray, or YCbCr with luma sampling 1x1 / 2x1 / 2x2 and 1x1 chroma),
+// libjpeg-turbo's islow IDCT, fancy upsampling and YCbCr->RGB bit for bit.
+struct JpegHuff {        // one Huffman table (jdhuff.c canonical decoding)
+  uint16_t look[512];    // 9-bit lookahead: (length << 8) | symbol; 0 = code longer than 9 bits
+  int32_t maxcode[18];   // largest code of each length (-1: none); [17] sentinel
+  int32_t valoff[18];    // huffval index = code + valoff[length]
+  uint8_t huffval[256];
+};
+struct JpegDesc {        // one image of a decode batch
+  const uint8_t *ecs;    // entropy-coded segment (device)
+  int32_t ecs_len;
+  int32_t W, H, ncomp;
+  int32_t hmax, vmax, mcux, mcuy;  // MCUs per row / per column
+  int32_t h[3], v[3];              // sampling factors
+  int32_t tq[3], td[3], ta[3];     // quant / DC / AC table of each component
+  int32_t bw[3], bh[3];            // component block grid (whole MCUs)
+  int32_t dw[3], dh[3];            // downsampled width / height (jdmaster.c)
+  int64_t coef[3];                 // byte offsets in the work buffer: int16 blocks [bh][bw][64], natural order
+  int64_t plane[3];                // u8 samples [bh * 8][bw * 8]
+  int32_t qt;                      // index of the image's 4 quant tables (u16 [4][64], natural order)
+  int32_t ht[4];                   // its Huffman tables DC0, DC1, AC0, AC1 (batch table index, -1: none)
+  uint8_t *dst;                    // HWC: 3 channels (YCbCr sources) or 1 (gray)
+  int64_t dst_stride;
+};
+struct JpegInterval {    // one restart interval: its MCUs and where its bits start
+  int32_t img, mcu0, mcu1, byte0;
+};
+
 }  // namespace fi

@@ -1,0 +1,719 @@
+// fi_jpeg.hip -- baseline JPEG decode on the GPU, bit-exact with the
+// libjpeg-turbo decoder the host codec path uses (Pillow 12.2.0 bundles
+// libjpeg-turbo 3.x; SURVEY.md 8(f) 1: "nvJPEG-style batched decode").
+//
+//   host     marker parse (SOF0/SOF1 8-bit, DQT, DHT, DRI, one SOS), canonical
+//            Huffman tables deduplicated over the batch, restart intervals
+//            located by their RSTn markers;
+//   k_jpeg_huff   one thread per restart interval (the whole scan when there
+//            is none): jdhuff.c's sequential decode -- DC prediction, AC run /
+//            size symbols, HUFF_EXTEND -- into int16 coefficient blocks in
+//            natural order; byte stuffing and markers as jdhuff.c (a marker
+//            feeds zero bits);
+//   k_jpeg_idct   one thread per 8x8 block: jidctint.c jpeg_idct_islow
+//            (dequantise, 13-bit constants, PASS1_BITS 2, range limit);
+//   k_jpeg_color  one thread per output pixel: jdsample.c fancy upsampling
+//            (h2v1 / h2v2 triangle filters, edge replication) and jdcolor.c
+//            ycc_rgb_convert with its 16-bit fixed-point tables.
+//
+// Unsupported streams (progressive, arithmetic, 12-bit, CMYK / Adobe
+// transforms, other samplings, several scans) return FI_EUNSUPPORTED from
+// jpeg_parse so the caller decodes them on the host.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "fi_internal.h"
+
+namespace fi {
+
+__constant__ uint8_t c_natural[64 + 16] = {  // jpeg_natural_order (+16 guard entries)
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13,
+    6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31,
+    39, 46, 53, 60, 61, 54, 47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+// ---------------------------------------------------------------------------
+// host: headers
+// ---------------------------------------------------------------------------
+struct JpegHdr {
+  int W = 0, H = 0, ncomp = 0, restart = 0;
+  int id[3] = {}, h[3] = {}, v[3] = {}, tq[3] = {}, td[3] = {}, ta[3] = {};
+  uint16_t qt[4][64] = {};  // natural order
+  bool qt_ok[4] = {};
+  std::string dht[4];       // DC0, DC1, AC0, AC1: bits[16] + huffval
+  size_t ecs0 = 0, ecs1 = 0;  // entropy-coded segment [ecs0, ecs1)
+};
+
+static int be16(const uint8_t *p) { return (p[0] << 8) | p[1]; }
+
+// 0 = OK; FI_EUNSUPPORTED for streams the GPU decoder does not handle;
+// FI_EINVAL for malformed data
+int jpeg_parse(const uint8_t *d, size_t n, JpegHdr *o) {
+  if (!d || n < 4 || d[0] != 0xFF || d[1] != 0xD8) return FI_EINVAL;
+  static const uint8_t zz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+  size_t p = 2;
+  bool sof = false;
+  while (p + 4 <= n) {
+    if (d[p] != 0xFF) return FI_EINVAL;
+    const int m = d[p + 1];
+    if (m == 0xFF) {  // fill byte
+      p++;
+      continue;
+    }
+    if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) {
+      p += 2;
+      continue;
+    }
+    const size_t L = (size_t)be16(d + p + 2);
+    if (L < 2 || p + 2 + L > n) return FI_EINVAL;
+    const uint8_t *s = d + p + 4, *e = d + p + 2 + L;
+    switch (m) {
+      case 0xC0:
+      case 0xC1: {  // baseline / extended sequential, Huffman
+        if (sof || L < 8 || s[0] != 8) return FI_EUNSUPPORTED;
+        sof = true;
+        o->H = be16(s + 1);
+        o->W = be16(s + 3);
+        o->ncomp = s[5];
+        if (o->W <= 0 || o->H <= 0) return FI_EUNSUPPORTED;  // DNL-defined height
+        if (o->ncomp != 1 && o->ncomp != 3) return FI_EUNSUPPORTED;
+        if (L != 8 + 3 * (size_t)o->ncomp) return FI_EINVAL;
+        for (int c = 0; c < o->ncomp; c++) {
+          o->id[c] = s[6 + 3 * c];
+          o->h[c] = s[7 + 3 * c] >> 4;
+          o->v[c] = s[7 + 3 * c] & 15;
+          o->tq[c] = s[8 + 3 * c];
+          if (o->tq[c] > 3 || o->h[c] < 1 || o->v[c] < 1) return FI_EINVAL;
+        }
+        break;
+      }
+      case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA: case 0xCB:
+      case 0xCD: case 0xCE: case 0xCF:
+        return FI_EUNSUPPORTED;  // progressive, lossless, hierarchical, arithmetic
+      case 0xDB: {  // DQT
+        for (const uint8_t *q = s; q < e;) {
+          const int pq = q[0] >> 4, tq = q[0] & 15;
+          if (tq > 3 || pq > 1 || q + 1 + 64 * (pq + 1) > e) return FI_EINVAL;
+          for (int k = 0; k < 64; k++)
+            o->qt[tq][zz[k]] = (uint16_t)(pq ? be16(q + 1 + 2 * k) : q[1 + k]);
+          o->qt_ok[tq] = true;
+          q += 1 + 64 * (pq + 1);
+        }
+        break;
+      }
+      case 0xC4: {  // DHT
+        for (const uint8_t *q = s; q < e;) {
+          if (q + 17 > e) return FI_EINVAL;
+          const int tc = q[0] >> 4, th = q[0] & 15;
+          if (tc > 1 || th > 1) return FI_EUNSUPPORTED;  // baseline: two tables per class
+          int cnt = 0;
+          for (int l = 0; l < 16; l++) cnt += q[1 + l];
+          if (cnt > 256 || q + 17 + cnt > e) return FI_EINVAL;
+          o->dht[2 * tc + th].assign((const char *)q + 1, 16 + cnt);
+          q += 17 + cnt;
+        }
+        break;
+      }
+      case 0xDD:  // DRI
+        if (L != 4) return FI_EINVAL;
+        o->restart = be16(s);
+        break;
+      case 0xDA: {  // SOS: the one scan, then the entropy-coded data up to EOI
+        if (!sof) return FI_EINVAL;
+        const int ns = s[0];
+        if (ns != o->ncomp || L != 6 + 2 * (size_t)ns) return FI_EUNSUPPORTED;  // one interleaved scan
+        for (int k = 0; k < ns; k++) {
+          const int cs = s[1 + 2 * k];
+          if (cs != o->id[k]) return FI_EUNSUPPORTED;
+          o->td[k] = s[2 + 2 * k] >> 4;
+          o->ta[k] = s[2 + 2 * k] & 15;
+          if (o->td[k] > 1 || o->ta[k] > 1) return FI_EUNSUPPORTED;
+        }
+        const uint8_t *t = s + 1 + 2 * ns;
+        if (t[0] != 0 || t[1] != 63 || t[2] != 0) return FI_EUNSUPPORTED;
+        o->ecs0 = (size_t)(e - d);
+        // end of the scan: the first marker other than RSTn (stuffed 0xFF00 and fill bytes skipped)
+        size_t q = o->ecs0;
+        for (;;) {
+          const void *f = memchr(d + q, 0xFF, n - q);
+          if (!f) {
+            q = n;
+            break;
+          }
+          q = (size_t)((const uint8_t *)f - d);
+          if (q + 1 >= n) {
+            q = n;
+            break;
+          }
+          const int b = d[q + 1];
+          if (b == 0x00 || b == 0xFF || (b >= 0xD0 && b <= 0xD7)) {
+            q += b == 0xFF ? 1 : 2;
+            continue;
+          }
+          break;
+        }
+        o->ecs1 = q;
+        for (int c = 0; c < o->ncomp; c++) {
+          if (!o->qt_ok[o->tq[c]] || o->dht[o->td[c]].empty() || o->dht[2 + o->ta[c]].empty()) return FI_EINVAL;
+        }
+        if (o->ncomp == 1) {
+          o->h[0] = o->v[0] = 1;  // non-interleaved scan: one block per MCU
+        } else {
+          // YCbCr with luma 1x1 / 2x1 / 2x2 over 1x1 chroma (jdsample.c fullsize / h2v1 / h2v2)
+          if (o->h[1] != 1 || o->v[1] != 1 || o->h[2] != 1 || o->v[2] != 1) return FI_EUNSUPPORTED;
+          const int hv = o->h[0] * 10 + o->v[0];
+          if (hv != 11 && hv != 21 && hv != 22) return FI_EUNSUPPORTED;
+        }
+        return 0;
+      }
+      case 0xEE:  // APP14 "Adobe": a transform flag other than YCbCr is unsupported
+        if (L >= 14 && memcmp(s, "Adobe", 5) == 0 && o->ncomp == 3 && s[11] != 1) return FI_EUNSUPPORTED;
+        break;
+      default:
+        break;  // APPn, COM, ...
+    }
+    p += 2 + L;
+  }
+  return FI_EINVAL;
+}
+
+// jdhuff.c jpeg_make_d_derived_tbl: canonical codes, maxcode / valoffset,
+// 9-bit lookahead
+static bool jpeg_build_huff(const std::string &dht, JpegHuff *t) {
+  memset(t, 0, sizeof(*t));
+  const uint8_t *bits = (const uint8_t *)dht.data();
+  const int nv = (int)dht.size() - 16;
+  memcpy(t->huffval, bits + 16, nv);
+  int p = 0;
+  uint32_t code = 0;
+  for (int l = 1; l <= 16; l++) {
+    if (bits[l - 1]) {
+      t->valoff[l] = p - (int)code;
+      for (int i = 0; i < bits[l - 1]; i++, p++, code++) {
+        if (l <= 9) {
+          const uint32_t lo = code << (9 - l), cnt = 1u << (9 - l);
+          for (uint32_t k = 0; k < cnt; k++) t->look[lo + k] = (uint16_t)((l << 8) | t->huffval[p]);
+        }
+      }
+      t->maxcode[l] = (int32_t)code - 1;
+      if (code > (1u << l)) return false;  // over-subscribed
+    } else {
+      t->maxcode[l] = -1;
+    }
+    code <<= 1;
+  }
+  t->maxcode[17] = 0x7FFFFFFF;
+  return p == nv;
+}
+
+// ---------------------------------------------------------------------------
+// device: Huffman decode
+// ---------------------------------------------------------------------------
+constexpr int kJpegLanes = 16;   // intervals per 64-lane workgroup (one per lane < kJpegLanes)
+constexpr int kJpegLdsTabs = 8;  // distinct Huffman tables staged in LDS (more: read from global)
+
+struct BitReader {
+  const uint8_t *p;  // 16-byte aligned base of the window
+  uint4 c0, c1;      // bytes [base, base + 32)
+  int base, pos, end;
+  uint64_t buf;
+  int nbits;
+  bool marker;
+  __device__ __forceinline__ uint32_t byte_at(int q) const {
+    const int o = q - base;  // 0 .. 31
+    const uint4 &c = o < 16 ? c0 : c1;
+    const int w = (o >> 2) & 3;
+    const uint32_t d = w == 0 ? c.x : w == 1 ? c.y : w == 2 ? c.z : c.w;
+    return (d >> (8 * (o & 3))) & 255u;
+  }
+  __device__ __forceinline__ void advance_window() {
+    while (pos - base >= 16) {  // keep [pos, pos + 1] inside the window
+      c0 = c1;
+      base += 16;
+      c1 = *reinterpret_cast<const uint4 *>(p + base + 16);
+    }
+  }
+  __device__ void init(const uint8_t *ecs, int byte0, int len) {
+    p = ecs;
+    base = byte0 & ~15;
+    c0 = *reinterpret_cast<const uint4 *>(p + base);
+    c1 = *reinterpret_cast<const uint4 *>(p + base + 16);
+    pos = byte0;
+    end = len;
+    buf = 0;
+    nbits = 0;
+    marker = false;
+  }
+  // jdhuff.c jpeg_fill_bit_buffer: stuffed 0xFF00 -> 0xFF; at a marker (or the
+  // end of the data) zero bits are supplied
+  __device__ __forceinline__ void fill() {
+    while (nbits <= 56) {
+      uint32_t b = 0;
+      if (!marker && pos < end) {
+        advance_window();
+        b = byte_at(pos);
+        if (b == 0xFFu) {
+          if (byte_at(pos + 1) == 0u) {
+            pos += 2;
+          } else {
+            marker = true;
+            b = 0;
+          }
+        } else {
+          pos++;
+        }
+      }
+      buf = (buf << 8) | b;
+      nbits += 8;
+    }
+  }
+  __device__ __forceinline__ uint32_t peek(int n) const { return (uint32_t)(buf >> (nbits - n)) & ((1u << n) - 1u); }
+  __device__ __forceinline__ void skip(int n) { nbits -= n; }
+};
+
+__device__ __forceinline__ int jpeg_decode_sym(BitReader &br, const JpegHuff *t) {
+  br.fill();
+  const uint32_t lk = t->look[br.peek(9)];
+  if (lk) {
+    br.skip(lk >> 8);
+    return lk & 255;
+  }
+  int l = 10;
+  int32_t code = (int32_t)br.peek(10);
+  while (l <= 16 && code > t->maxcode[l]) {
+    l++;
+    code = (int32_t)br.peek(l);
+  }
+  if (l > 16) {  // corrupt data: jdhuff.c warns and returns 0
+    br.skip(0);
+    return 0;
+  }
+  br.skip(l);
+  return t->huffval[(code + t->valoff[l]) & 255];
+}
+__device__ __forceinline__ int jpeg_extend(uint32_t r, int s) {  // HUFF_EXTEND
+  return r < (1u << (s - 1)) ? (int)r - (1 << s) + 1 : (int)r;
+}
+
+__global__ __launch_bounds__(64) void k_jpeg_huff(const JpegDesc *__restrict__ descs,
+                                                  const JpegInterval *__restrict__ ivs, int niv,
+                                                  const JpegHuff *__restrict__ huff, int nhuff,
+                                                  uint8_t *__restrict__ work) {
+  __shared__ JpegHuff sh[kJpegLdsTabs];
+  __shared__ int16_t blk[kJpegLanes][64];
+  const int tid = threadIdx.x;
+  const bool lds_tabs = nhuff <= kJpegLdsTabs;
+  if (lds_tabs) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(huff);
+    uint32_t *dstw = reinterpret_cast<uint32_t *>(sh);
+    const int nw = nhuff * (int)sizeof(JpegHuff) / 4;
+    for (int i = tid; i < nw; i += 64) dstw[i] = src[i];
+  }
+  for (int i = tid; i < kJpegLanes * 64 / 2; i += 64) reinterpret_cast<uint32_t *>(blk)[i] = 0;
+  __syncthreads();
+  const int iv = blockIdx.x * kJpegLanes + tid;
+  if (tid >= kJpegLanes || iv >= niv) return;
+  const JpegInterval I = ivs[iv];
+  const JpegDesc &D = descs[I.img];
+  const JpegHuff *tabs = lds_tabs ? sh : huff;
+  BitReader br;
+  br.init(D.ecs, I.byte0, D.ecs_len);
+  int pred[3] = {0, 0, 0};
+  int16_t *b = blk[tid];
+  for (int mcu = I.mcu0; mcu < I.mcu1; mcu++) {
+    const int my = mcu / D.mcux, mx = mcu - my * D.mcux;
+    for (int c = 0; c < D.ncomp; c++) {
+      const JpegHuff *dc = tabs + D.ht[D.td[c]], *ac = tabs + D.ht[2 + D.ta[c]];
+      for (int by = 0; by < D.v[c]; by++)
+        for (int bx = 0; bx < D.h[c]; bx++) {
+          // DC: difference from the component's previous block
+          int s = jpeg_decode_sym(br, dc);
+          if (s) {
+            br.fill();
+            const uint32_t r = br.peek(s);
+            br.skip(s);
+            s = jpeg_extend(r, s);
+          }
+          pred[c] += s;
+          b[0] = (int16_t)pred[c];
+          // AC: run / size symbols
+          for (int k = 1; k < 64; k++) {
+            const int rs = jpeg_decode_sym(br, ac);
+            const int r = rs >> 4, sz = rs & 15;
+            if (sz) {
+              k += r;
+              br.fill();
+              const uint32_t v = br.peek(sz);
+              br.skip(sz);
+              b[c_natural[k < 79 ? k : 79]] = (int16_t)jpeg_extend(v, sz);
+            } else {
+              if (r != 15) break;
+              k += 15;
+            }
+          }
+          // block -> work, and clear the staging block
+          const int row = my * D.v[c] + by, col = mx * D.h[c] + bx;
+          uint4 *o = reinterpret_cast<uint4 *>(work + D.coef[c] + ((int64_t)row * D.bw[c] + col) * 128);
+          uint4 *bb = reinterpret_cast<uint4 *>(b);
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            o[q] = bb[q];
+            bb[q] = uint4{0, 0, 0, 0};
+          }
+        }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// device: islow IDCT (jidctint.c), one thread per block
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint8_t jpeg_range_limit(int x) {  // IDCT_range_limit[x & RANGE_MASK]
+  const int m = x & 1023;
+  const int v = (m >= 512 ? m - 1024 : m) + 128;
+  return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+}
+
+struct JpegBlockRef {  // one block of the batch: image, component, block index
+  int32_t img, comp, blk;
+};
+
+__global__ __launch_bounds__(256) void k_jpeg_idct(const JpegDesc *__restrict__ descs,
+                                                   const JpegBlockRef *__restrict__ refs, int nref,
+                                                   const uint16_t *__restrict__ qts, uint8_t *__restrict__ work) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nref) return;
+  const JpegBlockRef R = refs[i];
+  const JpegDesc &D = descs[R.img];
+  const int c = R.comp;
+  const int by = R.blk / D.bw[c], bx = R.blk - by * D.bw[c];
+  const int16_t *in = reinterpret_cast<const int16_t *>(work + D.coef[c] + (int64_t)R.blk * 128);
+  const uint16_t *q = qts + (int64_t)(D.qt + D.tq[c]) * 64;
+  constexpr int CB = 13, P1 = 2;
+  constexpr int F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373, F1175 = 9633, F1501 = 12299,
+                F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
+  int ws[64];
+  int cf[64];
+#pragma unroll
+  for (int k = 0; k < 64; k++) cf[k] = (int)in[k] * (int)q[k];
+  // pass 1: columns
+#pragma unroll
+  for (int x = 0; x < 8; x++) {
+    int z2 = cf[16 + x], z3 = cf[48 + x];
+    int z1 = (z2 + z3) * F0541;
+    int tmp2 = z1 + z3 * (-F1847);
+    int tmp3 = z1 + z2 * F0765;
+    z2 = cf[x];
+    z3 = cf[32 + x];
+    int tmp0 = (z2 + z3) * (1 << CB);
+    int tmp1 = (z2 - z3) * (1 << CB);
+    const int tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    tmp0 = cf[56 + x];
+    tmp1 = cf[40 + x];
+    tmp2 = cf[24 + x];
+    tmp3 = cf[8 + x];
+    z1 = tmp0 + tmp3;
+    z2 = tmp1 + tmp2;
+    z3 = tmp0 + tmp2;
+    int z4 = tmp1 + tmp3;
+    const int z5 = (z3 + z4) * F1175;
+    tmp0 *= F0298;
+    tmp1 *= F2053;
+    tmp2 *= F3072;
+    tmp3 *= F1501;
+    z1 *= -F0899;
+    z2 *= -F2562;
+    z3 *= -F1961;
+    z4 *= -F0390;
+    z3 += z5;
+    z4 += z5;
+    tmp0 += z1 + z3;
+    tmp1 += z2 + z4;
+    tmp2 += z2 + z3;
+    tmp3 += z1 + z4;
+    constexpr int S = CB - P1, R1 = 1 << (S - 1);
+    ws[x] = (tmp10 + tmp3 + R1) >> S;
+    ws[56 + x] = (tmp10 - tmp3 + R1) >> S;
+    ws[8 + x] = (tmp11 + tmp2 + R1) >> S;
+    ws[48 + x] = (tmp11 - tmp2 + R1) >> S;
+    ws[16 + x] = (tmp12 + tmp1 + R1) >> S;
+    ws[40 + x] = (tmp12 - tmp1 + R1) >> S;
+    ws[24 + x] = (tmp13 + tmp0 + R1) >> S;
+    ws[32 + x] = (tmp13 - tmp0 + R1) >> S;
+  }
+  // pass 2: rows -> samples
+  uint8_t *out = work + D.plane[c] + (int64_t)(by * 8) * (D.bw[c] * 8) + bx * 8;
+  const int pitch = D.bw[c] * 8;
+#pragma unroll
+  for (int y = 0; y < 8; y++) {
+    const int *w = ws + 8 * y;
+    int z2 = w[2], z3 = w[6];
+    int z1 = (z2 + z3) * F0541;
+    int tmp2 = z1 + z3 * (-F1847);
+    int tmp3 = z1 + z2 * F0765;
+    int tmp0 = (w[0] + w[4]) * (1 << CB);
+    int tmp1 = (w[0] - w[4]) * (1 << CB);
+    const int tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    tmp0 = w[7];
+    tmp1 = w[5];
+    tmp2 = w[3];
+    tmp3 = w[1];
+    z1 = tmp0 + tmp3;
+    z2 = tmp1 + tmp2;
+    z3 = tmp0 + tmp2;
+    int z4 = tmp1 + tmp3;
+    const int z5 = (z3 + z4) * F1175;
+    tmp0 *= F0298;
+    tmp1 *= F2053;
+    tmp2 *= F3072;
+    tmp3 *= F1501;
+    z1 *= -F0899;
+    z2 *= -F2562;
+    z3 *= -F1961;
+    z4 *= -F0390;
+    z3 += z5;
+    z4 += z5;
+    tmp0 += z1 + z3;
+    tmp1 += z2 + z4;
+    tmp2 += z2 + z3;
+    tmp3 += z1 + z4;
+    constexpr int S = CB + P1 + 3, R2 = 1 << (S - 1);
+    uint32_t lo = 0, hi = 0;
+    lo |= (uint32_t)jpeg_range_limit((tmp10 + tmp3 + R2) >> S);
+    lo |= (uint32_t)jpeg_range_limit((tmp11 + tmp2 + R2) >> S) << 8;
+    lo |= (uint32_t)jpeg_range_limit((tmp12 + tmp1 + R2) >> S) << 16;
+    lo |= (uint32_t)jpeg_range_limit((tmp13 + tmp0 + R2) >> S) << 24;
+    hi |= (uint32_t)jpeg_range_limit((tmp13 - tmp0 + R2) >> S);
+    hi |= (uint32_t)jpeg_range_limit((tmp12 - tmp1 + R2) >> S) << 8;
+    hi |= (uint32_t)jpeg_range_limit((tmp11 - tmp2 + R2) >> S) << 16;
+    hi |= (uint32_t)jpeg_range_limit((tmp10 - tmp3 + R2) >> S) << 24;
+    *reinterpret_cast<uint2 *>(out + (int64_t)y * pitch) = uint2{lo, hi};
+  }
+}
+
+// ---------------------------------------------------------------------------
+// device: fancy upsampling + YCbCr -> RGB (jdsample.c, jdcolor.c)
+// ---------------------------------------------------------------------------
+// chroma sample of output pixel (x, y) for luma sampling (hs, vs) over 1x1 chroma
+__device__ __forceinline__ int jpeg_up(const uint8_t *pl, int pitch, int dw, int dh, int hs, int vs, int x, int y) {
+  if (hs == 1 && vs == 1) return pl[(int64_t)y * pitch + x];
+  const int cx = x >> 1;
+  const int cl = cx > 0 ? cx - 1 : 0, cr = cx < dw - 1 ? cx + 1 : dw - 1;
+  const bool odd = x & 1;
+  if (vs == 1) {  // h2v1_fancy_upsample
+    const uint8_t *r = pl + (int64_t)y * pitch;
+    return odd ? (3 * r[cx] + r[cr] + 2) >> 2 : (3 * r[cx] + r[cl] + 1) >> 2;
+  }
+  // h2v2_fancy_upsample: column sums 3 * nearer row + further row (edge rows replicated)
+  const int cy = y >> 1;
+  const int fy = (y & 1) ? (cy < dh - 1 ? cy + 1 : dh - 1) : (cy > 0 ? cy - 1 : 0);
+  const uint8_t *r0 = pl + (int64_t)cy * pitch, *r1 = pl + (int64_t)fy * pitch;
+  const int t = 3 * r0[cx] + r1[cx];
+  if (odd) return (3 * t + 3 * r0[cr] + r1[cr] + 7) >> 4;
+  return (3 * t + 3 * r0[cl] + r1[cl] + 8) >> 4;
+}
+__device__ __forceinline__ uint8_t jpeg_clamp(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+__global__ __launch_bounds__(256) void k_jpeg_color(const JpegDesc *__restrict__ descs, const int64_t *__restrict__ px0,
+                                                    int nimg, const uint8_t *__restrict__ work) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // image of pixel i: binary search over the per-image pixel prefix
+  int lo = 0, hi = nimg;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (px0[mid] <= i)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  if (i >= px0[nimg]) return;
+  const JpegDesc &D = descs[lo];
+  const int64_t k = i - px0[lo];
+  const int y = (int)(k / D.W), x = (int)(k - (int64_t)y * D.W);
+  const int yp = D.bw[0] * 8;
+  const uint8_t Y = work[D.plane[0] + (int64_t)y * yp + x];
+  if (D.ncomp == 1) {
+    D.dst[(int64_t)y * D.dst_stride + x] = Y;
+    return;
+  }
+  const int hs = D.h[0], vs = D.v[0];
+  const int cb = jpeg_up(work + D.plane[1], D.bw[1] * 8, D.dw[1], D.dh[1], hs, vs, x, y);
+  const int cr = jpeg_up(work + D.plane[2], D.bw[2] * 8, D.dw[2], D.dh[2], hs, vs, x, y);
+  // build_ycc_rgb_table: FIX(x) = (int)(x * 65536 + 0.5), ONE_HALF = 1 << 15
+  const int xr = cr - 128, xb = cb - 128;
+  const int r = Y + ((91881 * xr + 32768) >> 16);
+  const int g = Y + ((-22554 * xb + 32768 + -46802 * xr) >> 16);
+  const int b = Y + ((116130 * xb + 32768) >> 16);
+  uint8_t *o = D.dst + (int64_t)y * D.dst_stride + 3 * x;
+  o[0] = jpeg_clamp(r);
+  o[1] = jpeg_clamp(g);
+  o[2] = jpeg_clamp(b);
+}
+
+// ---------------------------------------------------------------------------
+// host: batch plan + launches
+// ---------------------------------------------------------------------------
+int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c) {
+  JpegHdr hd;
+  const int rc = jpeg_parse(data, len, &hd);
+  if (rc) return rc;
+  *w = hd.W;
+  *h = hd.H;
+  *c = hd.ncomp == 1 ? 1 : 3;
+  return 0;
+}
+
+// Plans and runs one decode batch.  `alloc(which, bytes)` returns device
+// memory (0: compressed input, 1: tables/descriptors, 2: work) that stays
+// valid until the stream has run; `stage` is a pinned host buffer provider.
+int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *len, int n, uint8_t *const *dst,
+                      const int64_t *dst_stride, int32_t *status, void *(*alloc)(void *, int, size_t), void *actx,
+                      std::string *err) {
+  std::vector<JpegHdr> hd(n);
+  std::vector<int> ok(n, 0);
+  std::map<std::string, int> huff_ix;
+  std::vector<JpegHuff> huffs;
+  std::vector<uint16_t> qts;
+  std::vector<JpegDesc> descs;
+  std::vector<int> desc_img;
+  std::vector<JpegInterval> ivs;
+  std::vector<JpegBlockRef> refs;
+  std::vector<int64_t> px0(1, 0);
+  size_t ecs_total = 0, work_total = 0;
+  for (int i = 0; i < n; i++) {
+    status[i] = jpeg_parse(data[i], len[i], &hd[i]);
+    if (status[i]) continue;
+    JpegHdr &H = hd[i];
+    JpegDesc D{};
+    D.W = H.W;
+    D.H = H.H;
+    D.ncomp = H.ncomp;
+    D.hmax = D.vmax = 1;
+    for (int c = 0; c < H.ncomp; c++) {
+      D.hmax = std::max(D.hmax, H.h[c]);
+      D.vmax = std::max(D.vmax, H.v[c]);
+    }
+    D.mcux = (H.W + 8 * D.hmax - 1) / (8 * D.hmax);
+    D.mcuy = (H.H + 8 * D.vmax - 1) / (8 * D.vmax);
+    D.qt = (int)(qts.size() / 64);
+    for (int t = 0; t < 4; t++) qts.insert(qts.end(), H.qt[t], H.qt[t] + 64);
+    // the image's four table slots, deduplicated over the batch (an encoder's
+    // tables are shared by all its images: a few distinct tables, LDS resident)
+    for (int t = 0; t < 4; t++) {
+      D.ht[t] = -1;
+      if (H.dht[t].empty()) continue;
+      auto it = huff_ix.find(H.dht[t]);
+      if (it == huff_ix.end()) {
+        JpegHuff hf;
+        if (!jpeg_build_huff(H.dht[t], &hf)) {
+          status[i] = FI_EINVAL;
+          break;
+        }
+        it = huff_ix.emplace(H.dht[t], (int)huffs.size()).first;
+        huffs.push_back(hf);
+      }
+      D.ht[t] = it->second;
+    }
+    if (status[i]) continue;
+    for (int c = 0; c < H.ncomp; c++) {
+      D.h[c] = H.h[c];
+      D.v[c] = H.v[c];
+      D.tq[c] = H.tq[c];
+      D.td[c] = H.td[c];
+      D.ta[c] = H.ta[c];
+      D.bw[c] = D.mcux * H.h[c];
+      D.bh[c] = D.mcuy * H.v[c];
+      D.dw[c] = (H.W * H.h[c] + D.hmax - 1) / D.hmax;  // jdmaster.c downsampled_width
+      D.dh[c] = (H.H * H.v[c] + D.vmax - 1) / D.vmax;
+      D.coef[c] = (int64_t)work_total;
+      work_total += (size_t)D.bw[c] * D.bh[c] * 128;
+      D.plane[c] = (int64_t)work_total;
+      work_total += ((size_t)D.bw[c] * 8 * D.bh[c] * 8 + 255) & ~(size_t)255;
+    }
+    D.ecs_len = (int32_t)(H.ecs1 - H.ecs0);
+    D.ecs = reinterpret_cast<const uint8_t *>(ecs_total);  // offset until placed
+    D.dst = dst[i];
+    D.dst_stride = dst_stride[i];
+    const int img = (int)descs.size();
+    // restart intervals: RSTn markers split the segment
+    const int nmcu = D.mcux * D.mcuy;
+    if (H.restart > 0) {
+      const uint8_t *e = data[i] + H.ecs0;
+      int byte0 = 0, mcu0 = 0;
+      for (size_t q = 0; q + 1 < (size_t)D.ecs_len && mcu0 < nmcu; q++) {
+        if (e[q] == 0xFF && e[q + 1] >= 0xD0 && e[q + 1] <= 0xD7) {
+          ivs.push_back({img, mcu0, std::min(mcu0 + H.restart, nmcu), byte0});
+          mcu0 += H.restart;
+          byte0 = (int)q + 2;
+          q++;
+        }
+      }
+      if (mcu0 < nmcu) ivs.push_back({img, mcu0, nmcu, byte0});
+    } else {
+      ivs.push_back({img, 0, nmcu, 0});
+    }
+    for (int c = 0; c < H.ncomp; c++)
+      for (int b = 0; b < D.bw[c] * D.bh[c]; b++) refs.push_back({img, c, b});
+    px0.push_back(px0.back() + (int64_t)H.W * H.H);
+    ecs_total += ((size_t)D.ecs_len + 32 + 15) & ~(size_t)15;  // zero pad: the reader's window
+    descs.push_back(D);
+    desc_img.push_back(i);
+  }
+  if (descs.empty()) return 0;
+  // device buffers: compressed data, tables + descriptors, work
+  uint8_t *din = (uint8_t *)alloc(actx, 0, ecs_total);
+  const size_t o_desc = 0, o_iv = o_desc + ((descs.size() * sizeof(JpegDesc) + 255) & ~(size_t)255);
+  const size_t o_ref = o_iv + ((ivs.size() * sizeof(JpegInterval) + 255) & ~(size_t)255);
+  const size_t o_huff = o_ref + ((refs.size() * sizeof(JpegBlockRef) + 255) & ~(size_t)255);
+  const size_t o_qt = o_huff + ((huffs.size() * sizeof(JpegHuff) + 255) & ~(size_t)255);
+  const size_t o_px = o_qt + ((qts.size() * 2 + 255) & ~(size_t)255);
+  const size_t tab_total = o_px + px0.size() * 8;
+  uint8_t *dtab = (uint8_t *)alloc(actx, 1, tab_total);
+  uint8_t *dwork = (uint8_t *)alloc(actx, 2, std::max(work_total, (size_t)256));
+  if (!din || !dtab || !dwork) {
+    *err = "device memory for the JPEG batch";
+    return FI_ENOMEM;
+  }
+  std::vector<uint8_t> hin(ecs_total, 0), htab(tab_total, 0);
+  for (size_t k = 0; k < descs.size(); k++) {
+    JpegDesc &D = descs[k];
+    const size_t off = (size_t)reinterpret_cast<uintptr_t>(D.ecs);
+    memcpy(hin.data() + off, data[desc_img[k]] + hd[desc_img[k]].ecs0, D.ecs_len);
+    D.ecs = din + off;
+  }
+  memcpy(htab.data() + o_desc, descs.data(), descs.size() * sizeof(JpegDesc));
+  memcpy(htab.data() + o_iv, ivs.data(), ivs.size() * sizeof(JpegInterval));
+  memcpy(htab.data() + o_ref, refs.data(), refs.size() * sizeof(JpegBlockRef));
+  memcpy(htab.data() + o_huff, huffs.data(), huffs.size() * sizeof(JpegHuff));
+  memcpy(htab.data() + o_qt, qts.data(), qts.size() * 2);
+  memcpy(htab.data() + o_px, px0.data(), px0.size() * 8);
+  if (hipMemcpyAsync(din, hin.data(), ecs_total, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dtab, htab.data(), tab_total, hipMemcpyHostToDevice, st) != hipSuccess) {
+    *err = "JPEG batch upload";
+    return FI_EDEVICE;
+  }
+  const JpegDesc *dd = (const JpegDesc *)(dtab + o_desc);
+  // the distinct Huffman tables go to LDS when they are few (kJpegLdsTabs)
+  const int nhuff = (int)huffs.size();
+  hipLaunchKernelGGL(k_jpeg_huff, dim3((unsigned)((ivs.size() + kJpegLanes - 1) / kJpegLanes)), dim3(64), 0, st, dd,
+                     (const JpegInterval *)(dtab + o_iv), (int)ivs.size(), (const JpegHuff *)(dtab + o_huff), nhuff,
+                     dwork);
+  hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((refs.size() + 255) / 256)), dim3(256), 0, st, dd,
+                     (const JpegBlockRef *)(dtab + o_ref), (int)refs.size(), (const uint16_t *)(dtab + o_qt), dwork);
+  hipLaunchKernelGGL(k_jpeg_color, dim3((unsigned)((px0.back() + 255) / 256)), dim3(256), 0, st, dd,
+                     (const int64_t *)(dtab + o_px), (int)descs.size(), dwork);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+    *err = "JPEG decode kernels";
+    return FI_EDEVICE;
+  }
+  return 0;
+}
+
+}  // namespace fi

@@ -67,6 +67,14 @@ def plan_bytes(sizes_ops):
     return [int(out[i]) for i in range(n)]
 
 
+def jpeg_info(blob: bytes):
+    """(width, height, channels) of a JPEG the GPU decoder handles, else None
+    (fi_jpeg_info: progressive, CMYK, 4:1:1, ... decode on the host)."""
+    w, h, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    rc = L.lib().fi_jpeg_info(blob, len(blob), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c))
+    return (w.value, h.value, c.value) if rc == L.FI_OK else None
+
+
 class Context:
     def __init__(self, device: int = 0):
         self._lib = L.lib()
@@ -250,6 +258,45 @@ class Context:
         out = np.empty(nbytes, np.uint8)
         L.check(self._lib.fi_memcpy_d2h(self.h, out.ctypes.data, dptr, nbytes))
         return out
+
+    def jpeg_decode(self, blobs: list[bytes], dptrs: list[int], strides: list[int]) -> list[int]:
+        """fi_jpeg_decode_device: decodes baseline JPEG byte strings into the
+        device buffers ``dptrs`` (HWC rows of ``strides`` bytes; channels as
+        jpeg_info says); returns the per-image status (0 = decoded,
+        FI_EUNSUPPORTED = decode that one on the host)."""
+        n = len(blobs)
+        bufs = [ctypes.create_string_buffer(b, len(b)) for b in blobs]
+        data = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+        lens = (ctypes.c_size_t * n)(*[len(b) for b in blobs])
+        dst = (ctypes.c_void_p * n)(*dptrs)
+        st = (ctypes.c_int64 * n)(*strides)
+        status = (ctypes.c_int32 * n)()
+        rc = self._lib.fi_jpeg_decode_device(self.h, data, lens, n, dst, st, status)
+        if rc not in (L.FI_OK, L.FI_EUNSUPPORTED, L.FI_EINVAL):
+            L.check(rc)
+        return list(status)
+
+    def jpeg_decode_host(self, blobs: list[bytes]) -> list[np.ndarray | None]:
+        """jpeg_decode into scratch device buffers, copied back (tests / tools):
+        HWC uint8 arrays (H, W, 3) or (H, W) for gray; None where the GPU
+        decoder returned a non-zero status."""
+        infos = [jpeg_info(b) for b in blobs]
+        sizes = [(i[0] * i[1] * i[2]) if i else 1 for i in infos]
+        ptrs = [self.malloc(max(sz, 1)) for sz in sizes]
+        try:
+            status = self.jpeg_decode(blobs, ptrs, [(i[0] * i[2]) if i else 1 for i in infos])
+            out = []
+            for info, p, sz, s in zip(infos, ptrs, sizes, status):
+                if s != 0 or not info:
+                    out.append(None)
+                    continue
+                w, h, c = info
+                a = self.d2h(p, sz)
+                out.append(a.reshape(h, w, 3) if c == 3 else a.reshape(h, w))
+            return out
+        finally:
+            for p in ptrs:
+                self.free(p)
 
     def fill_synthetic(self, dptr: int, w: int, h: int, stride: int, seed: int):
         L.check(self._lib.fi_fill_synthetic(self.h, dptr, w, h, stride, seed & 0xFFFFFFFF))

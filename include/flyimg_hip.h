@@ -274,6 +274,20 @@ int fi_debug_convolve(fi_ctx *ctx, const uint16_t *q16, int32_t w, int32_t h, in
                       uint32_t ops, uint8_t *out);
 int fi_debug_monochrome(fi_ctx *ctx, const uint16_t *gray, int32_t w, int32_t h, int32_t rot, uint8_t *out,
                         int32_t out_stride);
+/* GPU JPEG decode: the decode step of ImageProcessor's `convert` (IM reads
+ * the source with libjpeg; ImageProcessor.php:66-110) moved onto the device,
+ * bit-exact with libjpeg-turbo's default decompression (islow IDCT, fancy
+ * upsampling, YCbCr->RGB).  Baseline / extended sequential Huffman 8-bit
+ * streams with one scan: gray, or YCbCr with 4:4:4, 4:2:2 or 4:2:0 chroma.
+ * fi_jpeg_info (host only): dimensions and output channels (1 gray, 3 RGB),
+ * FI_EUNSUPPORTED for streams to decode on the host (progressive, CMYK, ...).
+ * fi_jpeg_decode_device: decodes n streams (host memory) into caller device
+ * buffers dst[i] (HWC rows of dst_stride[i] bytes) and waits; status[i] per
+ * image; returns the first failing status (the other images are decoded). */
+int fi_jpeg_info(const uint8_t *data, size_t len, int32_t *w, int32_t *h, int32_t *channels);
+int fi_jpeg_decode_device(fi_ctx *ctx, const uint8_t *const *data, const size_t *len, int32_t n,
+                          uint8_t *const *dst, const int64_t *dst_stride, int32_t *status);
+
 /* Test hook (not a reference interface): the skin / saturation table k_sc_fz
  * reads (2^24 entries, index (r << 16) | (g << 8) | b, value skin | sat << 8)
  * built for `params` (NULL: defaults) and copied to out, so a test can compare
