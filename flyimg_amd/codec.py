@@ -106,39 +106,110 @@ class _PinnedSlot:
         return self._slices(buf, sizes)
 
 
-class CodecPipeline:
-    """Batches of encoded images through decode -> GPU -> encode."""
+def gpu_decodable(blob: bytes):
+    """(width, height) when the GPU decoder (fi_jpeg_decode_device) produces
+    exactly what decode_ex would: a baseline YCbCr JPEG (fi_jpeg_info) with no
+    EXIF rotation to apply; None otherwise (gray, progressive, CMYK, PNG, ...)."""
+    from PIL import Image
 
-    def __init__(self, ctx, threads: int = 16):
+    from .runtime import jpeg_info
+
+    info = jpeg_info(blob)
+    if not info or info[2] != 3:
+        return None
+    try:
+        orientation = Image.open(io.BytesIO(blob)).getexif().get(0x0112, 1)  # headers only
+    except Exception:  # noqa: BLE001 - unreadable EXIF: let the host path decide
+        return None
+    return info[:2] if orientation in (0, 1) else None
+
+
+class CodecPipeline:
+    """Batches of encoded images through decode -> GPU -> encode.  With
+    ``gpu_decode`` (default) baseline YCbCr JPEGs are decoded on the MI355X
+    straight into device memory (bit-exact with the host decoder) and only
+    the other sources take the host decoder."""
+
+    def __init__(self, ctx, threads: int = 16, gpu_decode: bool = True):
         self.ctx = ctx
         self.pool = ThreadPoolExecutor(max_workers=max(1, threads))
+        self.gpu_decode = gpu_decode
 
     def close(self):
         self.pool.shutdown()
 
-    def process(self, blobs: list[bytes], options: list[str]):
-        """Returns (encoded outputs, fi_image records); a failed image raises
-        ExecFailedException as Processor::execute does."""
+    @staticmethod
+    def _quality(bag):
+        q = bag.get_option("quality")
+        return int(q) if not _empty(q) else 90
+
+    def _host_batch(self, blobs, bags):
         decoded = list(self.pool.map(decode_ex, blobs))
-        srcs, ops, quality = [], [], []
-        for (img, pseudo), opts in zip(decoded, options):
-            bag = OptionsBag(opts)
+        srcs, ops = [], []
+        for (img, pseudo), bag in zip(decoded, bags):
             img = ExtractProcessor.extract(bag, img)
             h, w = img.shape[:2]
-            q = bag.get_option("quality")
-            quality.append(int(q) if not _empty(q) else 90)
             op = ImageProcessor(bag, w, h).to_op()
             if pseudo:
                 op.flags |= L.FI_SRC_PSEUDOCLASS
             ops.append(op)
             srcs.append(np.ascontiguousarray(img))
-        outs, recs, rc = self.ctx.process(srcs, ops)
+        outs, recs, _ = self.ctx.process(srcs, ops)
+        return outs, list(recs)
+
+    def _gpu_batch(self, blobs, bags, dims):
+        """GPU decode into one device pool (16-B aligned rows for the streaming
+        resample kernels), one device batch.
+        Returns (outputs, records, indices the GPU decoder turned down)."""
+        strides = [(w * 3 + 15) // 16 * 16 for w, _ in dims]
+        offs = np.concatenate([[0], np.cumsum([(s * h + 255) // 256 * 256 for s, (_, h) in zip(strides, dims)])])
+        base = self.ctx.malloc(int(offs[-1]))
+        try:
+            ptrs = [base + int(o) for o in offs[:-1]]
+            status = self.ctx.jpeg_decode(blobs, ptrs, strides)
+            views, ops, keep = [], [], []
+            for i, (bag, (w, h), p, st) in enumerate(zip(bags, dims, ptrs, strides)):
+                if status[i] != L.FI_OK:
+                    continue
+                views.append((p, w, h, st))
+                ops.append(ImageProcessor(bag, w, h).to_op())
+                keep.append(i)
+            outs, recs, _ = self.ctx.process_device_views(views, ops)
+        finally:
+            self.ctx.free(base)
+        full_o, full_r = [None] * len(blobs), [None] * len(blobs)
+        for k, i in enumerate(keep):
+            full_o[i], full_r[i] = outs[k], recs[k]
+        return full_o, full_r, [i for i in range(len(blobs)) if status[i] != L.FI_OK]
+
+    def process(self, blobs: list[bytes], options: list[str]):
+        """Returns (encoded outputs, fi_image records); a failed image raises
+        ExecFailedException as Processor::execute does."""
+        bags = [OptionsBag(o) for o in options]
+        n = len(blobs)
+        outs, recs = [None] * n, [None] * n
+        # extract (e_1) views start at any byte: the host path copies them to an
+        # aligned array, so they decode there and take the same kernels
+        # (bag.get: extract_key would consume the option, as InputImage::extractKey does)
+        dims = [gpu_decodable(b) if self.gpu_decode and _empty(bag.get("extract")) else None
+                for b, bag in zip(blobs, bags)]
+        host = [i for i in range(n) if dims[i] is None]
+        gpu = [i for i in range(n) if dims[i] is not None]
+        if gpu:
+            o, r, back = self._gpu_batch([blobs[i] for i in gpu], [bags[i] for i in gpu], [dims[i] for i in gpu])
+            for k, i in enumerate(gpu):
+                outs[i], recs[i] = o[k], r[k]
+            host += [gpu[k] for k in back]
+        if host:
+            o, r = self._host_batch([blobs[i] for i in host], [bags[i] for i in host])
+            for k, i in enumerate(host):
+                outs[i], recs[i] = o[k], r[k]
         for i, r in enumerate(recs):
             if r.status != L.FI_OK:
                 msg = L.lib().fi_last_error()
                 raise ExecFailedException("Command failed.\nThe exit code: %d\n%s" % (
                     r.status, msg.decode() if msg else f"image {i}"))
-        encoded = list(self.pool.map(lambda a: encode(a[0], a[1]), zip(outs, quality)))
+        encoded = list(self.pool.map(lambda a: encode(a[0], a[1]), zip(outs, [self._quality(b) for b in bags])))
         return encoded, recs
 
     def _prepare(self, slot, blobs, options):

@@ -221,7 +221,9 @@ struct fi_ctx {
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   bool sc_skinsat = true;   // FI_DISABLE_SC_SKINSAT=1: k_sc_fz evaluates skin / saturation per pixel (f64)
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
-  DevBuf jpeg[3];           // GPU JPEG decode: compressed input, tables + descriptors, coefficients + planes
+  DevBuf jpeg[3];           // GPU JPEG decode: upload (compressed data + tables), -, coefficients + planes
+  void *jpeg_host = nullptr;  // its pinned staging
+  size_t jpeg_host_cap = 0;
   std::string skinsat_key;
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
@@ -2311,6 +2313,8 @@ int fi_jpeg_info(const uint8_t *data, size_t len, int32_t *w, int32_t *h, int32_
 }
 static void *jpeg_alloc(void *actx, int which, size_t bytes) {
   fi_ctx *c = static_cast<fi_ctx *>(actx);
+  if (which == 3)  // pinned host staging (the previous call has synchronised)
+    return ensure_pinned_buf(&c->jpeg_host, &c->jpeg_host_cap, bytes) == FI_OK ? c->jpeg_host : nullptr;
   return ensure(c, &c->jpeg[which], bytes) == FI_OK ? c->jpeg[which].p : nullptr;
 }
 int fi_jpeg_decode_device(fi_ctx *c, const uint8_t *const *data, const size_t *len, int32_t n, uint8_t *const *dst,
@@ -2552,6 +2556,7 @@ void fi_destroy(fi_ctx *c) {
                     &c->jpeg[2]})
     if (b->p) (void)hipFree(b->p);
   if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->jpeg_host) (void)hipHostFree(c->jpeg_host);
   for (Slot &sl : c->slots) {
     if (sl.blob) (void)hipHostFree(sl.blob);
     if (sl.res) (void)hipHostFree(sl.res);

@@ -320,7 +320,7 @@ struct JpegDesc {        // one image of a decode batch
   int32_t tq[3], td[3], ta[3];     // quant / DC / AC table of each component
   int32_t bw[3], bh[3];            // component block grid (whole MCUs)
   int32_t dw[3], dh[3];            // downsampled width / height (jdmaster.c)
-  int64_t coef[3];                 // byte offsets in the work buffer: int16 blocks [bh][bw][64], natural order
+  int64_t coef[3];                 // byte offsets in the work buffer: int16 blocks [bh][bw][64], zigzag order
   int64_t plane[3];                // u8 samples [bh * 8][bw * 8]
   int32_t qt;                      // index of the image's 4 quant tables (u16 [4][64], natural order)
   int32_t ht[4];                   // its Huffman tables DC0, DC1, AC0, AC1 (batch table index, -1: none)

@@ -5,10 +5,11 @@
 //   host     marker parse (SOF0/SOF1 8-bit, DQT, DHT, DRI, one SOS), canonical
 //            Huffman tables deduplicated over the batch, restart intervals
 //            located by their RSTn markers;
-//   k_jpeg_huff   one thread per restart interval (the whole scan when there
-//            is none): jdhuff.c's sequential decode -- DC prediction, AC run /
+//   k_jpeg_huff   one 64-lane workgroup per restart interval (the whole scan
+//            when there is none), the lanes in lockstep on wave-uniform state,
+//            the segment window spread over the lanes: jdhuff.c's sequential decode -- DC prediction, AC run /
 //            size symbols, HUFF_EXTEND -- into int16 coefficient blocks in
-//            natural order; byte stuffing and markers as jdhuff.c (a marker
+//            zigzag order (the IDCT reads them back in natural order); byte stuffing and markers as jdhuff.c (a marker
 //            feeds zero bits);
 //   k_jpeg_idct   one thread per 8x8 block: jidctint.c jpeg_idct_islow
 //            (dequantise, 13-bit constants, PASS1_BITS 2, range limit);
@@ -30,11 +31,6 @@
 #include "fi_internal.h"
 
 namespace fi {
-
-__constant__ uint8_t c_natural[64 + 16] = {  // jpeg_natural_order (+16 guard entries)
-    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13,
-    6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31,
-    39, 46, 53, 60, 61, 54, 47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
 
 // ---------------------------------------------------------------------------
 // host: headers
@@ -216,35 +212,41 @@ static bool jpeg_build_huff(const std::string &dht, JpegHuff *t) {
 // ---------------------------------------------------------------------------
 // device: Huffman decode
 // ---------------------------------------------------------------------------
-constexpr int kJpegLanes = 16;   // intervals per 64-lane workgroup (one per lane < kJpegLanes)
 constexpr int kJpegLdsTabs = 8;  // distinct Huffman tables staged in LDS (more: read from global)
 
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+// All 64 lanes of the workgroup decode the same interval in lockstep (the
+// values are wave-uniform, so no lane diverges): the 256-byte window of the
+// segment is spread over the lanes, lane i holding bytes [wbase + 4 i, + 4),
+// read with v_readlane; the next 256 bytes are in flight in `nxt` (their
+// latency hides behind the decode of the current window).  The segment is
+// zero padded by >= 512 bytes.
 struct BitReader {
-  const uint8_t *p;  // 16-byte aligned base of the window
-  uint4 c0, c1;      // bytes [base, base + 32)
-  int base, pos, end;
+  const uint8_t *p;
+  uint32_t win, nxt;
+  int wbase, pos, end;
   uint64_t buf;
   int nbits;
   bool marker;
-  __device__ __forceinline__ uint32_t byte_at(int q) const {
-    const int o = q - base;  // 0 .. 31
-    const uint4 &c = o < 16 ? c0 : c1;
-    const int w = (o >> 2) & 3;
-    const uint32_t d = w == 0 ? c.x : w == 1 ? c.y : w == 2 ? c.z : c.w;
-    return (d >> (8 * (o & 3))) & 255u;
-  }
   __device__ __forceinline__ void advance_window() {
-    while (pos - base >= 16) {  // keep [pos, pos + 1] inside the window
-      c0 = c1;
-      base += 16;
-      c1 = *reinterpret_cast<const uint4 *>(p + base + 16);
+    if (pos - wbase >= 256) {  // bytes [pos, pos + 4) stay inside win + the first dword of nxt
+      win = nxt;
+      wbase += 256;
+      nxt = *(g_u32 *)(p + wbase + 256 + 4 * (threadIdx.x & 63));
     }
+  }
+  // the 4 bytes at pos, little-endian
+  __device__ __forceinline__ uint32_t word_at_pos() const {
+    const int o = __builtin_amdgcn_readfirstlane(pos - wbase), k = o >> 2;
+    const uint32_t lo = __builtin_amdgcn_readlane(win, k);
+    const uint32_t hi = k < 63 ? __builtin_amdgcn_readlane(win, k + 1) : __builtin_amdgcn_readfirstlane(nxt);
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3));
   }
   __device__ void init(const uint8_t *ecs, int byte0, int len) {
     p = ecs;
-    base = byte0 & ~15;
-    c0 = *reinterpret_cast<const uint4 *>(p + base);
-    c1 = *reinterpret_cast<const uint4 *>(p + base + 16);
+    wbase = byte0 & ~255;
+    win = *(g_u32 *)(p + wbase + 4 * (threadIdx.x & 63));
+    nxt = *(g_u32 *)(p + wbase + 256 + 4 * (threadIdx.x & 63));
     pos = byte0;
     end = len;
     buf = 0;
@@ -252,15 +254,28 @@ struct BitReader {
     marker = false;
   }
   // jdhuff.c jpeg_fill_bit_buffer: stuffed 0xFF00 -> 0xFF; at a marker (or the
-  // end of the data) zero bits are supplied
+  // end of the data) zero bits are supplied.  Called once per symbol: leaves
+  // >= 32 bits, enough for a code (<= 16) and its value bits (<= 16); four
+  // bytes at a time while they hold no 0xFF, else byte by byte.
   __device__ __forceinline__ void fill() {
-    while (nbits <= 56) {
+    if (nbits >= 32) return;
+    const uint32_t w = word_at_pos();
+    const uint32_t t = ~w;
+    const bool ff = ((t - 0x01010101u) & ~t & 0x80808080u) != 0u;  // some byte of w is 0xFF
+    if (!ff && !marker && pos + 4 <= end) {
+      buf = (buf << 32) | __builtin_bswap32(w);
+      nbits += 32;
+      pos += 4;
+      advance_window();
+      return;
+    }
+    while (nbits < 32) {
       uint32_t b = 0;
       if (!marker && pos < end) {
-        advance_window();
-        b = byte_at(pos);
+        const uint32_t x = word_at_pos();
+        b = x & 255u;
         if (b == 0xFFu) {
-          if (byte_at(pos + 1) == 0u) {
+          if (((x >> 8) & 255u) == 0u) {
             pos += 2;
           } else {
             marker = true;
@@ -269,6 +284,7 @@ struct BitReader {
         } else {
           pos++;
         }
+        advance_window();
       }
       buf = (buf << 8) | b;
       nbits += 8;
@@ -278,7 +294,8 @@ struct BitReader {
   __device__ __forceinline__ void skip(int n) { nbits -= n; }
 };
 
-__device__ __forceinline__ int jpeg_decode_sym(BitReader &br, const JpegHuff *t) {
+template <typename TAB>
+__device__ __forceinline__ int jpeg_decode_sym(BitReader &br, const TAB *t) {
   br.fill();
   const uint32_t lk = t->look[br.peek(9)];
   if (lk) {
@@ -302,41 +319,59 @@ __device__ __forceinline__ int jpeg_extend(uint32_t r, int s) {  // HUFF_EXTEND
   return r < (1u << (s - 1)) ? (int)r - (1 << s) + 1 : (int)r;
 }
 
+template <bool LDS>
 __global__ __launch_bounds__(64) void k_jpeg_huff(const JpegDesc *__restrict__ descs,
                                                   const JpegInterval *__restrict__ ivs, int niv,
                                                   const JpegHuff *__restrict__ huff, int nhuff,
                                                   uint8_t *__restrict__ work) {
   __shared__ JpegHuff sh[kJpegLdsTabs];
-  __shared__ int16_t blk[kJpegLanes][64];
+  __shared__ __attribute__((aligned(16))) int16_t blk[64];
   const int tid = threadIdx.x;
-  const bool lds_tabs = nhuff <= kJpegLdsTabs;
-  if (lds_tabs) {
+  if (LDS) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(huff);
     uint32_t *dstw = reinterpret_cast<uint32_t *>(sh);
     const int nw = nhuff * (int)sizeof(JpegHuff) / 4;
     for (int i = tid; i < nw; i += 64) dstw[i] = src[i];
   }
-  for (int i = tid; i < kJpegLanes * 64 / 2; i += 64) reinterpret_cast<uint32_t *>(blk)[i] = 0;
+  if (tid < 32) reinterpret_cast<uint32_t *>(blk)[tid] = 0;
   __syncthreads();
-  const int iv = blockIdx.x * kJpegLanes + tid;
-  if (tid >= kJpegLanes || iv >= niv) return;
+  const int iv = blockIdx.x;
+  if (iv >= niv) return;
   const JpegInterval I = ivs[iv];
-  const JpegDesc &D = descs[I.img];
-  const JpegHuff *tabs = lds_tabs ? sh : huff;
+  const JpegDesc *Dp = descs + I.img;
+  // the descriptor in registers (the block stores below may alias it for the
+  // compiler: fields read through the pointer would be reloaded per block)
+  const int ncomp = Dp->ncomp, mcux = Dp->mcux;
+  int tdc[3], tac[3], hs[3], vs[3], bw[3];
+  int64_t co[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const bool on = c < ncomp;
+    tdc[c] = on ? Dp->ht[Dp->td[c]] : 0;
+    tac[c] = on ? Dp->ht[2 + Dp->ta[c]] : 0;
+    hs[c] = on ? Dp->h[c] : 0;
+    vs[c] = on ? Dp->v[c] : 0;
+    bw[c] = on ? Dp->bw[c] : 0;
+    co[c] = on ? Dp->coef[c] : 0;
+  }
+  // the address space of the table reads is static: LDS reads (ds_read, ~100
+  // cycles) or global ones, never flat pointers into either
+  typedef __attribute__((address_space(3))) const JpegHuff l_huff;
+  typedef __attribute__((address_space(1))) const JpegHuff g_huff;
   BitReader br;
-  br.init(D.ecs, I.byte0, D.ecs_len);
-  int pred[3] = {0, 0, 0};
-  int16_t *b = blk[tid];
+  br.init(Dp->ecs, I.byte0, Dp->ecs_len);
+  int pred[3] = {0, 0, 0};  // DC predictions (static indices only: registers)
+  int16_t *b = blk;
   for (int mcu = I.mcu0; mcu < I.mcu1; mcu++) {
-    const int my = mcu / D.mcux, mx = mcu - my * D.mcux;
-    for (int c = 0; c < D.ncomp; c++) {
-      const JpegHuff *dc = tabs + D.ht[D.td[c]], *ac = tabs + D.ht[2 + D.ta[c]];
-      for (int by = 0; by < D.v[c]; by++)
-        for (int bx = 0; bx < D.h[c]; bx++) {
+    const int my = mcu / mcux, mx = mcu - my * mcux;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      if (c >= ncomp) break;
+      for (int by = 0; by < vs[c]; by++)
+        for (int bx = 0; bx < hs[c]; bx++) {
           // DC: difference from the component's previous block
-          int s = jpeg_decode_sym(br, dc);
-          if (s) {
-            br.fill();
+          int s = LDS ? jpeg_decode_sym(br, (l_huff *)(sh + tdc[c])) : jpeg_decode_sym(br, (g_huff *)(huff + tdc[c]));
+          if (s) {  // (the symbol's fill left enough bits for its value)
             const uint32_t r = br.peek(s);
             br.skip(s);
             s = jpeg_extend(r, s);
@@ -345,27 +380,26 @@ __global__ __launch_bounds__(64) void k_jpeg_huff(const JpegDesc *__restrict__ d
           b[0] = (int16_t)pred[c];
           // AC: run / size symbols
           for (int k = 1; k < 64; k++) {
-            const int rs = jpeg_decode_sym(br, ac);
+            const int rs = LDS ? jpeg_decode_sym(br, (l_huff *)(sh + tac[c]))
+                               : jpeg_decode_sym(br, (g_huff *)(huff + tac[c]));
             const int r = rs >> 4, sz = rs & 15;
             if (sz) {
               k += r;
-              br.fill();
               const uint32_t v = br.peek(sz);
               br.skip(sz);
-              b[c_natural[k < 79 ? k : 79]] = (int16_t)jpeg_extend(v, sz);
+              b[k < 63 ? k : 63] = (int16_t)jpeg_extend(v, sz);  // zigzag order (k > 63: jpeg_natural_order's guard -> 63)
             } else {
               if (r != 15) break;
               k += 15;
             }
           }
-          // block -> work, and clear the staging block
-          const int row = my * D.v[c] + by, col = mx * D.h[c] + bx;
-          uint4 *o = reinterpret_cast<uint4 *>(work + D.coef[c] + ((int64_t)row * D.bw[c] + col) * 128);
-          uint4 *bb = reinterpret_cast<uint4 *>(b);
-#pragma unroll
-          for (int q = 0; q < 8; q++) {
-            o[q] = bb[q];
-            bb[q] = uint4{0, 0, 0, 0};
+          // block -> work (lanes 0-7: 16 bytes each), and clear the staging block
+          const int row = my * vs[c] + by, col = mx * hs[c] + bx;
+          if (tid < 8) {
+            uint4 *o = reinterpret_cast<uint4 *>(work + co[c] + ((int64_t)row * bw[c] + col) * 128);
+            uint4 *bb = reinterpret_cast<uint4 *>(b);
+            o[tid] = bb[tid];
+            bb[tid] = uint4{0, 0, 0, 0};
           }
         }
     }
@@ -401,8 +435,13 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(const JpegDesc *__restrict__ 
                 F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
   int ws[64];
   int cf[64];
+  // coefficient blocks are stored in zigzag order: natural k = jpeg_natural_order[z]
+  constexpr uint8_t zz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                              12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                              35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                              58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 #pragma unroll
-  for (int k = 0; k < 64; k++) cf[k] = (int)in[k] * (int)q[k];
+  for (int z = 0; z < 64; z++) cf[zz[z]] = (int)in[z] * (int)q[zz[z]];
   // pass 1: columns
 #pragma unroll
   for (int x = 0; x < 8; x++) {
@@ -570,9 +609,9 @@ int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c) {
   return 0;
 }
 
-// Plans and runs one decode batch.  `alloc(which, bytes)` returns device
-// memory (0: compressed input, 1: tables/descriptors, 2: work) that stays
-// valid until the stream has run; `stage` is a pinned host buffer provider.
+// Plans and runs one decode batch.  `alloc(which, bytes)` returns memory that
+// stays valid until the stream has run: 0 device upload (compressed data +
+// tables), 2 device work (coefficients + planes), 3 pinned host staging.
 int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *len, int n, uint8_t *const *dst,
                       const int64_t *dst_stride, int32_t *status, void *(*alloc)(void *, int, size_t), void *actx,
                       std::string *err) {
@@ -662,49 +701,55 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
     for (int c = 0; c < H.ncomp; c++)
       for (int b = 0; b < D.bw[c] * D.bh[c]; b++) refs.push_back({img, c, b});
     px0.push_back(px0.back() + (int64_t)H.W * H.H);
-    ecs_total += ((size_t)D.ecs_len + 32 + 15) & ~(size_t)15;  // zero pad: the reader's window
+    ecs_total += ((size_t)D.ecs_len + 512 + 255) & ~(size_t)255;  // zero pad: the reader's window
     descs.push_back(D);
     desc_img.push_back(i);
   }
   if (descs.empty()) return 0;
-  // device buffers: compressed data, tables + descriptors, work
-  uint8_t *din = (uint8_t *)alloc(actx, 0, ecs_total);
+  // one upload: compressed data (each segment zero padded for the reader's
+  // window) then tables + descriptors, staged in pinned host memory
   const size_t o_desc = 0, o_iv = o_desc + ((descs.size() * sizeof(JpegDesc) + 255) & ~(size_t)255);
   const size_t o_ref = o_iv + ((ivs.size() * sizeof(JpegInterval) + 255) & ~(size_t)255);
   const size_t o_huff = o_ref + ((refs.size() * sizeof(JpegBlockRef) + 255) & ~(size_t)255);
   const size_t o_qt = o_huff + ((huffs.size() * sizeof(JpegHuff) + 255) & ~(size_t)255);
   const size_t o_px = o_qt + ((qts.size() * 2 + 255) & ~(size_t)255);
-  const size_t tab_total = o_px + px0.size() * 8;
-  uint8_t *dtab = (uint8_t *)alloc(actx, 1, tab_total);
+  const size_t tab0 = (ecs_total + 255) & ~(size_t)255, up_total = tab0 + o_px + px0.size() * 8;
+  uint8_t *din = (uint8_t *)alloc(actx, 0, up_total);
+  uint8_t *hst = (uint8_t *)alloc(actx, 3, up_total);
   uint8_t *dwork = (uint8_t *)alloc(actx, 2, std::max(work_total, (size_t)256));
-  if (!din || !dtab || !dwork) {
-    *err = "device memory for the JPEG batch";
+  if (!din || !hst || !dwork) {
+    *err = "memory for the JPEG batch";
     return FI_ENOMEM;
   }
-  std::vector<uint8_t> hin(ecs_total, 0), htab(tab_total, 0);
+  uint8_t *dtab = din + tab0, *htab = hst + tab0;
   for (size_t k = 0; k < descs.size(); k++) {
     JpegDesc &D = descs[k];
     const size_t off = (size_t)reinterpret_cast<uintptr_t>(D.ecs);
-    memcpy(hin.data() + off, data[desc_img[k]] + hd[desc_img[k]].ecs0, D.ecs_len);
+    memcpy(hst + off, data[desc_img[k]] + hd[desc_img[k]].ecs0, D.ecs_len);
+    const size_t pad_end = k + 1 < descs.size() ? (size_t)reinterpret_cast<uintptr_t>(descs[k + 1].ecs) : tab0;
+    memset(hst + off + D.ecs_len, 0, pad_end - off - D.ecs_len);
     D.ecs = din + off;
   }
-  memcpy(htab.data() + o_desc, descs.data(), descs.size() * sizeof(JpegDesc));
-  memcpy(htab.data() + o_iv, ivs.data(), ivs.size() * sizeof(JpegInterval));
-  memcpy(htab.data() + o_ref, refs.data(), refs.size() * sizeof(JpegBlockRef));
-  memcpy(htab.data() + o_huff, huffs.data(), huffs.size() * sizeof(JpegHuff));
-  memcpy(htab.data() + o_qt, qts.data(), qts.size() * 2);
-  memcpy(htab.data() + o_px, px0.data(), px0.size() * 8);
-  if (hipMemcpyAsync(din, hin.data(), ecs_total, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(dtab, htab.data(), tab_total, hipMemcpyHostToDevice, st) != hipSuccess) {
+  memcpy(htab + o_desc, descs.data(), descs.size() * sizeof(JpegDesc));
+  memcpy(htab + o_iv, ivs.data(), ivs.size() * sizeof(JpegInterval));
+  memcpy(htab + o_ref, refs.data(), refs.size() * sizeof(JpegBlockRef));
+  memcpy(htab + o_huff, huffs.data(), huffs.size() * sizeof(JpegHuff));
+  memcpy(htab + o_qt, qts.data(), qts.size() * 2);
+  memcpy(htab + o_px, px0.data(), px0.size() * 8);
+  if (hipMemcpyAsync(din, hst, up_total, hipMemcpyHostToDevice, st) != hipSuccess) {
     *err = "JPEG batch upload";
     return FI_EDEVICE;
   }
   const JpegDesc *dd = (const JpegDesc *)(dtab + o_desc);
   // the distinct Huffman tables go to LDS when they are few (kJpegLdsTabs)
   const int nhuff = (int)huffs.size();
-  hipLaunchKernelGGL(k_jpeg_huff, dim3((unsigned)((ivs.size() + kJpegLanes - 1) / kJpegLanes)), dim3(64), 0, st, dd,
-                     (const JpegInterval *)(dtab + o_iv), (int)ivs.size(), (const JpegHuff *)(dtab + o_huff), nhuff,
-                     dwork);
+  const dim3 g((unsigned)ivs.size());  // one restart interval per 64-lane workgroup
+  if (nhuff <= kJpegLdsTabs)
+    hipLaunchKernelGGL(k_jpeg_huff<true>, g, dim3(64), 0, st, dd, (const JpegInterval *)(dtab + o_iv), (int)ivs.size(),
+                       (const JpegHuff *)(dtab + o_huff), nhuff, dwork);
+  else
+    hipLaunchKernelGGL(k_jpeg_huff<false>, g, dim3(64), 0, st, dd, (const JpegInterval *)(dtab + o_iv),
+                       (int)ivs.size(), (const JpegHuff *)(dtab + o_huff), nhuff, dwork);
   hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((refs.size() + 255) / 256)), dim3(256), 0, st, dd,
                      (const JpegBlockRef *)(dtab + o_ref), (int)refs.size(), (const uint16_t *)(dtab + o_qt), dwork);
   hipLaunchKernelGGL(k_jpeg_color, dim3((unsigned)((px0.back() + 255) / 256)), dim3(256), 0, st, dd,

@@ -265,8 +265,8 @@ class Context:
         jpeg_info says); returns the per-image status (0 = decoded,
         FI_EUNSUPPORTED = decode that one on the host)."""
         n = len(blobs)
-        bufs = [ctypes.create_string_buffer(b, len(b)) for b in blobs]
-        data = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+        bufs = [ctypes.c_char_p(b) for b in blobs]  # the bytes objects' own storage, no copy
+        data = (ctypes.c_void_p * n)(*[ctypes.cast(b, ctypes.c_void_p).value for b in bufs])
         lens = (ctypes.c_size_t * n)(*[len(b) for b in blobs])
         dst = (ctypes.c_void_p * n)(*dptrs)
         st = (ctypes.c_int64 * n)(*strides)
@@ -297,6 +297,40 @@ class Context:
         finally:
             for p in ptrs:
                 self.free(p)
+
+    def process_device_views(self, views, ops: list[Op]):
+        """fi_process_batch_device on device-resident RGB8 sources given as
+        (device pointer, width, height, stride) views (e.g. fi_jpeg_decode_device
+        targets, extract offsets applied); outputs land in a scratch device
+        buffer and come back as host arrays: (outputs, fi_image records, rc)
+        like ``process``."""
+        n = len(views)
+        arr = (L.FiImage * max(n, 1))()
+        for i, ((p, w, h, st), op) in enumerate(zip(views, ops)):
+            a = arr[i]
+            a.src, a.src_w, a.src_h, a.src_stride, a.src_channels = p, w, h, st, 3
+            _fill(a, op)
+        L.lib().fi_plan(arr, n)
+        caps = [max(arr[i].out_w * arr[i].out_h * max(arr[i].out_channels, 1), 1) for i in range(n)]
+        offs = np.concatenate([[0], np.cumsum([(c + 255) // 256 * 256 for c in caps])]).astype(np.int64)
+        base = self.malloc(int(offs[-1]) if n else 256)
+        try:
+            for i in range(n):
+                arr[i].dst, arr[i].dst_capacity = base + int(offs[i]), caps[i]
+            rc = self._lib.fi_process_batch_device(self.h, arr, n)
+            results = []
+            for i in range(n):
+                a = arr[i]
+                if a.status == L.FI_OK:
+                    o = self.d2h(base + int(offs[i]), a.out_h * a.out_stride)
+                    o = o.reshape(a.out_h, a.out_stride)[:, : a.out_w * a.out_channels]
+                    o = o.reshape(a.out_h, a.out_w, a.out_channels)
+                    results.append(o[:, :, 0] if a.out_channels == 1 else o)
+                else:
+                    results.append(None)
+        finally:
+            self.free(base)
+        return results, [arr[i] for i in range(n)], rc
 
     def fill_synthetic(self, dptr: int, w: int, h: int, stride: int, seed: int):
         L.check(self._lib.fi_fill_synthetic(self.h, dptr, w, h, stride, seed & 0xFFFFFFFF))

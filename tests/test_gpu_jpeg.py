@@ -133,3 +133,42 @@ def test_jpeg_decode_then_resize_matches_host_decode(ctx):
     outs_b, recs_b, rc_b = ctx.process([_ref(blob)], [op])
     assert rc_a == rc_b == 0
     assert np.array_equal(outs_a[0], outs_b[0])
+
+
+def test_codec_pipeline_gpu_decode_equals_host_decode(ctx):
+    """CodecPipeline.process with the GPU decoder (baseline JPEGs decoded into
+    device memory) returns byte-identical encoded outputs and the same records
+    as the host-decode pipeline, on a mixed batch: 4:2:0 / 4:4:4 JPEGs, an
+    extract, a progressive JPEG, an EXIF-rotated JPEG and a PNG (the last four
+    decode on the host)."""
+    from flyimg_amd.codec import CodecPipeline, gpu_decodable
+
+    rot = io.BytesIO()
+    im = Image.fromarray(synth_rgb(300, 200, 9))
+    ex = im.getexif()
+    ex[0x0112] = 6
+    im.save(rot, "JPEG", quality=90, exif=ex.tobytes())
+    png = io.BytesIO()
+    Image.fromarray(synth_rgb(320, 240, 10)).save(png, "PNG")
+    blobs = [
+        _enc(synth_rgb(1280, 720, 1), quality=90, subsampling=2),
+        _enc(synth_rgb(999, 555, 2), quality=85, subsampling=0),
+        _enc(synth_rgb(800, 600, 3), quality=90, subsampling=2),
+        _enc(synth_rgb(640, 480, 4), quality=90, progressive=True),
+        rot.getvalue(),
+        png.getvalue(),
+    ]
+    opts = ["w_500,smc_1,q_90", "w_300,h_250,c_1", "e_1,p1x_100,p1y_50,p2x_700,p2y_450,w_200",
+            "w_200,h_200,c_1", "w_150", "w_100,q_80"]
+    assert [gpu_decodable(b) is not None for b in blobs] == [True, True, True, False, False, False]
+    res = {}
+    for gd in (True, False):
+        pipe = CodecPipeline(ctx, threads=4, gpu_decode=gd)
+        try:
+            res[gd] = pipe.process(blobs, opts)
+        finally:
+            pipe.close()
+    (ea, ra), (eb, rb) = res[True], res[False]
+    assert ea == eb
+    key = ("out_w", "out_h", "crop_x", "crop_y", "crop_w", "crop_h", "status")
+    assert [[getattr(r, k) for k in key] for r in ra] == [[getattr(r, k) for k in key] for r in rb]
