@@ -24,8 +24,11 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
+#include <functional>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fi_internal.h"
@@ -626,8 +629,24 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
   std::vector<JpegBlockRef> refs;
   std::vector<int64_t> px0(1, 0);
   size_t ecs_total = 0, work_total = 0;
+  // header parse (incl. the scan for the end of each entropy-coded segment)
+  // and, below, the staging copies run on a few host threads
+  const int nthr = (int)std::min<size_t>(8, std::max<size_t>(1, (size_t)n / 16));
+  auto parallel = [&](int count, const std::function<void(int)> &fn) {
+    if (nthr <= 1 || count < 2) {
+      for (int i = 0; i < count; i++) fn(i);
+      return;
+    }
+    std::atomic<int> next(0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthr; t++)
+      th.emplace_back([&]() {
+        for (int i = next++; i < count; i = next++) fn(i);
+      });
+    for (auto &t : th) t.join();
+  };
+  parallel(n, [&](int i) { status[i] = jpeg_parse(data[i], len[i], &hd[i]); });
   for (int i = 0; i < n; i++) {
-    status[i] = jpeg_parse(data[i], len[i], &hd[i]);
     if (status[i]) continue;
     JpegHdr &H = hd[i];
     JpegDesc D{};
@@ -722,14 +741,15 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
     return FI_ENOMEM;
   }
   uint8_t *dtab = din + tab0, *htab = hst + tab0;
-  for (size_t k = 0; k < descs.size(); k++) {
-    JpegDesc &D = descs[k];
+  parallel((int)descs.size(), [&](int k) {
+    const JpegDesc &D = descs[k];
     const size_t off = (size_t)reinterpret_cast<uintptr_t>(D.ecs);
     memcpy(hst + off, data[desc_img[k]] + hd[desc_img[k]].ecs0, D.ecs_len);
-    const size_t pad_end = k + 1 < descs.size() ? (size_t)reinterpret_cast<uintptr_t>(descs[k + 1].ecs) : tab0;
+    const size_t pad_end =
+        k + 1 < (int)descs.size() ? (size_t)reinterpret_cast<uintptr_t>(descs[k + 1].ecs) : tab0;
     memset(hst + off + D.ecs_len, 0, pad_end - off - D.ecs_len);
-    D.ecs = din + off;
-  }
+  });
+  for (JpegDesc &D : descs) D.ecs = din + (size_t)reinterpret_cast<uintptr_t>(D.ecs);
   memcpy(htab + o_desc, descs.data(), descs.size() * sizeof(JpegDesc));
   memcpy(htab + o_iv, ivs.data(), ivs.size() * sizeof(JpegInterval));
   memcpy(htab + o_ref, refs.data(), refs.size() * sizeof(JpegBlockRef));

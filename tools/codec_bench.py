@@ -4,8 +4,9 @@ JPEG 1920x1080 q90 in -> decode (threads) -> GPU w_500,smc_1 -> JPEG q90 out,
 batches of --batch images, first serially (decode, fi_process_batch with
 pageable buffers, encode), then pipelined (CodecPipeline.process_batches:
 decode into pinned slots, fi_submit_batch, encode of batch k during batch
-k+1).  Prints one JSON line with both stage splits; gpu_path_share = host
-time blocked on the GPU path / wall."""
+k+1), then with the JPEGs decoded on the GPU (CodecPipeline gpu_decode).
+Prints one JSON line with the stage splits; gpu_path_share = host time
+blocked on the GPU path / wall."""
 import argparse
 import io
 import json
@@ -36,7 +37,7 @@ def main():
         Image.fromarray(synth_rgb(1920, 1080, 100 + i)).save(b, "JPEG", quality=90)
         blobs.append(b.getvalue())
     ctx = Context(0)
-    pipe = codec.CodecPipeline(ctx, a.threads)
+    pipe = codec.CodecPipeline(ctx, a.threads, gpu_decode=False)
     pipe.process(blobs[:2], [a.options] * 2)  # warm
     t_dec = t_gpu = t_enc = 0.0
     t0 = time.perf_counter()
@@ -79,8 +80,23 @@ def main():
     piped = {"images": got, "images_per_s": round(got / el, 1), "input_mpix_per_s": round(got * 1920 * 1080 / 1e6 / el, 1),
              "wall_s": round(el, 3), "s_decode": round(st["s_decode"], 3), "s_gpu_wait": round(st["s_gpu_wait"], 3),
              "s_encode": round(st["s_encode"], 3), "gpu_path_share": round(st["s_gpu_wait"] / el, 4)}
+    # GPU decode: CodecPipeline.process decodes the (baseline YCbCr) JPEGs on
+    # the MI355X into device memory (fi_jpeg_decode_device), one device batch,
+    # host threads only encode the outputs
+    gpipe = codec.CodecPipeline(ctx, a.threads, gpu_decode=True)
+    gpipe.process(blobs[:2], [a.options] * 2)  # warm
+    t0 = time.perf_counter()
+    done = 0
+    while done < a.images:
+        n = min(a.batch, a.images - done)
+        gpipe.process([blobs[(done + k) % len(blobs)] for k in range(n)], [a.options] * n)
+        done += n
+    el = time.perf_counter() - t0
+    gdec = {"images": done, "images_per_s": round(done / el, 1),
+            "input_mpix_per_s": round(done * 1920 * 1080 / 1e6 / el, 1), "wall_s": round(el, 3)}
+    gpipe.close()
     print(json.dumps({"batch": a.batch, "threads": a.threads, "options": a.options, "serial": serial,
-                      "pipelined": piped}))
+                      "pipelined": piped, "gpu_decode": gdec}))
     pipe.close()
     ctx.close()
 
