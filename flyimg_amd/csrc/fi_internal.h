@@ -310,6 +310,8 @@ struct JpegHuff {        // one Huffman table (jdhuff.c canonical decoding)
   int32_t maxcode[18];   // largest code of each length (-1: none); [17] sentinel
   int32_t valoff[18];    // huffval index = code + valoff[length]
   uint8_t huffval[256];
+  int16_t fast_ac[512];  // AC tables: code + value bits within the 9-bit lookahead:
+                         // (value << 8) | (run << 4) | total length; 0 = not this fast path
 };
 struct JpegDesc {        // one image of a decode batch
   const uint8_t *ecs;    // entropy-coded segment (device)

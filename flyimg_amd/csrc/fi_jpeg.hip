@@ -209,6 +209,18 @@ static bool jpeg_build_huff(const std::string &dht, JpegHuff *t) {
     code <<= 1;
   }
   t->maxcode[17] = 0x7FFFFFFF;
+  // fast AC entries (as stb_image's fast_ac): run/size symbols whose code and
+  // value bits both fit the 9-bit lookahead and whose value fits a signed byte
+  for (int l = 0; l < 512; l++) {
+    const int lk = t->look[l];
+    if (!lk) continue;
+    const int len = lk >> 8, rs = lk & 255, run = rs >> 4, sz = rs & 15;
+    if (sz == 0 || len + sz > 9) continue;
+    const int v = (l >> (9 - len - sz)) & ((1 << sz) - 1);
+    const int val = v < (1 << (sz - 1)) ? v - (1 << sz) + 1 : v;  // HUFF_EXTEND
+    if (val < -128 || val > 127) continue;
+    t->fast_ac[l] = (int16_t)((val * 256) | (run << 4) | (len + sz));
+  }
   return p == nv;
 }
 
@@ -383,6 +395,15 @@ __global__ __launch_bounds__(64) void k_jpeg_huff(const JpegDesc *__restrict__ d
           b[0] = (int16_t)pred[c];
           // AC: run / size symbols
           for (int k = 1; k < 64; k++) {
+            br.fill();
+            const int fa = LDS ? ((l_huff *)(sh + tac[c]))->fast_ac[br.peek(9)]
+                               : ((g_huff *)(huff + tac[c]))->fast_ac[br.peek(9)];
+            if (fa) {  // code + value in one lookahead
+              k += (fa >> 4) & 15;
+              br.skip(fa & 15);
+              b[k < 63 ? k : 63] = (int16_t)(fa >> 8);
+              continue;
+            }
             const int rs = LDS ? jpeg_decode_sym(br, (l_huff *)(sh + tac[c]))
                                : jpeg_decode_sym(br, (g_huff *)(huff + tac[c]));
             const int r = rs >> 4, sz = rs & 15;
@@ -418,16 +439,24 @@ __device__ __forceinline__ uint8_t jpeg_range_limit(int x) {  // IDCT_range_limi
   return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
 }
 
-struct JpegBlockRef {  // one block of the batch: image, component, block index
-  int32_t img, comp, blk;
-};
-
+// one thread per 8x8 block of the batch; blk0[j] = first block of the j-th
+// (image, component) pair (3 pairs per image, empty ones for gray), blk0[3 n] = total
 __global__ __launch_bounds__(256) void k_jpeg_idct(const JpegDesc *__restrict__ descs,
-                                                   const JpegBlockRef *__restrict__ refs, int nref,
+                                                   const int64_t *__restrict__ blk0, int nimg,
                                                    const uint16_t *__restrict__ qts, uint8_t *__restrict__ work) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= nref) return;
-  const JpegBlockRef R = refs[i];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= blk0[3 * nimg]) return;
+  int lo = 0, hi = 3 * nimg;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (blk0[mid] <= i)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  struct {
+    int img, comp, blk;
+  } R = {lo / 3, lo % 3, (int)(i - blk0[lo])};
   const JpegDesc &D = descs[R.img];
   const int c = R.comp;
   const int by = R.blk / D.bw[c], bx = R.blk - by * D.bw[c];
@@ -626,7 +655,8 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
   std::vector<JpegDesc> descs;
   std::vector<int> desc_img;
   std::vector<JpegInterval> ivs;
-  std::vector<JpegBlockRef> refs;
+  std::vector<int64_t> blk0;  // first block of each (image, component)
+  int64_t nblocks = 0;
   std::vector<int64_t> px0(1, 0);
   size_t ecs_total = 0, work_total = 0;
   // header parse (incl. the scan for the end of each entropy-coded segment)
@@ -717,8 +747,10 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
     } else {
       ivs.push_back({img, 0, nmcu, 0});
     }
-    for (int c = 0; c < H.ncomp; c++)
-      for (int b = 0; b < D.bw[c] * D.bh[c]; b++) refs.push_back({img, c, b});
+    for (int c = 0; c < 3; c++) {
+      blk0.push_back(nblocks);
+      if (c < H.ncomp) nblocks += (int64_t)D.bw[c] * D.bh[c];
+    }
     px0.push_back(px0.back() + (int64_t)H.W * H.H);
     ecs_total += ((size_t)D.ecs_len + 512 + 255) & ~(size_t)255;  // zero pad: the reader's window
     descs.push_back(D);
@@ -729,7 +761,8 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
   // window) then tables + descriptors, staged in pinned host memory
   const size_t o_desc = 0, o_iv = o_desc + ((descs.size() * sizeof(JpegDesc) + 255) & ~(size_t)255);
   const size_t o_ref = o_iv + ((ivs.size() * sizeof(JpegInterval) + 255) & ~(size_t)255);
-  const size_t o_huff = o_ref + ((refs.size() * sizeof(JpegBlockRef) + 255) & ~(size_t)255);
+  blk0.push_back(nblocks);
+  const size_t o_huff = o_ref + ((blk0.size() * 8 + 255) & ~(size_t)255);
   const size_t o_qt = o_huff + ((huffs.size() * sizeof(JpegHuff) + 255) & ~(size_t)255);
   const size_t o_px = o_qt + ((qts.size() * 2 + 255) & ~(size_t)255);
   const size_t tab0 = (ecs_total + 255) & ~(size_t)255, up_total = tab0 + o_px + px0.size() * 8;
@@ -752,7 +785,7 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
   for (JpegDesc &D : descs) D.ecs = din + (size_t)reinterpret_cast<uintptr_t>(D.ecs);
   memcpy(htab + o_desc, descs.data(), descs.size() * sizeof(JpegDesc));
   memcpy(htab + o_iv, ivs.data(), ivs.size() * sizeof(JpegInterval));
-  memcpy(htab + o_ref, refs.data(), refs.size() * sizeof(JpegBlockRef));
+  memcpy(htab + o_ref, blk0.data(), blk0.size() * 8);
   memcpy(htab + o_huff, huffs.data(), huffs.size() * sizeof(JpegHuff));
   memcpy(htab + o_qt, qts.data(), qts.size() * 2);
   memcpy(htab + o_px, px0.data(), px0.size() * 8);
@@ -770,8 +803,8 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
   else
     hipLaunchKernelGGL(k_jpeg_huff<false>, g, dim3(64), 0, st, dd, (const JpegInterval *)(dtab + o_iv),
                        (int)ivs.size(), (const JpegHuff *)(dtab + o_huff), nhuff, dwork);
-  hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((refs.size() + 255) / 256)), dim3(256), 0, st, dd,
-                     (const JpegBlockRef *)(dtab + o_ref), (int)refs.size(), (const uint16_t *)(dtab + o_qt), dwork);
+  hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, st, dd,
+                     (const int64_t *)(dtab + o_ref), (int)descs.size(), (const uint16_t *)(dtab + o_qt), dwork);
   hipLaunchKernelGGL(k_jpeg_color, dim3((unsigned)((px0.back() + 255) / 256)), dim3(256), 0, st, dd,
                      (const int64_t *)(dtab + o_px), (int)descs.size(), dwork);
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
