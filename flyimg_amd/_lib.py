@@ -166,7 +166,7 @@ def lib():
     L.fi_debug_convolve.argtypes = [vp, vp, i32, i32, i32, vp, ctypes.c_uint32, vp]
     L.fi_debug_skinsat.argtypes = [vp, vp, vp]
     L.fi_jpeg_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t, P(i32), P(i32), P(i32)]
-    L.fi_jpeg_decode_device.argtypes = [vp, vp, vp, i32, vp, vp, vp]
+    L.fi_jpeg_decode_device.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp]
     _lib = L
     return L
 

@@ -107,26 +107,28 @@ class _PinnedSlot:
 
 
 def gpu_decodable(blob: bytes):
-    """(width, height) when the GPU decoder (fi_jpeg_decode_device) produces
-    exactly what decode_ex would: a baseline YCbCr JPEG (fi_jpeg_info) with no
-    EXIF rotation to apply; None otherwise (gray, progressive, CMYK, PNG, ...)."""
+    """(width, height, source channels) when the GPU decoder
+    (fi_jpeg_decode_device, RGB output) produces exactly what decode_ex would:
+    a baseline gray or YCbCr JPEG (fi_jpeg_info) with no EXIF rotation to
+    apply; None otherwise (progressive, CMYK, PNG, ...).  A gray (1-component)
+    JPEG is an IM PseudoClass source, as decode_ex flags it."""
     from PIL import Image
 
     from .runtime import jpeg_info
 
     info = jpeg_info(blob)
-    if not info or info[2] != 3:
+    if not info:
         return None
     try:
         orientation = Image.open(io.BytesIO(blob)).getexif().get(0x0112, 1)  # headers only
     except Exception:  # noqa: BLE001 - unreadable EXIF: let the host path decide
         return None
-    return info[:2] if orientation in (0, 1) else None
+    return info if orientation in (0, 1) else None
 
 
 class CodecPipeline:
     """Batches of encoded images through decode -> GPU -> encode.  With
-    ``gpu_decode`` (default) baseline YCbCr JPEGs are decoded on the MI355X
+    ``gpu_decode`` (default) baseline gray / YCbCr JPEGs are decoded on the MI355X
     straight into device memory (bit-exact with the host decoder) and only
     the other sources take the host decoder."""
 
@@ -161,18 +163,21 @@ class CodecPipeline:
         """GPU decode into one device pool (16-B aligned rows for the streaming
         resample kernels), one device batch.
         Returns (outputs, records, indices the GPU decoder turned down)."""
-        strides = [(w * 3 + 15) // 16 * 16 for w, _ in dims]
-        offs = np.concatenate([[0], np.cumsum([(s * h + 255) // 256 * 256 for s, (_, h) in zip(strides, dims)])])
+        strides = [(w * 3 + 15) // 16 * 16 for w, _, _ in dims]
+        offs = np.concatenate([[0], np.cumsum([(s * h + 255) // 256 * 256 for s, (_, h, _) in zip(strides, dims)])])
         base = self.ctx.malloc(int(offs[-1]))
         try:
             ptrs = [base + int(o) for o in offs[:-1]]
-            status = self.ctx.jpeg_decode(blobs, ptrs, strides)
+            status = self.ctx.jpeg_decode(blobs, ptrs, strides, channels=3)
             views, ops, keep = [], [], []
-            for i, (bag, (w, h), p, st) in enumerate(zip(bags, dims, ptrs, strides)):
+            for i, (bag, (w, h, c), p, st) in enumerate(zip(bags, dims, ptrs, strides)):
                 if status[i] != L.FI_OK:
                     continue
                 views.append((p, w, h, st))
-                ops.append(ImageProcessor(bag, w, h).to_op())
+                op = ImageProcessor(bag, w, h).to_op()
+                if c == 1:  # 1-component JPEG: IM PseudoClass (Mitchell), as decode_ex flags it
+                    op.flags |= L.FI_SRC_PSEUDOCLASS
+                ops.append(op)
                 keep.append(i)
             outs, recs, _ = self.ctx.process_device_views(views, ops)
         finally:

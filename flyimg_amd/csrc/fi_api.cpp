@@ -52,8 +52,8 @@ int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32
 int launch_sc_skinsat(hipStream_t s, uint16_t *table, const ScParamsDev &P);
 int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c);
 int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *len, int n, uint8_t *const *dst,
-                      const int64_t *dst_stride, int32_t *status, void *(*alloc)(void *, int, size_t), void *actx,
-                      std::string *err);
+                      const int64_t *dst_stride, int out_channels, int32_t *status,
+                      void *(*alloc)(void *, int, size_t), void *actx, std::string *err);
 int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, int max_px, const DevCrop *crops,
                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P);
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
@@ -2318,14 +2318,15 @@ static void *jpeg_alloc(void *actx, int which, size_t bytes) {
   return ensure(c, &c->jpeg[which], bytes) == FI_OK ? c->jpeg[which].p : nullptr;
 }
 int fi_jpeg_decode_device(fi_ctx *c, const uint8_t *const *data, const size_t *len, int32_t n, uint8_t *const *dst,
-                          const int64_t *dst_stride, int32_t *status) {
-  if (!c || n < 0 || (n > 0 && (!data || !len || !dst || !dst_stride || !status)))
+                          const int64_t *dst_stride, int32_t out_channels, int32_t *status) {
+  if (!c || n < 0 || (n > 0 && (!data || !len || !dst || !dst_stride || !status)) ||
+      (out_channels != 0 && out_channels != 3))
     return set_err(FI_EINVAL, "bad arguments");
   if (n == 0) return FI_OK;
   HIP_TRY(hipSetDevice(c->device));
   std::lock_guard<std::mutex> lk(c->mu);
   std::string err;
-  const int rc = jpeg_decode_batch(c->stream, data, len, n, dst, dst_stride, status, jpeg_alloc, c, &err);
+  const int rc = jpeg_decode_batch(c->stream, data, len, n, dst, dst_stride, out_channels, status, jpeg_alloc, c, &err);
   if (rc) return set_err(rc, "%s", err.c_str());
   for (int i = 0; i < n; i++)  // the others are decoded; the caller decodes these on the host
     if (status[i])

@@ -326,8 +326,9 @@ struct JpegDesc {        // one image of a decode batch
   int64_t plane[3];                // u8 samples [bh * 8][bw * 8]
   int32_t qt;                      // index of the image's 4 quant tables (u16 [4][64], natural order)
   int32_t ht[4];                   // its Huffman tables DC0, DC1, AC0, AC1 (batch table index, -1: none)
-  uint8_t *dst;                    // HWC: 3 channels (YCbCr sources) or 1 (gray)
+  uint8_t *dst;                    // HWC: 3 channels (YCbCr sources, or gray replicated) or 1 (gray)
   int64_t dst_stride;
+  int32_t dst_c;
 };
 struct JpegInterval {    // one restart interval: its MCUs and where its bits start
   int32_t img, mcu0, mcu1, byte0;

@@ -611,7 +611,8 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const JpegDesc *__restrict__
   const int yp = D.bw[0] * 8;
   const uint8_t Y = work[D.plane[0] + (int64_t)y * yp + x];
   if (D.ncomp == 1) {
-    D.dst[(int64_t)y * D.dst_stride + x] = Y;
+    uint8_t *o = D.dst + (int64_t)y * D.dst_stride + x * D.dst_c;
+    for (int k = 0; k < D.dst_c; k++) o[k] = Y;
     return;
   }
   const int hs = D.h[0], vs = D.v[0];
@@ -645,8 +646,8 @@ int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c) {
 // stays valid until the stream has run: 0 device upload (compressed data +
 // tables), 2 device work (coefficients + planes), 3 pinned host staging.
 int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *len, int n, uint8_t *const *dst,
-                      const int64_t *dst_stride, int32_t *status, void *(*alloc)(void *, int, size_t), void *actx,
-                      std::string *err) {
+                      const int64_t *dst_stride, int out_channels, int32_t *status,
+                      void *(*alloc)(void *, int, size_t), void *actx, std::string *err) {
   std::vector<JpegHdr> hd(n);
   std::vector<int> ok(n, 0);
   std::map<std::string, int> huff_ix;
@@ -729,6 +730,7 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
     D.ecs = reinterpret_cast<const uint8_t *>(ecs_total);  // offset until placed
     D.dst = dst[i];
     D.dst_stride = dst_stride[i];
+    D.dst_c = out_channels == 3 || H.ncomp == 3 ? 3 : 1;
     const int img = (int)descs.size();
     // restart intervals: RSTn markers split the segment
     const int nmcu = D.mcux * D.mcuy;

@@ -259,10 +259,11 @@ class Context:
         L.check(self._lib.fi_memcpy_d2h(self.h, out.ctypes.data, dptr, nbytes))
         return out
 
-    def jpeg_decode(self, blobs: list[bytes], dptrs: list[int], strides: list[int]) -> list[int]:
+    def jpeg_decode(self, blobs: list[bytes], dptrs: list[int], strides: list[int], channels: int = 0) -> list[int]:
         """fi_jpeg_decode_device: decodes baseline JPEG byte strings into the
         device buffers ``dptrs`` (HWC rows of ``strides`` bytes; channels as
-        jpeg_info says); returns the per-image status (0 = decoded,
+        jpeg_info says, or 3 for every image with ``channels=3``: gray
+        replicated); returns the per-image status (0 = decoded,
         FI_EUNSUPPORTED = decode that one on the host)."""
         n = len(blobs)
         bufs = [ctypes.c_char_p(b) for b in blobs]  # the bytes objects' own storage, no copy
@@ -271,7 +272,7 @@ class Context:
         dst = (ctypes.c_void_p * n)(*dptrs)
         st = (ctypes.c_int64 * n)(*strides)
         status = (ctypes.c_int32 * n)()
-        rc = self._lib.fi_jpeg_decode_device(self.h, data, lens, n, dst, st, status)
+        rc = self._lib.fi_jpeg_decode_device(self.h, data, lens, n, dst, st, channels, status)
         if rc not in (L.FI_OK, L.FI_EUNSUPPORTED, L.FI_EINVAL):
             L.check(rc)
         return list(status)

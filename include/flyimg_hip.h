@@ -282,11 +282,13 @@ int fi_debug_monochrome(fi_ctx *ctx, const uint16_t *gray, int32_t w, int32_t h,
  * fi_jpeg_info (host only): dimensions and output channels (1 gray, 3 RGB),
  * FI_EUNSUPPORTED for streams to decode on the host (progressive, CMYK, ...).
  * fi_jpeg_decode_device: decodes n streams (host memory) into caller device
- * buffers dst[i] (HWC rows of dst_stride[i] bytes) and waits; status[i] per
- * image; returns the first failing status (the other images are decoded). */
+ * buffers dst[i] (HWC rows of dst_stride[i] bytes; out_channels 0 = the
+ * source's, 3 = RGB for every source, gray replicated) and waits; status[i]
+ * per image; returns the first failing status (the others are decoded). */
 int fi_jpeg_info(const uint8_t *data, size_t len, int32_t *w, int32_t *h, int32_t *channels);
 int fi_jpeg_decode_device(fi_ctx *ctx, const uint8_t *const *data, const size_t *len, int32_t n,
-                          uint8_t *const *dst, const int64_t *dst_stride, int32_t *status);
+                          uint8_t *const *dst, const int64_t *dst_stride, int32_t out_channels,
+                          int32_t *status);
 
 /* Test hook (not a reference interface): the skin / saturation table k_sc_fz
  * reads (2^24 entries, index (r << 16) | (g << 8) | b, value skin | sat << 8)

@@ -80,6 +80,21 @@ def test_jpeg_decode_gray_bit_exact(ctx, w, h, q):
     assert got.shape == ref.shape and np.array_equal(got, ref)
 
 
+def test_jpeg_decode_gray_as_rgb(ctx):
+    """out_channels=3: a gray stream comes out with its luma in all three
+    channels (Image.convert("RGB") of the decode), a YCbCr one unchanged."""
+    blobs = [_enc(synth_rgb(57, 43, 6)[..., 2].copy(), quality=85), _enc(synth_rgb(57, 43, 7), quality=85)]
+    ptrs = [ctx.malloc(57 * 43 * 3) for _ in blobs]
+    try:
+        assert ctx.jpeg_decode(blobs, ptrs, [57 * 3] * 2, channels=3) == [0, 0]
+        got = [ctx.d2h(p, 57 * 43 * 3).reshape(43, 57, 3) for p in ptrs]
+    finally:
+        for p in ptrs:
+            ctx.free(p)
+    for g, b in zip(got, blobs):
+        assert np.array_equal(g, np.asarray(Image.open(io.BytesIO(b)).convert("RGB")))
+
+
 def test_jpeg_decode_batch_mixed_with_unsupported(ctx):
     """One call: several geometries and samplings; a progressive and a CMYK
     stream get FI_EUNSUPPORTED (host decode) and the others are exact."""
@@ -138,9 +153,9 @@ def test_jpeg_decode_then_resize_matches_host_decode(ctx):
 def test_codec_pipeline_gpu_decode_equals_host_decode(ctx):
     """CodecPipeline.process with the GPU decoder (baseline JPEGs decoded into
     device memory) returns byte-identical encoded outputs and the same records
-    as the host-decode pipeline, on a mixed batch: 4:2:0 / 4:4:4 JPEGs, an
-    extract, a progressive JPEG, an EXIF-rotated JPEG and a PNG (the last four
-    decode on the host)."""
+    as the host-decode pipeline, on a mixed batch: 4:2:0 / 4:4:4 JPEGs, a gray
+    JPEG (PseudoClass: Mitchell), an extract, a progressive JPEG, an
+    EXIF-rotated JPEG and a PNG (the last four decode on the host)."""
     from flyimg_amd.codec import CodecPipeline, gpu_decodable
 
     rot = io.BytesIO()
@@ -157,10 +172,11 @@ def test_codec_pipeline_gpu_decode_equals_host_decode(ctx):
         _enc(synth_rgb(640, 480, 4), quality=90, progressive=True),
         rot.getvalue(),
         png.getvalue(),
+        _enc(synth_rgb(720, 480, 11)[..., 1].copy(), quality=90),
     ]
     opts = ["w_500,smc_1,q_90", "w_300,h_250,c_1", "e_1,p1x_100,p1y_50,p2x_700,p2y_450,w_200",
-            "w_200,h_200,c_1", "w_150", "w_100,q_80"]
-    assert [gpu_decodable(b) is not None for b in blobs] == [True, True, True, False, False, False]
+            "w_200,h_200,c_1", "w_150", "w_100,q_80", "w_300,h_200,c_1"]
+    assert [gpu_decodable(b) is not None for b in blobs] == [True, True, True, False, False, False, True]
     res = {}
     for gd in (True, False):
         pipe = CodecPipeline(ctx, threads=4, gpu_decode=gd)
