@@ -441,11 +441,19 @@ __device__ __forceinline__ uint8_t jpeg_range_limit(int x) {  // IDCT_range_limi
 
 // one thread per 8x8 block of the batch; blk0[j] = first block of the j-th
 // (image, component) pair (3 pairs per image, empty ones for gray), blk0[3 n] = total
+__device__ __forceinline__ void jpeg_idct_block(const JpegDesc *__restrict__ descs, const int64_t *__restrict__ blk0,
+                                                int nimg, const uint16_t *__restrict__ qts, uint8_t *__restrict__ work,
+                                                int64_t i);
+// (grid-stride, as k_jpeg_color)
 __global__ __launch_bounds__(256) void k_jpeg_idct(const JpegDesc *__restrict__ descs,
                                                    const int64_t *__restrict__ blk0, int nimg,
                                                    const uint16_t *__restrict__ qts, uint8_t *__restrict__ work) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= blk0[3 * nimg]) return;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < blk0[3 * nimg]; i += (int64_t)gridDim.x * 256)
+    jpeg_idct_block(descs, blk0, nimg, qts, work, i);
+}
+__device__ __forceinline__ void jpeg_idct_block(const JpegDesc *__restrict__ descs, const int64_t *__restrict__ blk0,
+                                                int nimg, const uint16_t *__restrict__ qts, uint8_t *__restrict__ work,
+                                                int64_t i) {
   int lo = 0, hi = 3 * nimg;
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
@@ -592,9 +600,8 @@ __device__ __forceinline__ int jpeg_up(const uint8_t *pl, int pitch, int dw, int
 }
 __device__ __forceinline__ uint8_t jpeg_clamp(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
 
-__global__ __launch_bounds__(256) void k_jpeg_color(const JpegDesc *__restrict__ descs, const int64_t *__restrict__ px0,
-                                                    int nimg, const uint8_t *__restrict__ work) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void jpeg_color_px(const JpegDesc *__restrict__ descs, const int64_t *__restrict__ px0,
+                                              int nimg, const uint8_t *__restrict__ work, int64_t i) {
   // image of pixel i: binary search over the per-image pixel prefix
   int lo = 0, hi = nimg;
   while (hi - lo > 1) {
@@ -627,6 +634,13 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const JpegDesc *__restrict__
   o[0] = jpeg_clamp(r);
   o[1] = jpeg_clamp(g);
   o[2] = jpeg_clamp(b);
+}
+
+// (grid-stride: a dispatch's work-item count is 32-bit, a batch may hold more pixels)
+__global__ __launch_bounds__(256) void k_jpeg_color(const JpegDesc *__restrict__ descs, const int64_t *__restrict__ px0,
+                                                    int nimg, const uint8_t *__restrict__ work) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < px0[nimg]; i += (int64_t)gridDim.x * 256)
+    jpeg_color_px(descs, px0, nimg, work, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -805,9 +819,9 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
   else
     hipLaunchKernelGGL(k_jpeg_huff<false>, g, dim3(64), 0, st, dd, (const JpegInterval *)(dtab + o_iv),
                        (int)ivs.size(), (const JpegHuff *)(dtab + o_huff), nhuff, dwork);
-  hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, st, dd,
+  hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)std::min<int64_t>((nblocks + 255) / 256, 1 << 20)), dim3(256), 0, st, dd,
                      (const int64_t *)(dtab + o_ref), (int)descs.size(), (const uint16_t *)(dtab + o_qt), dwork);
-  hipLaunchKernelGGL(k_jpeg_color, dim3((unsigned)((px0.back() + 255) / 256)), dim3(256), 0, st, dd,
+  hipLaunchKernelGGL(k_jpeg_color, dim3((unsigned)std::min<int64_t>((px0.back() + 255) / 256, 1 << 20)), dim3(256), 0, st, dd,
                      (const int64_t *)(dtab + o_px), (int)descs.size(), dwork);
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
     *err = "JPEG decode kernels";

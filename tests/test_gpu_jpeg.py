@@ -188,3 +188,21 @@ def test_codec_pipeline_gpu_decode_equals_host_decode(ctx):
     assert ea == eb
     key = ("out_w", "out_h", "crop_x", "crop_y", "crop_w", "crop_h", "status")
     assert [[getattr(r, k) for k in key] for r in ra] == [[getattr(r, k) for k in key] for r in rb]
+
+
+def test_jpeg_decode_batch_beyond_2_32_pixels(ctx):
+    """2100 1080p images (4.35 G pixels, 13 GB of output) in one call: the
+    per-pixel and per-block kernels stride over the batch (a dispatch's
+    work-item count is 32-bit), so images past 2^32 pixels decode too."""
+    W, H, N = 1920, 1080, 2100
+    blob = _enc(synth_rgb(W, H, 5), quality=90, subsampling=2)
+    ref = _ref(blob)
+    stride = W * 3
+    base = ctx.malloc(stride * H * N)
+    try:
+        st = ctx.jpeg_decode([blob] * N, [base + i * stride * H for i in range(N)], [stride] * N)
+        assert st == [0] * N
+        for i in (0, 1000, 2069, N - 1):
+            assert np.array_equal(ctx.d2h(base + i * stride * H, stride * H).reshape(H, W, 3), ref), i
+    finally:
+        ctx.free(base)
