@@ -92,3 +92,47 @@ def test_oracle_under_asan_ubsan():
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
         assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
         assert "0 unexpected errors" in r.stdout
+
+
+def _jpeg_inputs(d):
+    """Small JPEGs of every layout the GPU decoder's parser accepts, plus the
+    progressive smart_crop.jpg fixture (rejected as unsupported)."""
+    import io
+
+    import numpy as np
+    from PIL import Image
+    rng = np.random.default_rng(5)
+    px = rng.integers(0, 256, (37, 53, 3), dtype=np.uint8)
+    cases = [("s420.jpg", dict(quality=90, subsampling=2)),
+             ("s444r.jpg", dict(quality=75, subsampling=0, restart_marker_blocks=2)),
+             ("s422o.jpg", dict(quality=95, subsampling=1, optimize=True))]
+    paths = []
+    for name, kw in cases:
+        b = io.BytesIO()
+        Image.fromarray(px).save(b, "JPEG", **kw)
+        paths.append(os.path.join(d, name))
+        open(paths[-1], "wb").write(b.getvalue())
+    b = io.BytesIO()
+    Image.fromarray(px[..., 0]).save(b, "JPEG", quality=80)
+    paths.append(os.path.join(d, "gray.jpg"))
+    open(paths[-1], "wb").write(b.getvalue())
+    paths.append(os.path.join(ROOT, "tests/golden/smart_crop.jpg"))
+    return paths
+
+
+def test_jpeg_parser_under_asan_ubsan():
+    """fi_jpeg_parse.cpp (the GPU decoder's host header parser and Huffman
+    table builder) over every truncation and 3000 random mutations of each
+    input, under ASan/UBSan."""
+    hipcc = _compiler("hipcc")
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "jpeg_fuzz")
+        subprocess.run([hipcc, "-std=c++17", "-fno-gpu-sanitize", *SAN, "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests/native/jpeg_fuzz_driver.cpp"),
+                        os.path.join(ROOT, "flyimg_amd/csrc/fi_jpeg_parse.cpp"), "-o", exe],
+                       check=True, capture_output=True, timeout=300)
+        files = _jpeg_inputs(d)
+        r = subprocess.run([exe, *files], capture_output=True, text=True, timeout=300, env=ENV)
+        assert r.returncode == 0, r.stderr[-4000:]
+        assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
+        assert "DONE" in r.stdout and int(r.stdout.split()[1]) > 5 * 3000
