@@ -459,6 +459,16 @@ __global__ __launch_bounds__(256) void k_sc_skinsat(uint16_t *__restrict__ t, co
   t[c] = (uint16_t)((v & 255u) | ((v >> 16) << 8));
 }
 
+// n / d for 0 <= n < 2^22, 0 < d < 2^12 from a float reciprocal and one
+// correction each way (exact: the float quotient is within 1 of n / d)
+__device__ __forceinline__ int fz_div(int n, int d, float rcp) {
+  int q = (int)((float)n * rcp);
+  const int r = n - q * d;
+  q += r >= d ? 1 : 0;
+  q -= r < 0 ? 1 : 0;
+  return q;
+}
+
 template <bool LUT>
 __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restrict__ descs,
                                                         const int32_t *__restrict__ ai, const ScParamsDev P,
@@ -478,32 +488,60 @@ __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restric
   typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
   typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
   const int ng = PP >> 4;                                 // 16-pixel groups per plane row
+  const float rcp_ng = 1.0f / (float)ng;
   const int nitem = 16 * ng;                              // items of one 16-row block
   const bool a4 = (((uintptr_t)src | (uintptr_t)sstride) & 3) == 0;
   // one block of 16 source rows -> planes of (p - 128): items of 16 pixels of a
   // row, two per thread at a time (six 16-byte loads in flight, then the
-  // deinterleave); row tails and narrow rows byte by byte
+  // deinterleave); RGB row tails as dword + byte loads issued together (a
+  // byte-by-byte tail loop serialised ~16 load round trips per block); gray
+  // or unaligned sources byte by byte
   auto stage_block = [&](int r0) {
 #pragma unroll 1
     for (int base = 0; base < nitem; base += 2 * kFzThreads) {
       u32x4a q[2][3];
       bool fast[2];
+      int rrs[2], gs[2];
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const int it = base + u * kFzThreads + tid;
-        const int rr = it / ng, g = it - rr * ng;
-        fast[u] = it < nitem && r0 + rr < hrows && sC == 3 && a4 && 16 * g + 16 <= sW;
+        const int rr = fz_div(it, ng, rcp_ng), g = it - rr * ng;
+        rrs[u] = rr;
+        gs[u] = g;
+        fast[u] = it < nitem && sC == 3 && a4;
         if (fast[u]) {
-          const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride;
+          const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride + 48 * g;
+          const int remb = r0 + rr < hrows ? 3 * (sW - 16 * g) : 0;  // the group's bytes inside the row
+          if (remb >= 48) {
 #pragma unroll
-          for (int k = 0; k < 3; k++) q[u][k] = *reinterpret_cast<const u32x4a *>(s + 48 * g + 16 * k);
+            for (int k = 0; k < 3; k++) q[u][k] = *reinterpret_cast<const u32x4a *>(s + 16 * k);
+          } else {
+            // row tail (or a row / group past the source): whole dwords, then
+            // the last bytes, all loads in flight together; pixels past the
+            // row read as 128 like the plane padding
+            uint32_t d[12];
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+              if (4 * k + 4 <= remb) {
+                d[k] = *reinterpret_cast<const uint32_t *>(s + 4 * k);
+              } else {
+                uint32_t v = 0x80808080u;
+#pragma unroll
+                for (int j = 0; j < 3; j++)
+                  if (4 * k + j < remb) v = (v & ~(0xFFu << (8 * j))) | ((uint32_t)s[4 * k + j] << (8 * j));
+                d[k] = v;
+              }
+            }
+#pragma unroll
+            for (int k = 0; k < 3; k++) q[u][k] = u32x4a{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
+          }
         }
       }
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const int it = base + u * kFzThreads + tid;
         if (it >= nitem) break;
-        const int rr = it / ng, g = it - rr * ng;
+        const int rr = rrs[u], g = gs[u];
         const bool rowok = r0 + rr < hrows;
         const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride;
         u32x4s w0, w1, w2;
@@ -601,6 +639,10 @@ __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restric
   int produced = 0;  // H-stage rows in the ring: [produced - ring span, produced)
   const int rA = 16 * (lane >> 4) + ((lane & 15) >> 1);
   const int nq = apitch >> 4, nbytes = 3 * aw;
+  // per-thread (row, column) walks over [rows][aw] items in steps of
+  // kFzThreads: start and step once, no integer division per item
+  const int stepy = kFzThreads / aw, stepx = kFzThreads - stepy * aw;
+  const int lm0 = tid / aw, lx0 = tid - lm0 * aw;
 #pragma unroll 1
   for (int c = 0; c < chunks; c++) {
     const int k0 = ai[D.vqK0 + c];
@@ -640,9 +682,13 @@ __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restric
     }
     __syncthreads();
     const int nr = pe - pa;
+    int m = lm0, x = lx0;  // (m, x) of it, stepped by (stepy, stepx) without a division
 #pragma unroll 1
-    for (int it = tid; it < nr * aw; it += kFzThreads) {
-      const int m = it / aw, x = it - m * aw;
+    for (int it = tid; it < nr * aw; it += kFzThreads, m += stepy, x += stepx) {
+      if (x >= aw) {
+        x -= aw;
+        m++;
+      }
       const uint8_t *qq = prer + m * apitch + 3 * x;
       lum[m * lpitch + x] = (uint8_t)sc_luma(qq[0], qq[1], qq[2]);
       const int y = pa + m;
@@ -659,17 +705,29 @@ __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restric
     // flight per thread before they are used)
     const int nit = (y1 - y0) * aw;
     constexpr int kG = LUT ? kFzGather : 1;
+    int yr_n = lm0, x_n = lx0;  // (row, column) of the next item
 #pragma unroll 1
     for (int base = tid; base < nit; base += kG * kFzThreads) {
       uint32_t sv[kG];
+      int yrs[kG], xs[kG];
+#pragma unroll
+      for (int u = 0; u < kG; u++) {
+        if (x_n >= aw) {
+          x_n -= aw;
+          yr_n++;
+        }
+        yrs[u] = yr_n;
+        xs[u] = x_n;
+        yr_n += stepy;
+        x_n += stepx;
+      }
       if (LUT) {
 #pragma unroll
         for (int u = 0; u < kG; u++) {
           const int it = base + u * kFzThreads;
           sv[u] = 0;
           if (it < nit) {
-            const int yr = it / aw, x = it - yr * aw;
-            const uint8_t *qq = prer + (y0 + yr - pa) * apitch + 3 * x;
+            const uint8_t *qq = prer + (y0 + yrs[u] - pa) * apitch + 3 * xs[u];
             sv[u] = skinsat[((uint32_t)qq[0] << 16) | ((uint32_t)qq[1] << 8) | qq[2]];
           }
         }
@@ -678,7 +736,7 @@ __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restric
       for (int u = 0; u < kG; u++) {
         const int it = base + u * kFzThreads;
         if (it >= nit) break;
-        const int yr = it / aw, x = it - yr * aw, y = y0 + yr, m = y - pa;
+        const int yr = yrs[u], x = xs[u], y = y0 + yr, m = y - pa;
         const uint8_t *lrow = lum + m * lpitch;
         const uint32_t L = lrow[x];
         uint32_t E = L;
