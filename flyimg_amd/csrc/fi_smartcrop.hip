@@ -470,7 +470,7 @@ __device__ __forceinline__ int fz_div(int n, int d, float rcp) {
 }
 
 template <bool LUT>
-__global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restrict__ descs,
+__global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restrict__ descs,
                                                         const int32_t *__restrict__ ai, const ScParamsDev P,
                                                         const uint16_t *__restrict__ skinsat) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
@@ -592,16 +592,37 @@ __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restric
   const i32x4 *hmB = reinterpret_cast<const i32x4 *>(ai + D.hmB);
   const int k0l = mfma_i8_k(lane, 0), k8l = mfma_i8_k(lane, 8);
   auto hpass = [&](int r0) {  // the staged block -> H-stage rows r0 .. r0 + 15 into the ring
+    // a wave's two column blocks (b, b + 8) per pass: both blocks' weight
+    // fragments are loaded before the first block's MFMAs, so the second
+    // block's load latency hides behind the first block's work
+    constexpr int kW = kFzThreads / 64;
 #pragma unroll 1
-    for (int b = wave; b < nb; b += kFzThreads / 64) {
-      const int s0 = hmS0[b];
-      i32x4 Bf[2][3];
+    for (int bp = wave; bp < nb; bp += 2 * kW) {
+      i32x4 Bfs[2][2][3];
+      int s0s[2];
+      int32_t cxs[2];
 #pragma unroll
-      for (int t = 0; t < 2; t++)
+      for (int h = 0; h < 2; h++) {
+        const int b = bp + h * kW;
+        if (b < nb) {
+          s0s[h] = hmS0[b];
 #pragma unroll
-        for (int qq = 0; qq < 3; qq++) Bf[t][qq] = t < KS ? hmB[((b * KS + t) * 3 + qq) * 64 + lane] : i32x4{0, 0, 0, 0};
+          for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int qq = 0; qq < 3; qq++)
+              Bfs[h][t][qq] = t < KS ? hmB[((b * KS + t) * 3 + qq) * 64 + lane] : i32x4{0, 0, 0, 0};
+          const int x = 16 * b + (lane & 15);
+          cxs[h] = x < aw ? hmC[x] : 0;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+      const int b = bp + h * kW;
+      if (b >= nb) break;
+      const int s0 = s0s[h];
       const int x = 16 * b + (lane & 15);
-      const int32_t cx = x < aw ? hmC[x] : 0;
+      const int32_t cx = cxs[h];
+      i32x4 (&Bf)[2][3] = Bfs[h];
 #pragma unroll 1
       for (int c = 0; c < nch; c++) {
         i32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
@@ -631,6 +652,7 @@ __global__ __launch_bounds__(kFzThreads, 2) void k_sc_fz(const ScDesc *__restric
             }
           }
         }
+      }
       }
     }
   };
