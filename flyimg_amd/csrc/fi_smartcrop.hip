@@ -859,10 +859,12 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
       const int dxc = act ? dx : 0;
       const uint32_t *mcol = maps + (int64_t)cr.y0 * W + cr.x0 + dxc;
       const double *tcol = tab + dxc;
-#pragma unroll 4
-      for (int dy = 0; dy < cr.nin_y; dy++) {
-        const uint32_t m = act ? mcol[dy * W] : 0u;  // m = 0: every term is 0
-        const double imp = tcol[(int64_t)dy * cr.table_w];
+      // rows in groups of 4: the four map words are read unconditionally (the
+      // column is clamped) and zeroed for idle lanes after the read, so the
+      // group's map reads, then its 12 table reads, go out together (a
+      // conditional read put an exec-masked block and a full LDS wait
+      // between consecutive rows)
+      auto row_terms = [&](uint32_t m, double imp) {
         const double d = lut[(m >> 8) & 255];
         const double a1 = lut[m & 255] * (d + sb);
         const double a2 = lut[(m >> 16) & 255] * (d + tb);
@@ -872,6 +874,23 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
         id += d;
         is += a1;
         it += a2;
+      };
+      int dy = 0;
+#pragma unroll 1
+      for (; dy + 4 <= cr.nin_y; dy += 4) {
+        uint32_t m[4];
+        double imp[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) m[u] = mcol[(dy + u) * W];
+#pragma unroll
+        for (int u = 0; u < 4; u++) imp[u] = tcol[(int64_t)(dy + u) * cr.table_w];
+#pragma unroll
+        for (int u = 0; u < 4; u++) row_terms(act ? m[u] : 0u, imp[u]);  // m = 0: every term is 0
+      }
+#pragma unroll 1
+      for (; dy < cr.nin_y; dy++) {
+        const uint32_t m = mcol[dy * W];
+        row_terms(act ? m : 0u, tcol[(int64_t)dy * cr.table_w]);
       }
     }
     sd = wave_sum(sd);
