@@ -99,12 +99,9 @@ def cpu_baseline(W, H, options, budget_s=8.0, threads=None, max_images=None):
     op = ImageProcessor(OptionsBag(options), W, H).to_op()
     from flyimg_amd import _lib as L
 
-    flags = 0
-    for f, o in ((L.FI_OP_THUMBNAIL, orc.FLAG_THUMBNAIL), (L.FI_GEOM_FILL, orc.FLAG_FILL),
-                 (L.FI_GEOM_SHRINK_ONLY, orc.FLAG_SHRINK), (L.FI_OP_EXTENT, orc.FLAG_EXTENT),
-                 (L.FI_OP_GRAY, orc.FLAG_GRAY), (L.FI_OP_ROTATE, orc.FLAG_ROTATE)):
-        if op.flags & f:
-            flags |= o
+    from oracle.verify import oracle_flags
+
+    flags = oracle_flags(op)
     smc = bool(op.flags & L.FI_OP_SMARTCROP)
     if threads is None:
         try:
@@ -184,6 +181,8 @@ def main():
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--images", type=int, default=0, help="override images per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true", help="skip the oracle check of the last timed batch "
+                    "(profiling ablations only)")
     args = ap.parse_args()
 
     from flyimg_amd import _lib as L
@@ -269,6 +268,19 @@ def main():
     allv = comm.allgather_obj({"elapsed": el, "stats": stats,
                                "ncand": sum(last[i].n_candidates for i in range(nimg)),
                                "bad": bad[0]})
+    # correctness of the headline batch itself (untimed): the last timed batch's
+    # records and outputs against the oracle, including images past 2^32 of pool
+    vlast = (args.warmup + args.steps - 1) % 2
+    vok, vtot, verr = (0, 0, None)
+    if not args.no_verify:
+        from oracle.verify import verify_batch, verify_sample  # the checker (test infrastructure)
+
+        vok, vtot, verr = verify_batch(
+            ctx, last, verify_sample(nimg, src_bytes), lambda i: pool + i * src_bytes,
+            lambda i: 0x5EED + rank * nimg + i, W, H, src_stride, op, lambda i: dsts[vlast] + i * dst_cap, dst_cap)
+        if verr:
+            log(f"rank {rank}: VERIFY FAILED {vok}/{vtot}: {verr}")
+    allv_v = comm.allgather_obj({"ok": vok, "tot": vtot, "err": verr})
     if rank == 0:
         T = max(v["elapsed"] for v in allv)
         mpix = world * nimg * W * H * args.steps / 1e6
@@ -312,6 +324,9 @@ def main():
             "stages_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()},
             "exact_rescored_crops_per_step": allv[0]["ncand"],
             "failed_images": sum(v["bad"] for v in allv),
+            "verified": (f"{sum(v['ok'] for v in allv_v)}/{sum(v['tot'] for v in allv_v)} images of the last "
+                         "timed batch vs the oracle (pixels +-1 LSB, crop box bit-exact on the GPU pixels)")
+                        if not args.no_verify else "skipped (--no-verify)",
         }
         # HBM traffic of the dominant kernel from the committed rocprofv3 PMC
         # passes (tools/gpu_profile.sh -> profiles/traffic_<workload>_<kernel>.json)
@@ -331,11 +346,14 @@ def main():
             except Exception as e:  # noqa: BLE001
                 result["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(result), flush=True)
+    verify_failed = any(v["err"] for v in allv_v)
     ctx.free(pool)
     for d in dsts:
         ctx.free(d)
     comm.close()
     ctx.close()
+    if verify_failed:
+        sys.exit(1)
 
 
 def run_cfg4(args, rank, world, local_rank, comm):
@@ -492,6 +510,7 @@ def run_cfg4(args, rank, world, local_rank, comm):
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cfg4_cpu_baseline(items)
         print(json.dumps(result), flush=True)
+    verify_failed = any(v["err"] for v in allv_v)
     ctx.free(pool)
     for d in dst:
         ctx.free(d)

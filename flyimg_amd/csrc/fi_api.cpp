@@ -73,8 +73,13 @@ int launch_mono(hipStream_t s, const MonoDesc *descs, int n, const double *wts);
 // streaming exact-integer MFMA resample (fi_vm.hip)
 size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16);
 int vm_read_stamps(uint64_t *out, int slots);
+int vp_read_stamps(uint64_t *out, int slots);
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
+// its persistent warp-specialised form (fi_vp.hip)
+VpLayout vp_lds_layout(int vpitch, bool q16);
+int launch_vp(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
+              const int32_t *nphase, int G, const int32_t *ai, VpLayout L);
 // streaming exact-integer MFMA resample, horizontal first (fi_hv.hip)
 size_t hv_lds_bytes(int pp, int nocb);
 int launch_hv(hipStream_t s, const HvDesc *descs, const HvStripD *strips, const HvTile *tiles, int ntiles,
@@ -215,6 +220,8 @@ struct fi_ctx {
   std::map<const AxisTable *, std::vector<StripTab>> strip_cache;
   bool fused = true;    // FI_DISABLE_FUSED=1 forces the generic two-pass resample
   bool vm_rs = true;     // FI_DISABLE_VM_RS=1: no k_rs_vm (streaming MFMA resample, the default)
+  bool vp_rs = false;    // FI_VP_RS=1: k_rs_vm's tiles run on the persistent k_rs_vp
+  int n_cu = 256;        // compute units (k_rs_vp: one persistent workgroup per CU)
   bool hv_rs = true;     // FI_DISABLE_HV_RS=1: horizontal-first geometries take the generic two-pass kernels
   bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
   bool sc_vq = true;        // FI_DISABLE_SC_VQ=1: k_sc_vmaps (VALU vertical pass) instead of k_sc_vq
@@ -1042,6 +1049,11 @@ struct BatchPlan {
   std::vector<MStrip> vstrips;
   std::vector<VTile> vtiles;
   size_t vm_lds = 0;
+  // k_rs_vp: persistent grid, per-workgroup piece counts, LDS layout (vp_G = 0: run k_rs_vm)
+  int vp_G = 0;
+  std::vector<int32_t> vp_nphase;
+  VpLayout vp_L{};
+  int vp_images = 0;
   std::vector<HvDesc> hdescs;
   std::vector<HvStripD> hstrips;
   std::vector<HvTile> htiles;
@@ -1049,7 +1061,7 @@ struct BatchPlan {
 };
 // Blob offsets and launch lists of a packed batch.
 struct Packed {
-  size_t all_rd_off = 0, vdesc_off = 0, vstrip_off = 0, vtile_off = 0, apply_off = 0, mono_off = 0;
+  size_t all_rd_off = 0, vdesc_off = 0, vstrip_off = 0, vtile_off = 0, vnph_off = 0, apply_off = 0, mono_off = 0;
   size_t hdesc_off = 0, hstrip_off = 0, htile_off = 0;
   size_t ai_off = 0, af_off = 0, ad_off = 0, mono_wts = 0;
   Launch L0, L1a, L2a, L2b, Q0, Q1a, Q2a, Q2b, CL[6];
@@ -1623,6 +1635,38 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   for (size_t i = 0; i < mx; i++)
     for (int x = 0; x < 8; x++)
       if (i < q8[x].size()) Bp.vtiles.push_back(q8[x][i]);
+  // k_rs_vp: one persistent workgroup per CU walks tiles g, g + G, ... (G a
+  // multiple of 8 keeps an image's strips on one XCD queue); it needs the
+  // launch's widest Q16 plane and output-tile kind to fit in LDS, and every
+  // image's row gaps x stride in 32 bits (the DMA's per-lane offset)
+  Bp.vp_G = 0;
+  if (c->vp_rs && !Bp.vtiles.empty()) {
+    int vpitch = 0;
+    bool q16 = false, ok = true;
+    for (const VTile &t : Bp.vtiles) {
+      vpitch = std::max(vpitch, Bp.vstrips[t.strip].vpitch);
+      const VDesc &d = Bp.vdescs[t.img];
+      q16 = q16 || d.gray || d.rot != 0;
+      ok = ok && t.p1 > t.p0;
+    }
+    for (const Work1 &w : work) {
+      const VDesc &d = Bp.vdescs[w.img];
+      const std::vector<int32_t> &rows = w.V->rows;
+      const int64_t gap = rows.size() > 1 ? (int64_t)(rows.back() - rows.front()) : 0;
+      ok = ok && gap * d.src_stride < ((int64_t)1 << 31);
+    }
+    const VpLayout L = vp_lds_layout(vpitch, q16);
+    if (ok && L.total <= kVpMaxLds) {
+      const int ntiles = (int)Bp.vtiles.size();
+      int G = std::min(ntiles, c->n_cu);
+      if (G > 8) G -= G % 8;
+      Bp.vp_G = G;
+      Bp.vp_L = L;
+      Bp.vp_nphase.assign(G, 0);
+      for (int t = 0; t < ntiles; t++) Bp.vp_nphase[t % G] += Bp.vtiles[t].p1 - Bp.vtiles[t].p0;
+      Bp.vp_images = (int)work.size();
+    }
+  }
 }
 
 // k_rs_hv workgroups: (image, strip, band of output blocks); bands only when
@@ -1738,6 +1782,7 @@ static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
   K.vdesc_off = B.addv(Bp.vdescs);
   K.vstrip_off = B.addv(Bp.vstrips);
   K.vtile_off = B.addv(Bp.vtiles);
+  K.vnph_off = B.addv(Bp.vp_nphase);
   K.hdesc_off = B.addv(Bp.hdescs);
   K.hstrip_off = B.addv(Bp.hstrips);
   K.htile_off = B.addv(Bp.htiles);
@@ -1800,9 +1845,15 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
     if (K.L0.tiles)
       hipLaunchKernelGGL(k_rs_copy, dim3(K.L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(K.L0),
                          pre_p(K.L0), K.L0.n);
-    if (!Bp.vtiles.empty() &&
-        launch_vm(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
-                  (const VTile *)(ab + K.vtile_off), (int)Bp.vtiles.size(), ai, Bp.vm_lds) != 0)
+    if (!Bp.vtiles.empty() && Bp.vp_G > 0) {
+      if (launch_vp(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
+                    (const VTile *)(ab + K.vtile_off), (int)Bp.vtiles.size(), (const int32_t *)(ab + K.vnph_off),
+                    Bp.vp_G, ai, Bp.vp_L) != 0)
+        return set_err(FI_EDEVICE, "persistent MFMA resample launch rejected (LDS %d)", Bp.vp_L.total);
+      c->stats["path_vp"].launches += Bp.vp_images;
+    } else if (!Bp.vtiles.empty() &&
+               launch_vm(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
+                         (const VTile *)(ab + K.vtile_off), (int)Bp.vtiles.size(), ai, Bp.vm_lds) != 0)
       return set_err(FI_EDEVICE, "streaming MFMA resample launch rejected (LDS %zu)", Bp.vm_lds);
     // (k_rs_hv on a stream of its own beside k_rs_vm was measured: cfg4 102.1
     // vs 102.5 ms/step -- k_rs_vm's LDS leaves no CU room to overlap into)
@@ -2299,6 +2350,12 @@ int fi_debug_vm_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   return vm_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
 }
+int fi_debug_vp_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
+  if (!c || !out) return FI_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return vp_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
+}
 // GPU JPEG decode (fi_jpeg.hip): the decode half of the host codec pipeline
 // (ImageProcessor's `convert` reads the source with libjpeg) on the device
 int fi_jpeg_info(const uint8_t *data, size_t len, int32_t *w, int32_t *h, int32_t *channels) {
@@ -2512,6 +2569,10 @@ int fi_create(fi_ctx **out, int32_t device) {
   c->device = device;
   if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
+  // k_rs_vp: opt-in (FI_VP_RS=1) until it is faster than k_rs_vm
+  c->vp_rs = false;
+  if (const char *e = getenv("FI_VP_RS")) c->vp_rs = e[0] == '1';
+  c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   if (const char *e = getenv("FI_DISABLE_HV_RS")) c->hv_rs = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
   if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');

@@ -207,6 +207,16 @@ constexpr int kVmOtilePitch = 64 * 3 + 4;      // Q16 output tile row, u16 units
 constexpr int kVmOtileBytes = 16 * kVmOtilePitch * 2;
 constexpr int kVmOtile8Pitch = 64 * 3 + 4;     // 8-bit tile row (fast RGB path)
 constexpr int kVmOtile8Bytes = 16 * kVmOtile8Pitch;
+// k_rs_vp (fi_vp.hip): the persistent, warp-specialised form of k_rs_vm (same
+// tables, bit-identical output); one 1024-thread workgroup per CU.  LDS
+// layout from vp_lds_layout (Q16-plane stride and output-tile kind of the launch).
+struct VpLayout {
+  int32_t plane;        // bytes of one limb plane of one channel (16 vpitch + pad)
+  int32_t otile_off;    // output tiles [2][otile_bytes]
+  int32_t otile_bytes;
+  int32_t total;        // dynamic LDS of the launch
+};
+constexpr int kVpMaxLds = 160 * 1024;
 
 // k_rs_hv (fi_hv.hip): streaming exact-integer MFMA resample, horizontal first
 // (fi_plan.h HvH / HvV).

@@ -25,8 +25,9 @@ struct JpegHdr {
 // FI_EINVAL for malformed data
 int jpeg_parse(const uint8_t *d, size_t n, JpegHdr *o);
 // jdhuff.c jpeg_make_d_derived_tbl (+ the fast-AC entries); false when the
-// code lengths are over-subscribed or the value count does not match
-bool jpeg_build_huff(const std::string &dht, JpegHuff *t);
+// code lengths are over-subscribed, the value count does not match, or (dc) a
+// DC symbol exceeds 15 -- the tables libjpeg rejects with JERR_BAD_HUFF_TABLE
+bool jpeg_build_huff(const std::string &dht, bool dc, JpegHuff *t);
 // dimensions and output channels of a stream the GPU decoder takes
 int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c);
 

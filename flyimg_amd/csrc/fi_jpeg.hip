@@ -514,14 +514,15 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
     for (int t = 0; t < 4; t++) {
       D.ht[t] = -1;
       if (H.dht[t].empty()) continue;
-      auto it = huff_ix.find(H.dht[t]);
+      const std::string key = std::string(1, t < 2 ? 'D' : 'A') + H.dht[t];  // class + table bytes
+      auto it = huff_ix.find(key);
       if (it == huff_ix.end()) {
         JpegHuff hf;
-        if (!jpeg_build_huff(H.dht[t], &hf)) {
+        if (!jpeg_build_huff(H.dht[t], t < 2, &hf)) {
           status[i] = FI_EINVAL;
           break;
         }
-        it = huff_ix.emplace(H.dht[t], (int)huffs.size()).first;
+        it = huff_ix.emplace(key, (int)huffs.size()).first;
         huffs.push_back(hf);
       }
       D.ht[t] = it->second;

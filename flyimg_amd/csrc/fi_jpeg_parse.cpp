@@ -19,6 +19,10 @@ int jpeg_parse(const uint8_t *d, size_t n, JpegHdr *o) {
                                  58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
   size_t p = 2;
   bool sof = false;
+  // jdmarker.c examine_app0 / examine_app14: what default_decompress_parms
+  // (jdapimin.c) reads to pick the colour space of a 3-component stream
+  bool jfif = false, adobe = false;
+  int adobe_transform = 0;
   while (p + 4 <= n) {
     if (d[p] != 0xFF) return FI_EINVAL;
     const int m = d[p + 1];
@@ -85,7 +89,7 @@ int jpeg_parse(const uint8_t *d, size_t n, JpegHdr *o) {
         o->restart = be16(s);
         break;
       case 0xDA: {  // SOS: the one scan, then the entropy-coded data up to EOI
-        if (!sof) return FI_EINVAL;
+        if (!sof || L < 3) return FI_EINVAL;
         const int ns = s[0];
         if (ns != o->ncomp || L != 6 + 2 * (size_t)ns) return FI_EUNSUPPORTED;  // one interleaved scan
         for (int k = 0; k < ns; k++) {
@@ -119,6 +123,18 @@ int jpeg_parse(const uint8_t *d, size_t n, JpegHdr *o) {
           break;
         }
         o->ecs1 = q;
+        // the scan must end at EOI: a truncated stream (no marker before the
+        // end of the data) or one with markers after the scan goes to the host
+        // decoder, which reports truncation as libjpeg / Pillow do
+        if (q + 1 >= n || d[q + 1] != 0xD9) return FI_EUNSUPPORTED;
+        // libjpeg decodes a 3-component stream as RGB (no colour conversion) when
+        // it has no JFIF marker and either an Adobe marker with transform 0 or,
+        // with no Adobe marker, the component ids 'R', 'G', 'B'; the GPU path
+        // converts YCbCr only
+        if (o->ncomp == 3 && !jfif) {
+          if (adobe && adobe_transform == 0) return FI_EUNSUPPORTED;
+          if (!adobe && o->id[0] == 82 && o->id[1] == 71 && o->id[2] == 66) return FI_EUNSUPPORTED;
+        }
         for (int c = 0; c < o->ncomp; c++) {
           if (!o->qt_ok[o->tq[c]] || o->dht[o->td[c]].empty() || o->dht[2 + o->ta[c]].empty()) return FI_EINVAL;
         }
@@ -132,8 +148,14 @@ int jpeg_parse(const uint8_t *d, size_t n, JpegHdr *o) {
         }
         return 0;
       }
-      case 0xEE:  // APP14 "Adobe": a transform flag other than YCbCr is unsupported
-        if (L >= 14 && memcmp(s, "Adobe", 5) == 0 && o->ncomp == 3 && s[11] != 1) return FI_EUNSUPPORTED;
+      case 0xE0:  // APP0 "JFIF\0" (examine_app0: at least 14 data bytes)
+        if (L >= 16 && memcmp(s, "JFIF\0", 5) == 0) jfif = true;
+        break;
+      case 0xEE:  // APP14 "Adobe" (examine_app14: at least 12 data bytes); it may precede SOF
+        if (L >= 14 && memcmp(s, "Adobe", 5) == 0) {
+          adobe = true;
+          adobe_transform = s[11];
+        }
         break;
       default:
         break;  // APPn, COM, ...
@@ -145,14 +167,26 @@ int jpeg_parse(const uint8_t *d, size_t n, JpegHdr *o) {
 
 // jdhuff.c jpeg_make_d_derived_tbl: canonical codes, maxcode / valoffset,
 // 9-bit lookahead
-bool jpeg_build_huff(const std::string &dht, JpegHuff *t) {
+bool jpeg_build_huff(const std::string &dht, bool dc, JpegHuff *t) {
   memset(t, 0, sizeof(*t));
+  if (dht.size() < 16 || dht.size() > 16 + 256) return false;
   const uint8_t *bits = (const uint8_t *)dht.data();
   const int nv = (int)dht.size() - 16;
+  int cnt = 0;
+  for (int l = 0; l < 16; l++) cnt += bits[l];
+  if (cnt != nv) return false;
   memcpy(t->huffval, bits + 16, nv);
+  // jdhuff.c: DC symbols are coefficient sizes, 0..15 (JERR_BAD_HUFF_TABLE)
+  if (dc)
+    for (int k = 0; k < nv; k++)
+      if (t->huffval[k] > 15) return false;
   int p = 0;
   uint32_t code = 0;
   for (int l = 1; l <= 16; l++) {
+    // jdhuff.c: the codes of length l, and the next code after them, must fit
+    // in l bits (no code is all ones); checked before any lookahead entry is
+    // written, so an over-subscribed table never writes past look[]
+    if ((uint64_t)code + bits[l - 1] >= ((uint64_t)1 << l)) return false;
     if (bits[l - 1]) {
       t->valoff[l] = p - (int)code;
       for (int i = 0; i < bits[l - 1]; i++, p++, code++) {
@@ -162,7 +196,6 @@ bool jpeg_build_huff(const std::string &dht, JpegHuff *t) {
         }
       }
       t->maxcode[l] = (int32_t)code - 1;
-      if (code > (1u << l)) return false;  // over-subscribed
     } else {
       t->maxcode[l] = -1;
     }
@@ -191,7 +224,7 @@ int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c) {
   if (rc) return rc;
   for (int t = 0; t < 4; t++) {  // the Huffman tables must build (jdhuff.c rejects bad ones too)
     JpegHuff hf;
-    if (!hd.dht[t].empty() && !jpeg_build_huff(hd.dht[t], &hf)) return FI_EINVAL;
+    if (!hd.dht[t].empty() && !jpeg_build_huff(hd.dht[t], t < 2, &hf)) return FI_EINVAL;
   }
   *w = hd.W;
   *h = hd.H;

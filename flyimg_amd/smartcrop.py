@@ -104,9 +104,10 @@ def main(argv=None) -> int:
     options = parse_argument(argv)
     image = PIL.Image.open(options.inputfile)
     if image.mode not in ("RGB", "RGBA"):
-        # the same note on stderr, without a newline (smartcrop.py:357-362);
-        # SmartCropProcessor runs the command with 2>&1
-        sys.stderr.write("{1} convert from mode='{0}' to mode='RGB' ".format(image.mode, options.inputfile))
+        # the reference prints "<path> convert from mode='L' to mode='RGB' " here
+        # (smartcrop.py:357-362, no newline); SmartCropProcessor.php:24-29 runs the
+        # command with 2>&1 and reads output[0] as the -crop geometry, so the note
+        # would corrupt it.  Deliberately not reproduced: nothing on stderr.
         new_image = PIL.Image.new("RGB", image.size)
         new_image.paste(image)
         image = new_image

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Per-phase cycle sums of k_rs_vp (FI_VP_VARIANT=9 stamps, s_memtime ticks)
+on a full cfg2 batch, averaged over the persistent workgroups.
+V wave 0: tile entry, vertical MFMA issue, block done (planes), barrier.
+H wave 8: LUT staging, record / fragment reload, horizontal pass, stores, barrier.
+L wave 14: A-record DMA issue, piece DMA issue, vmcnt wait, barrier."""
+import ctypes
+import os
+import sys
+
+os.environ["FI_VP_VARIANT"] = "9"
+os.environ["FI_VP_RS"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from flyimg_amd import _lib as L  # noqa: E402
+from flyimg_amd.processor import ImageProcessor, OptionsBag  # noqa: E402
+from flyimg_amd.runtime import Context  # noqa: E402
+from flyimg_amd.runtime import plan as fi_plan  # noqa: E402
+
+W, H, n = 1920, 1080, int(os.environ.get("NIMG", "1024"))
+op = ImageProcessor(OptionsBag(os.environ.get("VP_OPTS", "w_500")), W, H).to_op()
+stride = (W * 3 + 15) // 16 * 16
+ow, oh, oc = fi_plan(W, H, op)
+cap = ow * oh * oc
+with Context(0) as ctx:
+    pool = ctx.malloc(stride * H * n)
+    dst = ctx.malloc(cap * n)
+    for i in range(n):
+        ctx.fill_synthetic(pool + i * stride * H, W, H, stride, 7 + i)
+    arr = (L.FiImage * n)()
+    for i in range(n):
+        a = arr[i]
+        a.src, a.src_w, a.src_h, a.src_stride, a.src_channels = pool + i * stride * H, W, H, stride, 3
+        a.target_w, a.target_h, a.flags, a.gravity = op.target_w, op.target_h, op.flags, op.gravity
+        a.dst, a.dst_capacity = dst + i * cap, cap
+    for _ in range(3):
+        L.check(ctx.process_device(arr, n))
+    NS = 16
+    buf = np.zeros(1024 * NS, np.uint64)
+    L.lib().fi_debug_vp_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
+    L.check(L.lib().fi_debug_vp_stamps(ctx.h, buf.ctypes.data, 1024))
+    rows = np.array([r for r in buf.reshape(1024, NS) if r[NS - 1] > 0], dtype=np.float64)
+    ph = rows[:, NS - 1].mean()
+    for name, base, names in (("V wave 0", 0, ["tile entry", "V-MFMA issue", "planes", "barrier"]),
+                              ("H wave 8", 5, ["LUT staging", "rec+frags", "horizontal", "stores", "barrier"]),
+                              ("L wave 14", 10, ["A DMA", "piece DMA", "vmcnt wait", "barrier"])):
+        a = rows[:, base:base + len(names)]
+        tot = a.sum(axis=1).mean()
+        print(f"{name}: {len(rows)} workgroups, phases/WG {ph:.0f}, ticks/WG {tot:.0f}, per phase {tot / ph:.0f}")
+        for k, nm in enumerate(names):
+            print(f"  {nm:14s} {a[:, k].mean() / ph:8.0f} per phase ({a[:, k].mean() / tot * 100:5.1f} %)")
