@@ -1557,6 +1557,7 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
         align4();
         o[1] = put(H.frag);
         o[2] = put(H.s0);
+        align4();  // 16-byte aligned LUT rows (k_rs_vp's LDS-DMA)
         o[3] = put(H.lut);
         ht = c->mh_at.emplace(&H, o).first;
       }

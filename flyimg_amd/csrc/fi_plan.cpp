@@ -446,6 +446,10 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
     int x1 = x0 + 1, b0;
     if (bytes_of(x0, x1, &b0) > kMfmaStripBytes) return false;
     while (x1 < nx && x1 - x0 < max_nx && bytes_of(x0, x1 + 1, &b0) <= kMfmaStripBytes) x1++;
+    // strips end on multiples of 4 px (the last one at nx): every strip's output
+    // segment then starts 12-byte aligned in its row, so with a dword-aligned
+    // destination row the stores are whole dwords / 8-byte units, no byte stores
+    if (x1 < nx && (x1 & ~3) > x0) x1 &= ~3;
     MfmaStrip S{};
     S.x0 = x0;
     S.x1 = x1;
@@ -483,6 +487,7 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
       if (px >= h.src_lo && px < h.src_hi && idx[px - h.src_lo] >= 0) ci = idx[px - h.src_lo] - S.c_lo;
       m->lut.push_back(ci >= 0 && ci < S.ncols ? ci : -1);
     }
+    while (m->lut.size() % 4) m->lut.push_back(-1);  // 16-byte rows: k_rs_vp stages the LUT by LDS-DMA
     S.frag = m->frag.size();
     m->frag.resize(m->frag.size() + (size_t)S.nocb * S.ks * 3 * 256, 0);
     for (int ob = 0; ob < S.nocb; ob++)

@@ -36,17 +36,18 @@ with Context(0) as ctx:
         a.dst, a.dst_capacity = dst + i * cap, cap
     for _ in range(3):
         L.check(ctx.process_device(arr, n))
-    NS = 16
-    buf = np.zeros(1024 * NS, np.uint64)
+    NS = 16 * 6
+    buf = np.zeros(256 * NS, np.uint64)
     L.lib().fi_debug_vp_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
-    L.check(L.lib().fi_debug_vp_stamps(ctx.h, buf.ctypes.data, 1024))
-    rows = np.array([r for r in buf.reshape(1024, NS) if r[NS - 1] > 0], dtype=np.float64)
-    ph = rows[:, NS - 1].mean()
-    for name, base, names in (("V wave 0", 0, ["tile entry", "V-MFMA issue", "planes", "barrier"]),
-                              ("H wave 8", 5, ["LUT staging", "rec+frags", "horizontal", "stores", "barrier"]),
-                              ("L wave 14", 10, ["A DMA", "piece DMA", "vmcnt wait", "barrier"])):
-        a = rows[:, base:base + len(names)]
-        tot = a.sum(axis=1).mean()
-        print(f"{name}: {len(rows)} workgroups, phases/WG {ph:.0f}, ticks/WG {tot:.0f}, per phase {tot / ph:.0f}")
-        for k, nm in enumerate(names):
-            print(f"  {nm:14s} {a[:, k].mean() / ph:8.0f} per phase ({a[:, k].mean() / tot * 100:5.1f} %)")
+    L.check(L.lib().fi_debug_vp_stamps(ctx.h, buf.ctypes.data, 256))
+    a = buf.reshape(256, 16, 6).astype(np.float64)
+    a = a[a[:, 0, 5] > 0]
+    ph = a[:, 0, 5].mean()
+    roles = {"V": (range(0, 8), ["tile entry", "V-MFMA issue", "planes", "barrier"]),
+             "H": (range(8, 14), ["-", "rec+frags", "horizontal", "stores", "barrier"]),
+             "L": (range(14, 16), ["stores+A DMA", "piece DMA", "vmcnt wait", "barrier"])}
+    print(f"{len(a)} workgroups, phases/WG {ph:.0f}; per-phase ticks by wave (mean over workgroups)")
+    for r, (waves, names) in roles.items():
+        for w in waves:
+            v = a[:, w, :len(names)].mean(axis=0) / ph
+            print(f"  {r} wave {w:2d}: work {v[:-1].sum():7.0f} | " + "  ".join(f"{n} {x:6.0f}" for n, x in zip(names, v)))
