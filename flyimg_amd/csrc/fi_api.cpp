@@ -1936,6 +1936,10 @@ static int queue_readback(fi_ctx *c, BatchPlan &Bp, int slot, uint8_t *wb, doubl
   if (host) {
     // outputs to the host, behind the batch's last kernel on sc_stream: the
     // planned (pre-apply) bytes cover the applied crop, which is never larger
+    double obytes = 0;
+    for (int i = 0; i < Bp.n; i++)
+      if (Bp.status[i] == FI_OK && host->user[i].dst) obytes += (double)Bp.imgs[i].out_stride * Bp.imgs[i].out_h;
+    Timer t(c, "d2h_out", obytes, c->rb_stream, c->rb_stream);
     for (int i = 0; i < Bp.n; i++) {
       const fi_image &d = Bp.imgs[i];
       if (Bp.status[i] != FI_OK || !host->user[i].dst) continue;
@@ -2794,6 +2798,13 @@ static int submit_host(fi_ctx *c, fi_image *imgs, int32_t n) {
   rc = ensure_pinned_buf(&S.hpin, &S.hpin_cap, pin_total + 256);
   if (rc) return rc;
   uint8_t *io = (uint8_t *)S.hio.p;
+  double sbytes = 0;
+  for (int i = 0; i < n; i++)
+    if (imgs[i].src && imgs[i].src_w > 0 && imgs[i].src_h > 0)
+      sbytes += (double)imgs[i].src_w * imgs[i].src_channels * imgs[i].src_h;
+  {
+  const double t_pack = now_ms();
+  Timer t(c, "h2d_src", sbytes, c->up_stream, c->up_stream);
   for (int i = 0; i < n; i++) {
     const fi_image &im = imgs[i];
     fi_image &d = host->dev[i];
@@ -2816,6 +2827,8 @@ static int submit_host(fi_ctx *c, fi_image *imgs, int32_t n) {
     HIP_TRY(hipMemcpy2DAsync(io + soff[i], d.src_stride, from, from_stride, row, im.src_h, hipMemcpyHostToDevice,
                              c->up_stream));
     d.src = io + soff[i];
+  }
+  host_stat(c, "host_src_stage", now_ms() - t_pack);  // pageable rows packed into pinned staging + copy issue
   }
   return run_batch(c, host->dev.data(), n, true, host);
 }

@@ -18,6 +18,8 @@ for v in ${VP_RUNS:-vp vm a1 a2 vp}; do
     a2) e="FI_VP_RS=1 FI_VP_VARIANT=2" ;;
     a3) e="FI_VP_RS=1 FI_VP_VARIANT=3" ;;
     a4) e="FI_VP_RS=1 FI_VP_VARIANT=4" ;;
+    a5) e="FI_VP_RS=1 FI_VP_VARIANT=5" ;;
+    a6) e="FI_VP_RS=1 FI_VP_VARIANT=6" ;;
   esac
   nv=""; case $v in a*) nv="--no-verify" ;; esac
   env $e timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline $nv ${BENCH_ARGS:-} > $OUT/$v.json 2> $OUT/$v.err || { echo "bench $v rc $?"; tail -5 $OUT/$v.err; exit 3; }
