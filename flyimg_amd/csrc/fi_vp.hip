@@ -152,13 +152,16 @@ static_assert(kVW + kHW + kLW == 16, "16 waves");
 
 // MODE (profiling ablations, FI_VP_VARIANT; wrong pixels): 0 production,
 // 1 DMA stream only, 2 no H role (vertical pass + planes only), 3 no stores,
-// 4 H waves take one horizontal item each (the rest skipped), 9 production +
+// 4 H waves take one horizontal item each (the rest skipped), 5 V waves skip
+// their piece reads, 6 H waves skip their plane reads, 7 V waves skip the MFMAs, 8 H role idle
+// (stores kept), 9 H without its epilogue, 20 L prio 3 / H prio 0, 21 H prio 0, 9 production +
 // per-phase s_memtime sums of V wave 0, H wave 8, L wave 14.
 template <int MODE>
 __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ descs, const MStrip *__restrict__ strips,
                                                    const VTile *__restrict__ tiles, int ntiles,
                                                    const int32_t *__restrict__ nphase, const int32_t *__restrict__ ai,
                                                    VpLayout Lo) {
+  constexpr int M = MODE >= 10 ? MODE - 10 : MODE;  // 10 + k: ablation k with the MODE 9 stamps
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = ufl(tid >> 6);
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
   uint8_t *planes = lds + kPlanesOff;                           // [2][6][plane]
   uint8_t *otiles = lds + Lo.otile_off;                         // [2][otile_bytes]
   const int plane = Lo.plane;
-  constexpr bool kStamp = MODE == 9;
+  constexpr bool kStamp = MODE == 9 || MODE >= 10;
   uint64_t tsum[5] = {}, tprev = 0;
   auto stamp = [&](int k) {
     if (kStamp) {
@@ -316,11 +319,14 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
     };
     // the loader's few instructions go first on its SIMD: a starved loader
     // starves the whole pipeline
-    __builtin_amdgcn_s_setprio(2);
+    if (M == 20)
+      __builtin_amdgcn_s_setprio(3);
+    else
+      __builtin_amdgcn_s_setprio(2);
     PI P1{};
     if (N > 0) {
       const PI P0 = issue(0, 0);
-      if (MODE != 1) issue_a(P0, 0);
+      if (M != 1) issue_a(P0, 0);
     }
     if (N > 1) P1 = issue(1, 1);
     if (N > 1)
@@ -350,7 +356,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
       int64_t st_stride = 0;
       int st_nb = 0, st_nrow = 0;
       const uint8_t *st_ot = nullptr;
-      if (p >= 2 && p - 2 < N && MODE != 3 && MODE != 1 && MODE != 2) {
+      if (p >= 2 && p - 2 < N && M != 3 && M != 1 && M != 2) {
         const Rec rs = read_rec(p - 2);
         if (rs.flags & kEmit) {
           if (stile != rs.t) {
@@ -456,7 +462,19 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
           }
         }
       }
-      if (MODE != 1 && p + 1 < N) issue_a(P1, (p + 1) & 1);
+      if (M == 22 && st_fast) {  // ablation: the fast stores at the top of the phase
+        const int U = st_nb >> 2;
+        const float invU = 1.0f / (float)U;
+        for (int it0 = 0; it0 < st_nrow * U; it0 += 64) {
+          const int it = it0 + lane;
+          if (it < st_nrow * U) {
+            const int r = (int)(((float)it + 0.5f) * invU), u = it - r * U;
+            *(g_u32 *)(st_row0 + r * st_stride + 4 * u) =
+                *reinterpret_cast<const uint32_t *>(st_ot + r * kLW * kOt8Pitch + 4 * u);
+          }
+        }
+      }
+      if (M != 1 && p + 1 < N) issue_a(P1, (p + 1) & 1);
       stamp(0);
       const bool more = p + 2 < N;
       PI P2{};
@@ -465,7 +483,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
       // dword-aligned fast8 stores of block p - 2: this wave's rows li, li + 2, ...
       // as dwords (lane -> row, dword), ns = store instructions issued
       int ns = 0;
-      if (st_fast) {
+      if (st_fast && M != 22) {
         const int U = st_nb >> 2;
         const float invU = 1.0f / (float)U;
         for (int it0 = 0; it0 < st_nrow * U; it0 += 64, ns++) {
@@ -533,7 +551,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
     Rec rC = N > 0 ? read_rec(0) : Rec{};
     if (kStamp) tprev = __builtin_amdgcn_s_memtime();
     for (int p = 0; p < N + 2; p++) {
-      if (p < N && MODE != 1) {
+      if (p < N && M != 1) {
         const Rec C = rC;
         const uint8_t *sp = lds + rslot * kPieceBytes;
         const i32x4 *al = reinterpret_cast<const i32x4 *>(lds + kAOff + (p & 1) * kABytes);
@@ -571,16 +589,17 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
 #pragma unroll
           for (int jj = 0; jj < 4; jj++) {
             const int o = offA0 + 16 * ((4 * hf + jj) ^ fA7);
-            const i32x2 lo = tr8(sp + o), hi = tr8(sp + o + 8 * 512);
+            const i32x2 lo = M == 5 ? i32x2{lane ^ p, o} : tr8(sp + o), hi = M == 5 ? i32x2{o, lane + jj} : tr8(sp + o + 8 * 512);
             B[jj] = i32x4{lo.x, lo.y, hi.x, hi.y} ^
                     i32x4{(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
           }
 #pragma unroll
-          for (int jj = 0; jj < 4; jj++) d[jj] = mfma(A[2], B[jj], i32x4{0, 0, 0, 0});
+          for (int jj = 0; jj < 4; jj++) d[jj] = M == 7 ? (A[2] ^ B[jj]) : mfma(A[2], B[jj], i32x4{0, 0, 0, 0});
 #pragma unroll
-          for (int jj = 0; jj < 4; jj++) d[jj] = mfma(A[1], B[jj], d[jj] << 8);
+          for (int jj = 0; jj < 4; jj++) d[jj] = M == 7 ? (A[1] + B[jj] + (d[jj] << 8)) : mfma(A[1], B[jj], d[jj] << 8);
 #pragma unroll
-          for (int jj = 0; jj < 4; jj++) acc[4 * hf + jj] = mfma(A[0], B[jj], acc[4 * hf + jj]) + (d[jj] << 8);
+          for (int jj = 0; jj < 4; jj++)
+            acc[4 * hf + jj] = (M == 7 ? (A[0] + B[jj] + acc[4 * hf + jj]) : mfma(A[0], B[jj], acc[4 * hf + jj])) + (d[jj] << 8);
         }
         stamp(1);
         if (C.flags & kLast) {
@@ -636,13 +655,13 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
 
   // the horizontal pass of the previous block is the longest chain of a phase:
   // it issues ahead of the vertical waves (the loader still goes first)
-  __builtin_amdgcn_s_setprio(1);
+  if (M != 20 && M != 21) __builtin_amdgcn_s_setprio(1);
   phase_barrier();
   phase_barrier();
   Rec rH{};  // record of the block this phase's horizontal pass takes (piece p - 1), read a phase early
   if (kStamp) tprev = __builtin_amdgcn_s_memtime();
   for (int p = 0; p < N + 2; p++) {
-    if (MODE != 1 && MODE != 2) {
+    if (M != 1 && M != 2 && M != 18) {
       stamp(0);
       // horizontal pass of the block completed in phase p - 1
       if (p >= 1 && p - 1 < N) {
@@ -687,7 +706,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
 #pragma unroll
           for (int k = 0; k < 2; k++) {
             const int it = hw + kHW * k;
-            if (it >= h_items || (MODE == 4 && k > 0)) break;
+            if (it >= h_items || (M == 4 && k > 0)) break;
             const int ob = it / 3, chn = it - 3 * ob;
             const int hw0 = hw0k[k], hks = hksk[k];
             i32x4 hh[3], hl[3];
@@ -699,8 +718,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
               if (t >= hks) break;
               const int cA = hw0 + 64 * t + 16 * (lane >> 4) + ((lane & 15) >> 1);
               const int o0 = col_off(cA) + 8 * (lane & 1), o1 = col_off(cA + 8) + 8 * (lane & 1);
-              const i32x2 h0 = tr8(ph + o0), h1 = tr8(ph + o1);
-              const i32x2 l0 = tr8(pl + o0), l1 = tr8(pl + o1);
+              const i32x2 h0 = M == 6 ? i32x2{lane, o0} : tr8(ph + o0), h1 = M == 6 ? i32x2{o1, lane} : tr8(ph + o1);
+              const i32x2 l0 = M == 6 ? i32x2{lane ^ o1, b} : tr8(pl + o0), l1 = M == 6 ? i32x2{b, o0} : tr8(pl + o1);
               const i32x4 Ah = {h0.x, h0.y, h1.x, h1.y}, Al = {l0.x, l0.y, l1.x, l1.y};
 #pragma unroll
               for (int q = 0; q < 3; q++) {
@@ -709,7 +728,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vp(const VDesc *__restrict__ des
               }
             }
             const int hx = 16 * ob + (lane & 15);
-            if (hx < nx) {
+            if (hx < nx && M != 19) {
               const float hws = hwsk[k];
 #pragma unroll
               for (int i = 0; i < 4; i++) {
@@ -770,6 +789,28 @@ int launch_vp(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTi
     hipLaunchKernelGGL((k_rs_vp<3>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
   else if (v == 4)
     hipLaunchKernelGGL((k_rs_vp<4>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 15)
+    hipLaunchKernelGGL((k_rs_vp<15>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 16)
+    hipLaunchKernelGGL((k_rs_vp<16>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 17)
+    hipLaunchKernelGGL((k_rs_vp<17>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 28)
+    hipLaunchKernelGGL((k_rs_vp<28>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 29)
+    hipLaunchKernelGGL((k_rs_vp<29>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 30)
+    hipLaunchKernelGGL((k_rs_vp<30>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 31)
+    hipLaunchKernelGGL((k_rs_vp<31>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 13)
+    hipLaunchKernelGGL((k_rs_vp<13>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 32)
+    hipLaunchKernelGGL((k_rs_vp<32>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 11)
+    hipLaunchKernelGGL((k_rs_vp<11>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
+  else if (v == 12)
+    hipLaunchKernelGGL((k_rs_vp<12>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
   else if (v == 9)
     hipLaunchKernelGGL((k_rs_vp<9>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, nphase, ai, L);
   else

@@ -8,7 +8,7 @@ import ctypes
 import os
 import sys
 
-os.environ["FI_VP_VARIANT"] = "9"
+os.environ["FI_VP_VARIANT"] = os.environ.get("VP_STAMP_VARIANT", "9")
 os.environ["FI_VP_RS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
