@@ -78,6 +78,10 @@ int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTi
               const int32_t *ai, size_t lds);
 // its persistent warp-specialised form (fi_vp.hip)
 VpLayout vp_lds_layout(int vpitch, bool q16);
+VrLayout vr_lds_layout(int vpitch, bool q16);
+int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrTile *tiles, int ntiles,
+              const int32_t *wginfo, int G, const int32_t *ai, VrLayout L);
+int vr_read_stamps(uint64_t *out, int slots);
 int launch_vp(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *nphase, int G, const int32_t *ai, VpLayout L);
 // streaming exact-integer MFMA resample, horizontal first (fi_hv.hip)
@@ -221,6 +225,7 @@ struct fi_ctx {
   bool fused = true;    // FI_DISABLE_FUSED=1 forces the generic two-pass resample
   bool vm_rs = true;     // FI_DISABLE_VM_RS=1: no k_rs_vm (streaming MFMA resample, the default)
   bool vp_rs = false;    // FI_VP_RS=1: k_rs_vm's tiles run on the persistent k_rs_vp
+  bool vr_rs = false;    // FI_VR_RS=1: images with block-major tables take the persistent k_rs_vr
   int n_cu = 256;        // compute units (k_rs_vp: one persistent workgroup per CU)
   bool hv_rs = true;     // FI_DISABLE_HV_RS=1: horizontal-first geometries take the generic two-pass kernels
   bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
@@ -233,6 +238,7 @@ struct fi_ctx {
   size_t jpeg_host_cap = 0;
   std::string skinsat_key;
   std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
+  std::map<const AxisTable *, VrV> vrv_cache;   // ok iff nblk > 0
   std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
   std::map<const AxisTable *, HvV> hvv_cache;  // ok iff nblk > 0
   std::map<const AxisTable *, HvH> hvh_cache;  // ok iff !strips.empty()
@@ -260,6 +266,7 @@ struct fi_ctx {
   std::map<const RingTable *, std::array<int32_t, 4>> ring_at;
   std::map<const StripTab *, std::pair<int32_t, int32_t>> strip_at;
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
+  std::map<const VrV *, std::array<int32_t, 4>> vr_at;    // rows, bmeta, w128, frag
   std::map<const MfmaH *, std::array<int32_t, 4>> mh_at;  // wsum, frag, s0, lut
   std::map<const HvV *, std::array<int32_t, 3>> hvv_at;   // k0ks, frag, wsum
   std::map<const HvH *, std::array<int32_t, 3>> hvh_at;   // w128, frag, s0
@@ -461,6 +468,7 @@ static void heap_reset(fi_ctx *c) {
   c->ring_at.clear();
   c->strip_at.clear();
   c->vv_at.clear();
+  c->vr_at.clear();
   c->mh_at.clear();
   c->hvv_at.clear();
   c->hvh_at.clear();
@@ -477,6 +485,7 @@ static int heap_prepare(fi_ctx *c, Exec &E) {
     c->ring_cache.clear();
     c->strip_cache.clear();
     c->vmv_cache.clear();
+    c->vrv_cache.clear();
     c->vmh_cache.clear();
     c->hvv_cache.clear();
     c->hvh_cache.clear();
@@ -1023,6 +1032,7 @@ struct BatchPlan {
   std::vector<int> vm_img;
   std::vector<const VmV *> vm_v;
   std::vector<const MfmaH *> vm_h;
+  std::vector<const AxisTable *> vm_vt;  // their vertical axes (k_rs_vr tables)
   std::vector<int> hv_img;
   std::vector<const HvV *> hv_v;
   std::vector<const HvH *> hv_h;
@@ -1048,6 +1058,11 @@ struct BatchPlan {
   std::vector<VDesc> vdescs;
   std::vector<MStrip> vstrips;
   std::vector<VTile> vtiles;
+  // k_rs_vr: persistent block-major tiles, per-workgroup {phases, stream rows}, LDS layout
+  std::vector<VrTile> vrtiles;
+  std::vector<int32_t> vr_info;
+  int vr_G = 0, vr_images = 0;
+  VrLayout vr_L{};
   size_t vm_lds = 0;
   // k_rs_vp: persistent grid, per-workgroup piece counts, LDS layout (vp_G = 0: run k_rs_vm)
   int vp_G = 0;
@@ -1062,6 +1077,7 @@ struct BatchPlan {
 // Blob offsets and launch lists of a packed batch.
 struct Packed {
   size_t all_rd_off = 0, vdesc_off = 0, vstrip_off = 0, vtile_off = 0, vnph_off = 0, apply_off = 0, mono_off = 0;
+  size_t vrtile_off = 0, vrinfo_off = 0;
   size_t hdesc_off = 0, hstrip_off = 0, htile_off = 0;
   size_t ai_off = 0, af_off = 0, ad_off = 0, mono_wts = 0;
   Launch L0, L1a, L2a, L2b, Q0, Q1a, Q2a, Q2b, CL[6];
@@ -1127,6 +1143,7 @@ static int64_t plan_resample(fi_ctx *c, Exec &E, BatchPlan &Bp, const ImPlan &P,
       Bp.vm_img.push_back((int)Bp.rd.size());
       Bp.vm_v.push_back(&vit->second);
       Bp.vm_h.push_back(hh);
+      Bp.vm_vt.push_back(vt);
       return strip_bytes;
     }
   }
@@ -1502,6 +1519,117 @@ static void build_fused_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   }
 }
 
+// k_rs_vr: images (their k_rs_vm VDesc, strips) with block-major tables.
+struct VrWork {
+  int32_t img, first_strip, nstrips;
+  const VrV *V;
+};
+// k_rs_vr workgroups: tiles (image, strip, band of blocks) in the XCD-aware
+// order of k_rs_vm, dealt round-robin to one persistent workgroup per CU; the
+// tiles of a workgroup form its row stream.  False (nothing launched) when the
+// ring does not fit LDS or a stream needs more rows resident than the ring has.
+static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<VrWork> &work) {
+  auto align4 = [&]() {
+    while (E.ai.size() % 4) E.ai.push_back(0);
+  };
+  auto put = [&](const std::vector<int32_t> &v) {
+    const int32_t o = E.oi();
+    E.ai.insert(E.ai.end(), v.begin(), v.end());
+    return o;
+  };
+  int vpitch = 0;
+  bool q16 = false;
+  int64_t nst = 0;
+  for (const VrWork &w : work) {
+    for (int st = 0; st < w.nstrips; st++) vpitch = std::max(vpitch, Bp.vstrips[w.first_strip + st].vpitch);
+    const VDesc &d = Bp.vdescs[w.img];
+    q16 = q16 || d.gray || d.rot != 0;
+    nst += w.nstrips;
+  }
+  const VrLayout L = vr_lds_layout(vpitch, q16);
+  if (L.R <= 0) return false;
+  // per image: a VDesc with the block-major tables
+  std::vector<int32_t> desc_of(work.size());
+  for (size_t k = 0; k < work.size(); k++) {
+    const VrV &V = *work[k].V;
+    auto vp = c->vr_at.find(&V);
+    if (vp == c->vr_at.end()) {
+      std::array<int32_t, 4> o;
+      o[0] = put(V.rows);
+      align4();
+      o[1] = put(V.bmeta);
+      o[2] = put(V.w128);
+      align4();
+      o[3] = put(V.frag);
+      vp = c->vr_at.emplace(&V, o).first;
+    }
+    VDesc m = Bp.vdescs[work[k].img];
+    m.rows = vp->second[0];
+    m.nrows = (int32_t)V.rows.size();
+    m.row0 = V.row0;
+    m.rstep = V.rstep;
+    m.pmeta = vp->second[1];
+    m.w128 = vp->second[2];
+    m.frag = vp->second[3];
+    m.nblk = V.nblk;
+    desc_of[k] = (int32_t)Bp.vdescs.size();
+    Bp.vdescs.push_back(m);
+  }
+  std::vector<std::vector<VrTile>> q8(8);
+  for (size_t k = 0; k < work.size(); k++) {
+    const VrWork &w = work[k];
+    const int nblk = w.V->nblk;
+    int bands = nst > 0 ? (int)((2048 + nst - 1) / nst) : 1;
+    bands = std::max(1, std::min(bands, nblk));
+    for (int bnd = 0; bnd < bands; bnd++) {
+      const int b0 = (int)((int64_t)nblk * bnd / bands), b1 = (int)((int64_t)nblk * (bnd + 1) / bands);
+      if (b1 <= b0) continue;
+      for (int st = 0; st < w.nstrips; st++)
+        q8[k % 8].push_back(VrTile{desc_of[k], w.first_strip + st, b0, b1, 0, 0, 0, (int32_t)k});
+    }
+  }
+  std::vector<VrTile> tiles;
+  size_t mx = 0;
+  for (auto &q : q8) mx = std::max(mx, q.size());
+  for (size_t i = 0; i < mx; i++)
+    for (int x = 0; x < 8; x++)
+      if (i < q8[x].size()) tiles.push_back(q8[x][i]);
+  const int ntiles = (int)tiles.size();
+  int G = std::min(ntiles, c->n_cu);
+  if (G > 8) G -= G % 8;
+  // the streams: tile t -> workgroup t % G; every phase's rows [K0, Rend) and the
+  // next phase's must be resident together
+  std::vector<int32_t> info(2 * (size_t)G, 0);
+  std::vector<int64_t> gpos(G, 0), prev_gk0(G, -1);
+  for (int t = 0; t < ntiles; t++) {
+    VrTile &T = tiles[t];
+    const VrV &V = *work[T.pad].V;
+    const int g = t % G;
+    const int32_t *bm = V.bmeta.data();
+    T.kbase = bm[4 * T.b0];
+    const int kend = bm[4 * (T.b1 - 1) + 2];
+    T.glen = (kend - T.kbase + 15) / 16 * 16;
+    T.g0 = (int32_t)gpos[g];
+    for (int b = T.b0; b < T.b1; b++) {
+      const int64_t gk0 = T.g0 + bm[4 * b] - T.kbase, grend = T.g0 + bm[4 * b + 2] - T.kbase;
+      if (grend - gk0 > L.R) return false;
+      if (prev_gk0[g] >= 0 && grend - prev_gk0[g] > L.R) return false;
+      prev_gk0[g] = gk0;
+      info[2 * g]++;
+    }
+    gpos[g] += T.glen;
+    if (gpos[g] >= ((int64_t)1 << 30)) return false;
+    T.pad = 0;
+  }
+  for (int g = 0; g < G; g++) info[2 * g + 1] = (int32_t)gpos[g];
+  Bp.vrtiles = std::move(tiles);
+  Bp.vr_info = std::move(info);
+  Bp.vr_G = G;
+  Bp.vr_L = L;
+  Bp.vr_images = (int)work.size();
+  return true;
+}
+
 // k_rs_vm workgroups: (image, strip, band of blocks); the tables of a geometry
 // are placed in the heap once.
 static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
@@ -1517,6 +1645,7 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   struct Work1 {
     int32_t img, first_strip, nstrips;
     const VmV *V;
+    const AxisTable *vt;
   };
   std::vector<Work1> work;
   const int nv = (int)Bp.vm_img.size();
@@ -1607,8 +1736,31 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     m.pmeta = vp->second[7];
     m.hwsum = hp->second.second;
     m.nblk = V.nblk;
-    work.push_back({(int32_t)Bp.vdescs.size(), hp->second.first, (int32_t)H.strips.size(), &V});
+    work.push_back({(int32_t)Bp.vdescs.size(), hp->second.first, (int32_t)H.strips.size(), &V, Bp.vm_vt[q]});
     Bp.vdescs.push_back(m);
+  }
+  // k_rs_vr (FI_VR_RS=1): the images whose vertical axis has block-major
+  // tables (fi_plan.h VrV) run on the persistent block-major kernel
+  Bp.vr_G = 0;
+  if (c->vr_rs) {
+    std::vector<Work1> rest;
+    std::vector<VrWork> vr;
+    for (const Work1 &w : work) {
+      auto it = c->vrv_cache.find(w.vt);
+      if (it == c->vrv_cache.end()) {
+        VrV m;
+        if (!build_vr_v(*w.vt, &m)) m = VrV();
+        it = c->vrv_cache.emplace(w.vt, std::move(m)).first;
+      }
+      const VrV &V = it->second;
+      int64_t gap = 0;  // widest gap between consecutive touched rows (the DMA's per-lane offset)
+      for (size_t k = 1; k < V.rows.size(); k++) gap = std::max<int64_t>(gap, V.rows[k] - V.rows[k - 1]);
+      if (V.nblk > 0 && gap * Bp.vdescs[w.img].src_stride < ((int64_t)1 << 31))
+        vr.push_back({w.img, w.first_strip, w.nstrips, &V});
+      else
+        rest.push_back(w);
+    }
+    if (!vr.empty() && build_vr_tiles(c, E, Bp, vr)) work.swap(rest);
   }
   // bands of blocks only when the batch is too small to fill the chip
   int64_t nst = 0;
@@ -1784,6 +1936,8 @@ static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
   K.vstrip_off = B.addv(Bp.vstrips);
   K.vtile_off = B.addv(Bp.vtiles);
   K.vnph_off = B.addv(Bp.vp_nphase);
+  K.vrtile_off = B.addv(Bp.vrtiles);
+  K.vrinfo_off = B.addv(Bp.vr_info);
   K.hdesc_off = B.addv(Bp.hdescs);
   K.hstrip_off = B.addv(Bp.hstrips);
   K.htile_off = B.addv(Bp.htiles);
@@ -1846,6 +2000,14 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
     if (K.L0.tiles)
       hipLaunchKernelGGL(k_rs_copy, dim3(K.L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(K.L0),
                          pre_p(K.L0), K.L0.n);
+    if (!Bp.vrtiles.empty()) {
+      if (launch_vr(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
+                    (const VrTile *)(ab + K.vrtile_off), (int)Bp.vrtiles.size(), (const int32_t *)(ab + K.vrinfo_off),
+                    Bp.vr_G, ai, Bp.vr_L) != 0)
+        return set_err(FI_EDEVICE, "block-major MFMA resample launch rejected (LDS %d)", Bp.vr_L.total);
+      c->stats["path_vr"].launches += Bp.vr_images;
+      c->stats["path_vm"].launches -= Bp.vr_images;
+    }
     if (!Bp.vtiles.empty() && Bp.vp_G > 0) {
       if (launch_vp(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
                     (const VTile *)(ab + K.vtile_off), (int)Bp.vtiles.size(), (const int32_t *)(ab + K.vnph_off),
@@ -2361,6 +2523,12 @@ int fi_debug_vp_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   return vp_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
 }
+int fi_debug_vr_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
+  if (!c || !out) return FI_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return vr_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
+}
 // GPU JPEG decode (fi_jpeg.hip): the decode half of the host codec pipeline
 // (ImageProcessor's `convert` reads the source with libjpeg) on the device
 int fi_jpeg_info(const uint8_t *data, size_t len, int32_t *w, int32_t *h, int32_t *channels) {
@@ -2577,6 +2745,8 @@ int fi_create(fi_ctx **out, int32_t device) {
   // k_rs_vp: opt-in (FI_VP_RS=1) until it is faster than k_rs_vm
   c->vp_rs = false;
   if (const char *e = getenv("FI_VP_RS")) c->vp_rs = e[0] == '1';
+  // k_rs_vr: opt-in (FI_VR_RS=1) until measured
+  if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   if (const char *e = getenv("FI_DISABLE_HV_RS")) c->hv_rs = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');

@@ -217,6 +217,23 @@ struct VpLayout {
   int32_t total;        // dynamic LDS of the launch
 };
 constexpr int kVpMaxLds = 160 * 1024;
+// k_rs_vr (fi_vr.hip): k_rs_vp's roles with a block-major vertical pass over a
+// ring of R touched source rows (fi_plan.h VrV).  The VDesc fields rows /
+// nrows / row0 / rstep / w128 / frag / hwsum are VrV's, pmeta the per-block
+// {K0, ks, Rend, 0}.  A workgroup walks tiles g, g + G, ...; their touched rows
+// form one stream: tile t's list rows [kbase, kbase + glen) at stream
+// positions [g0, g0 + glen) (kbase, g0, glen multiples of 16), ring slot of
+// stream row G = G mod R.
+struct VrTile {
+  int32_t img, strip, b0, b1, g0, kbase, glen, pad;
+};
+struct VrLayout {
+  int32_t R;            // ring rows (multiple of 32)
+  int32_t plane;        // bytes of one limb plane of one channel (16 vpitch + pad)
+  int32_t otile_off;    // output tiles [2][otile_bytes]
+  int32_t otile_bytes;
+  int32_t total;        // dynamic LDS of the launch
+};
 
 // k_rs_hv (fi_hv.hip): streaming exact-integer MFMA resample, horizontal first
 // (fi_plan.h HvH / HvV).

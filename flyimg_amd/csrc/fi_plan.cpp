@@ -583,6 +583,52 @@ bool build_vm_v(const AxisTable &v, VmV *m) {
   return true;
 }
 
+bool build_vr_v(const AxisTable &v, VrV *m) {
+  *m = VrV();
+  const int ny = (int)v.start.size();
+  if (ny == 0) return false;
+  std::vector<int32_t> idx;
+  touched_list(v, &m->rows, &idx);
+  const int nl = (int)m->rows.size();
+  if (nl == 0) return false;
+  m->nblk = (ny + 15) / 16;
+  m->frag.assign((size_t)m->nblk * 6 * 256, 0);
+  m->w128.assign((size_t)16 * m->nblk, 0);
+  int pK0 = 0, pR = 0;
+  for (int b = 0; b < m->nblk; b++) {
+    int lo = 1 << 30, hi = -1;
+    for (int y = 16 * b; y < std::min(ny, 16 * b + 16); y++) {
+      int a, e;
+      tap_range(v, idx, y, &a, &e);
+      if (e < a) return false;  // an output row without taps
+      lo = std::min(lo, a);
+      hi = std::max(hi, e);
+    }
+    const int K0 = lo / 16 * 16, R = hi + 1;
+    const int ks = (R - K0 + 63) / 64;
+    if (ks > 2) return false;
+    if (b > 0 && (K0 < pK0 || R < pR)) return false;  // not monotone
+    pK0 = K0;
+    pR = R;
+    m->bmeta.insert(m->bmeta.end(), {K0, ks, R, 0});
+    for (int t = 0; t < ks; t++)
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int y = 16 * b + (l & 15), k = K0 + 64 * t + mfma_i8_k(l, j);
+          int32_t limb[3];
+          limbs3(y < ny ? tap_w(v, m->rows, y, k) : 0, limb);
+          put_frag(m->frag, (size_t)(b * 2 + t) * 3 * 256, l, j, limb);
+        }
+  }
+  for (int y = 0; y < ny; y++)
+    for (int j = 0; j < v.count[y]; j++) m->w128[y] += 128 * quant_w(v.w[v.woff[y] + j]);
+  m->row0 = m->rows[0];
+  m->rstep = nl > 1 ? m->rows[1] - m->rows[0] : 1;
+  for (int k = 1; k < nl && m->rstep > 0; k++)
+    if (m->rows[k] != m->row0 + m->rstep * k) m->rstep = 0;
+  return true;
+}
+
 // source-index range [a, e] of output o's non-zero taps (false: none)
 static bool src_range(const AxisTable &t, int o, int *a, int *e) {
   *a = 1 << 30;

@@ -141,6 +141,24 @@ struct HvV {
 };
 bool build_hv_v(const AxisTable &v, HvV *m);
 
+// Block-major vertical tables of k_rs_vr (fi_vr.hip): the vertical-first pass
+// of k_rs_vm with each 16-row output block computed in one go from a ring of
+// touched source rows.  Per block b: window start K0(b) (touched-row list
+// index, a multiple of 16, nondecreasing), ks(b) <= 2 k-steps of 64 list rows,
+// Rend(b) = one past its last non-zero tap, A fragments [b][t][limb] (zero past
+// ks and past the taps) and 128 * the quantized weight sum of every output row
+// (pixels enter the MFMA as p - 128).  Same weights, limbs and float
+// conversions as k_rs_vm, so the two kernels are bit-identical.
+struct VrV {
+  std::vector<int32_t> rows;           // touched source rows, ascending
+  int32_t row0 = 0, rstep = 0;         // rstep > 0: rows[k] == row0 + rstep * k
+  int nblk = 0;
+  std::vector<int32_t> bmeta;          // [nblk][4] {K0, ks, Rend, 0}
+  std::vector<int32_t> frag;           // [nblk][2][3][256]
+  std::vector<int32_t> w128;           // [16 nblk]
+};
+bool build_vr_v(const AxisTable &v, VrV *m);
+
 // Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)
 // to `out_size`; taps mapped back to the `in_src` source indices through the
 // SampleImage offsets (identity when !sample) and merged.

@@ -1,0 +1,823 @@
+// fi_vr.hip -- ImageMagick ResizeImage, vertical pass first (the
+// ThumbnailImage sample pre-step folded into the tap tables), as a persistent,
+// warp-specialised, exact-integer matrix-core pipeline with a BLOCK-MAJOR
+// vertical pass: v_mfma_i32_16x16x64_i8.
+//
+// Same weights, limbs and float conversions as k_rs_vm / k_rs_vp (bit-identical
+// outputs); what differs is how the vertical pass walks the source rows
+// (fi_plan.h VrV):
+//
+//  * k_rs_vm / k_rs_vp cut the touched rows into pieces of <= 64 rows aligned to
+//    the 16-row output blocks, and every piece feeds two accumulator slots (its
+//    own block and the next) -- so a block whose rows do not fit one piece
+//    (every ThumbnailImage geometry: 80 sampled rows per block, 67-80 touched
+//    rows) costs two full phases of 64-row MFMAs, and each MFMA triple folds
+//    its limbs with VALU shifts;
+//  * here the touched rows stream through a RING of R rows in LDS (LDS-DMA,
+//    loader waves, as far ahead as the ring allows), and phase p computes ONE
+//    output block b from its own window [K0(b), K0(b) + 64 ks) of the ring:
+//    ks <= 2 k-steps x 3 weight limbs into three separate accumulators per
+//    column tile (no shifts; folded once per block), then the Q16 planes.
+//
+//  Roles per phase (one workgroup barrier per phase, as k_rs_vp):
+//    V waves 0-7   block p: vertical MFMAs from the ring, fold, Q16 planes
+//                  (single plane buffer: a wave writes it only after the six
+//                  H waves have counted their reads of block p - 1 off an LDS
+//                  counter);
+//    H waves 8-13  block p - 1: horizontal MFMAs from the planes -> output
+//                  tile slot (p - 1) & 1;
+//    L waves 14-15 the stream cursor: source row pairs by LDS-DMA (ring slot
+//                  G mod R, G < K0(p) + R), A fragments of block p + 1, the
+//                  record of phase p + 2 (+ the strip's LUT), the stores of
+//                  block p - 2; the end-of-phase vmcnt waits exactly for the
+//                  rows of block p + 1.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "fi_internal.h"
+
+namespace fi {
+
+namespace {
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const i32x4 g_i32x4;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint16_t g_u16;
+typedef __attribute__((address_space(3))) i32x2 l_i32x2;
+typedef __attribute__((address_space(3))) uint8_t l_u8;
+
+constexpr int kVW = 8;                   // V waves: 64 source bytes (4 column tiles) each
+constexpr int kHW = 6;                   // H waves 8-13
+constexpr int kLW = 2;                   // L waves 14-15
+static_assert(kVW + kHW + kLW == 16, "16 waves");
+constexpr int kABytes = 6144 + 64;       // [t][limb][64 lanes][16 B] + w128 of the block's 16 rows
+constexpr int kRecBytes = 32;
+constexpr int kLutSlots = 4;
+constexpr int kPlanePad = 176;           // 44 (mod 64) dwords: see fi_vm.hip kVmPlanePad
+constexpr int kOt8Pitch = 200;           // 8-bit output tile row (<= 64 px x 3 + the row shift)
+
+// record flags (one record per phase, written by L wave 0 two phases ahead)
+constexpr int kFirst = 1;                // first block of a tile
+constexpr int kSlot = 2;                 // output-tile slot of the block (phase parity)
+constexpr int kTslotShift = 4;           // bits 4-5: LUT slot (tile sequence number mod 4)
+
+__device__ __forceinline__ i32x2 tr8(const uint8_t *p) { return __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2 *)(p)); }
+__device__ __forceinline__ i32x4 mfma(i32x4 a, i32x4 b, i32x4 c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int col_off(int ci) { return (ci * 16) ^ (((ci >> 4) & 1) << 7); }
+__device__ __forceinline__ uint32_t q16_to_u8(uint32_t q) {
+  // ScaleQuantumToChar: (q + 128) / 257 = ((q + 128) * 65281) >> 24 on [0, 65535]
+  return (uint32_t)(((uint64_t)((q & 0xFFFFu) + 128u) * (65281ull << 8)) >> 32);
+}
+__device__ __forceinline__ uint32_t gray_q16(uint32_t r, uint32_t g, uint32_t b) {
+  // -colorspace Gray: Rec709Luma on gamma-encoded Q16, ClampToQuantum
+  const double gv = 0.212656 * (double)r + 0.715158 * (double)g + 0.072186 * (double)b;
+  return !(gv > 0.0) ? 0u : (gv >= 65535.0 ? 65535u : (uint32_t)(gv + 0.5));
+}
+__device__ __forceinline__ int32_t fold3(int32_t d0, int32_t d1, int32_t d2) {
+  return (int32_t)((uint32_t)d0 + ((uint32_t)d1 << 8) + ((uint32_t)d2 << 16));
+}
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t *p) { return (uint32_t)(uintptr_t)(const l_u8 *)p; }
+// read-only tables through the constant address space (scalar loads; see fi_vp.hip)
+template <class T>
+__device__ __forceinline__ T ldc(const T *p) {
+  static_assert(sizeof(T) % 4 == 0, "dword records");
+  T r;
+  const __attribute__((address_space(4))) int32_t *q = (const __attribute__((address_space(4))) int32_t *)p;
+  int32_t *o = reinterpret_cast<int32_t *>(&r);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); i++) o[i] = q[i];
+  return r;
+}
+__device__ __forceinline__ int32_t ldc1(const int32_t *p) { return *(const __attribute__((address_space(4))) int32_t *)p; }
+__device__ __forceinline__ int ufl(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// LDS-DMA, saddr form: lane i's 16 bytes at sbase + voff land at LDS m0 + 16 i.
+// Invisible to hipcc's waitcnt pass: the L loop waits for it explicitly.
+__device__ __forceinline__ void dma16(uint32_t m0, const uint8_t *sbase, uint32_t voff) {
+  unsigned keep;
+  const uint64_t sb = (uint64_t)(uintptr_t)sbase;
+  sbase = reinterpret_cast<const uint8_t *>(
+      (uintptr_t)(((uint64_t)(uint32_t)ufl((int)(uint32_t)(sb >> 32)) << 32) | (uint32_t)ufl((int)(uint32_t)sb)));
+  m0 = (uint32_t)ufl((int)m0);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(m0)
+      : "memory");
+}
+// the same DMA with a different asm text: keeps hipcc from tail-merging the
+// row stream's load-free loop into the table-lookup path (whose scalar-load
+// wait would then run before every DMA)
+__device__ __forceinline__ void dma16_fast(uint32_t m0, const uint8_t *sbase, uint32_t voff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2 ; row stream\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(m0)
+      : "memory");
+}
+__device__ __forceinline__ void phase_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// s_waitcnt vmcnt(<= n): the wave's n youngest vector-memory operations may stay
+// in flight (n rounded down to an immediate the switch has)
+__device__ __forceinline__ void wait_vm_le(int n) {
+  if (n >= 32)
+    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else if (n >= 24)
+    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 20)
+    asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else if (n >= 16)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 14)
+    asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if (n >= 12)
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 10)
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if (n >= 8)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 7)
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else if (n == 6)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n == 5)
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if (n == 4)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n == 3)
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (n == 2)
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n == 1)
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+struct Rec {  // 32 B in LDS
+  int32_t t, blk, flags, slot0, ks, grend, pad0, pad1;
+};
+struct Lds {  // offsets of the launch's LDS regions
+  int ring, a, rec, cnt, lut, planes, otile;
+};
+__device__ __forceinline__ Lds lds_of(const VrLayout &L) {
+  Lds o;
+  o.ring = 0;
+  o.a = L.R * 512;
+  o.rec = o.a + 2 * kABytes;
+  o.cnt = o.rec + 8 * kRecBytes;
+  o.lut = o.cnt + 16;
+  o.planes = o.lut + kLutSlots * 1024;
+  o.otile = L.otile_off;
+  return o;
+}
+}  // namespace
+
+// per-wave phase sums of MODE 9 (fi_debug_vr_stamps, tools/vp_timing.py VR=1)
+constexpr int kVrStampSlots = 256;
+constexpr int kVrStampN = 16 * 6;
+__device__ uint64_t g_vr_stamps[kVrStampSlots * kVrStampN];
+
+// MODE (profiling ablations, FI_VR_VARIANT; wrong pixels): 0 production,
+// 1 DMA stream only, 2 no H role and no stores, 3 no stores, 9 production +
+// per-phase s_memtime sums; 10 + k: ablation k with the stamps.
+template <int MODE>
+__global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ descs, const MStrip *__restrict__ strips,
+                                                   const VrTile *__restrict__ tiles, int ntiles,
+                                                   const int32_t *__restrict__ wginfo, const int32_t *__restrict__ ai,
+                                                   VrLayout Lo) {
+  constexpr int M = MODE >= 10 ? MODE - 10 : MODE;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = ufl(tid >> 6);
+  const int G = (int)gridDim.x, g = (int)blockIdx.x;
+  const int N = ldc1(wginfo + 2 * g);         // phases (blocks) of this workgroup's stream
+  const int gend = ldc1(wginfo + 2 * g + 1);  // stream rows
+  const int R = Lo.R;
+  const Lds O = lds_of(Lo);
+  Rec *recs = reinterpret_cast<Rec *>(lds + O.rec);
+  volatile uint32_t *hcnt = reinterpret_cast<volatile uint32_t *>(lds + O.cnt);
+  const int32_t *lut = reinterpret_cast<const int32_t *>(lds + O.lut);  // [kLutSlots][256]
+  uint8_t *planes = lds + O.planes;                                      // [6][plane]
+  uint8_t *otiles = lds + O.otile;                                       // [2][otile_bytes]
+  const int plane = Lo.plane;
+  constexpr bool kStamp = MODE == 9 || MODE >= 10;
+  uint64_t tsum[5] = {}, tprev = 0;
+  auto stamp = [&](int k) {
+    if (kStamp) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      tsum[k] += t - tprev;
+      tprev = t;
+    }
+  };
+  auto stamp_out = [&](int n) {
+    if (kStamp && lane == 0 && g < kVrStampSlots) {
+      uint64_t *o = g_vr_stamps + g * kVrStampN + 6 * wv;
+      for (int k = 0; k < 5; k++) o[k] = k < n ? tsum[k] : 0;
+      o[5] = (uint64_t)N;
+    }
+  };
+  auto read_rec = [&](int s) -> Rec {
+    const Rec x = recs[s & 7];
+    return Rec{ufl(x.t), ufl(x.blk), ufl(x.flags), ufl(x.slot0), ufl(x.ks), ufl(x.grend), 0, 0};
+  };
+
+  if (wv >= kVW + kHW) {
+    // ============ L role: phase records, row stream, A fragments, stores ============
+    const int li = wv - (kVW + kHW);
+    const int h = lane >> 5;  // half-wave: the two rows of one 1-KB DMA
+    // ---- phase cursor (records, A fragments) ----
+    struct PI {
+      int t, blk, gk0, grend, ks, frag, w128, flags;
+    };
+    int ct = g, ck = 0, cb = 0, c_bmeta = 0, c_frag = 0, c_w128 = 0, c_lut = 0, c_lut_n = 0;
+    VrTile CT{};
+    auto ptile_load = [&]() {
+      CT = ldc(tiles + ct);
+      const VDesc D = ldc(descs + CT.img);
+      const MStrip S = ldc(strips + CT.strip);
+      c_bmeta = D.pmeta;
+      c_frag = D.frag;
+      c_w128 = D.w128;
+      c_lut = S.lut;
+      c_lut_n = S.lut_n;
+      cb = CT.b0;
+    };
+    if (ct < ntiles) ptile_load();
+    // the phase at the cursor; writes its record (slot s) and stages its tile's
+    // LUT (first block of a tile) -- L wave 0 only; advances the cursor
+    auto next_phase = [&](int s) -> PI {
+      const int4 m = ldc(reinterpret_cast<const int4 *>(ai + c_bmeta + 4 * cb));  // {K0, ks, Rend, 0}
+      PI r;
+      r.t = ct;
+      r.blk = cb;
+      r.gk0 = CT.g0 + (m.x - CT.kbase);
+      r.grend = CT.g0 + (m.z - CT.kbase);
+      r.ks = m.y;
+      r.frag = c_frag + cb * 6 * 256;
+      r.w128 = c_w128 + 16 * cb;
+      r.flags = (cb == CT.b0 ? kFirst : 0) | ((s & 1) ? kSlot : 0) | ((ck & (kLutSlots - 1)) << kTslotShift);
+      if (li == 0) {
+        if (lane == 0) recs[s & 7] = Rec{r.t, r.blk, r.flags, r.gk0 % R, r.ks, r.grend, 0, 0};
+        if ((r.flags & kFirst) && lane < (c_lut_n + 3) / 4)
+          dma16(lds_addr(lds) + (uint32_t)(O.lut + (ck & (kLutSlots - 1)) * 1024),
+                reinterpret_cast<const uint8_t *>(ai + c_lut), 16u * lane);
+      }
+      cb++;
+      if (cb >= CT.b1) {
+        ck++;
+        ct += G;
+        if (ct < ntiles) ptile_load();
+      }
+      return r;
+    };
+    // A fragments (ks k-steps x 3 limbs x 1 KB) + the block's w128 row into A slot `slot`
+    auto issue_a = [&](const PI &r, int slot) {
+      const uint32_t m0 = lds_addr(lds) + (uint32_t)(O.a + slot * kABytes);
+      const int nf = 3 * r.ks;
+      for (int i = li; i <= nf; i += kLW) {
+        if (i < nf)
+          dma16(m0 + 1024 * i, reinterpret_cast<const uint8_t *>(ai + r.frag) + 1024 * i, 16u * lane);
+        else if (lane < 4)
+          dma16(m0 + 6144, reinterpret_cast<const uint8_t *>(ai + r.w128), 16u * lane);
+      }
+    };
+    // ---- row cursor: this wave's row pairs G = 4 m + 2 li of the stream ----
+    int rt = g, rG = 2 * li, rslot = 2 * li, n_issued = 0;
+    VrTile RT{};
+    const uint8_t *r_src = nullptr;
+    int64_t r_stride = 0;
+    int r_b0 = 0, r_nbytes = 0, r_row0 = 0, r_rstep = 0, r_rows = 0, r_nrows = 0;
+    auto rtile_load = [&]() {
+      RT = ldc(tiles + rt);
+      const VDesc D = ldc(descs + RT.img);
+      const MStrip S = ldc(strips + RT.strip);
+      r_src = D.src;
+      r_stride = D.src_stride;
+      r_b0 = S.b0;
+      r_nbytes = S.nbytes;
+      r_row0 = D.row0;
+      r_rstep = D.rstep;
+      r_rows = D.rows;
+      r_nrows = D.nrows;
+    };
+    if (rt < ntiles) rtile_load();
+    const uint32_t lane_c = (uint32_t)((lane & 31) ^ h);  // chunk of this lane before the row swizzle
+    // issue this wave's pairs up to stream row `limit`; returns the DMAs issued.
+    // Evenly spaced rows (rstep > 0) go through a loop with no loads: bases
+    // linear in the pair index, the chunk swizzle from the ring slot.
+    auto issue_rows = [&](int limit) -> int {
+      int n = 0;
+      while (rG < limit) {
+        if (rG >= RT.g0 + RT.glen) {
+          rt += G;
+          rtile_load();  // the host makes the stream cover [0, gend): rt < ntiles here
+          continue;
+        }
+        const int seg = min(limit, RT.g0 + RT.glen);
+        int k0 = RT.kbase + (rG - RT.g0);
+        if (r_rstep > 0 && k0 + 1 < r_nrows) {
+          // pairs with k0 + 1 < nrows and rG < seg
+          const int cnt = min((seg - rG + 3) >> 2, (r_nrows - 1 - k0 + 3) >> 2);
+          const int64_t rs = (int64_t)r_rstep * r_stride;
+          const uint8_t *base = r_src + (int64_t)(r_row0 + r_rstep * k0) * r_stride + r_b0;
+          const uint32_t hoff = h ? (uint32_t)rs : 0u;
+          for (int i = 0; i < cnt; i++) {
+            const uint32_t f = (uint32_t)((rslot & 7) | (((rslot >> 4) & 1) << 3));
+            uint32_t lc = lane_c ^ f;
+            if (16 * (int)lc >= r_nbytes) lc = 0;
+            dma16_fast(lds_addr(lds) + (uint32_t)(O.ring + rslot * 512), base, hoff + 16u * lc);
+            base += 4 * rs;
+            rslot += 4;
+            if (rslot >= R) rslot -= R;
+          }
+          n += cnt;
+          rG += 4 * cnt;
+          continue;
+        }
+        // one pair: the rows table, or clamped at the list end
+        k0 = min(k0, r_nrows - 1);
+        const int k1 = min(k0 + 1, r_nrows - 1);
+        const int r0 = r_rstep > 0 ? r_row0 + r_rstep * k0 : ldc1(ai + r_rows + k0);
+        const int r1 = r_rstep > 0 ? r_row0 + r_rstep * k1 : ldc1(ai + r_rows + k1);
+        const uint8_t *base = r_src + (int64_t)r0 * r_stride + r_b0;
+        const uint32_t f = (uint32_t)((rslot & 7) | (((rslot >> 4) & 1) << 3));  // chunk swizzle of row rslot (rslot + 1: f ^ 1)
+        uint32_t lc = lane_c ^ f;
+        if (16 * (int)lc >= r_nbytes) lc = 0;
+        const uint32_t voff = (h ? (uint32_t)((int64_t)(r1 - r0) * r_stride) : 0u) + 16u * lc;
+        dma16(lds_addr(lds) + (uint32_t)(O.ring + rslot * 512), base, voff);
+        n++;
+        rG += 4;
+        rslot += 4;
+        if (rslot >= R) rslot -= R;
+      }
+      return n;
+    };
+    // own pairs (starts 4 m + 2 li) below stream row x
+    auto own_below = [&](int x) -> int { return x > 2 * li ? (x - 2 * li + 3) >> 2 : 0; };
+
+    // the loader's few instructions go first on its SIMD
+    __builtin_amdgcn_s_setprio(2);
+    if (li == 0 && lane == 0) hcnt[0] = 0;
+    PI P0{}, P1{};
+    if (N > 0) {
+      P0 = next_phase(0);
+      if (M != 1) issue_a(P0, 0);
+    }
+    if (N > 1) P1 = next_phase(1);
+    if (N > 0) n_issued += issue_rows(min(P0.gk0 + R, gend));
+    wait_vm0();
+    phase_barrier();  // records 0 / 1, A(0), the rows of block 0 and the first LUT visible
+    phase_barrier();
+    if (kStamp) tprev = __builtin_amdgcn_s_memtime();
+    int stile = -1;  // tile of the cached store descriptors
+    struct StoreD {
+      uint8_t *dst;
+      int64_t dst_stride;
+      int32_t ew, eh, rot, gray, x0, x1;
+    } sD{};
+    for (int p = 0; p < N + 2; p++) {
+      // stores of the block of phase p - 2 (output tile slot (p - 2) & 1): dword-
+      // aligned 8-bit segments go after this phase's DMAs (their count enters the
+      // end-of-phase vmcnt), the other output kinds before them
+      bool st_fast = false;
+      uint8_t *st_row0 = nullptr;
+      int64_t st_stride = 0;
+      int st_nb = 0, st_nrow = 0;
+      const uint8_t *st_ot = nullptr;
+      if (p >= 2 && p - 2 < N && M != 3 && M != 1 && M != 2) {
+        const Rec rs = read_rec(p - 2);
+        if (stile != rs.t) {
+          stile = rs.t;
+          const VrTile T = ldc(tiles + rs.t);
+          const VDesc D0 = ldc(descs + T.img);
+          const MStrip S0 = ldc(strips + T.strip);
+          sD = StoreD{D0.dst, D0.dst_stride, D0.ew, D0.eh, D0.rot, D0.gray, S0.x0, S0.x1};
+        }
+        const StoreD &D = sD;
+        const int b = rs.blk;
+        const int nx = D.x1 - D.x0;
+        const int oc = D.gray ? 1 : 3;
+        const int rows_here = min(16, D.eh - 16 * b);
+        const int nb = nx * oc;
+        uint8_t *ot = otiles + ((rs.flags & kSlot) ? Lo.otile_bytes : 0);
+        const uint16_t *otile = reinterpret_cast<const uint16_t *>(ot);
+        const bool fastA = !D.gray && D.rot == 0 && (((uintptr_t)D.dst + (uint64_t)D.x0 * 3) & 3u) == 0 &&
+                           (D.dst_stride & 3) == 0 && (nb & 3) == 0;
+        auto out_byte = [&](int yl, int k) -> uint32_t {
+          const uint16_t *o = otile + yl * kVmOtilePitch;
+          if (!D.gray) return q16_to_u8(o[k]);
+          return q16_to_u8(gray_q16(o[3 * k], o[3 * k + 1], o[3 * k + 2]));
+        };
+        if (fastA) {
+          st_fast = true;
+          st_row0 = D.dst + (int64_t)(16 * b + li) * D.dst_stride + (int64_t)D.x0 * 3;
+          st_stride = (int64_t)kLW * D.dst_stride;
+          st_nb = nb;
+          st_nrow = (rows_here - li + kLW - 1) / kLW;
+          st_ot = ot + li * kOt8Pitch;
+        } else if (D.gray == 2) {
+          for (int it = tid - 64 * (kVW + kHW); it < rows_here * nx; it += 64 * kLW) {
+            const int yl = it / nx, x = it - yl * nx;
+            const uint16_t *o = otile + yl * kVmOtilePitch + 3 * x;
+            ((g_u16 *)(D.dst + (int64_t)(16 * b + yl) * D.dst_stride))[D.x0 + x] = (uint16_t)gray_q16(o[0], o[1], o[2]);
+          }
+        } else if (!D.gray && D.rot == 0) {
+          // 8-bit tile, rows shifted to the destination's address mod 4: L wave li
+          // copies rows li, li + 2, ..., one destination dword per lane
+          const uint32_t sh0 = (uint32_t)(((uintptr_t)D.dst + (uint64_t)D.x0 * 3) & 3u);
+          const uint32_t shs = (uint32_t)(D.dst_stride & 3);
+          constexpr int kRows = 16 / kLW;
+          uint32_t wd[kRows];
+#pragma unroll
+          for (int r = 0; r < kRows; r++) wd[r] = *reinterpret_cast<const uint32_t *>(ot + (li + kLW * r) * kOt8Pitch + 4 * lane);
+#pragma unroll
+          for (int r = 0; r < kRows; r++) {
+            const int yl = li + kLW * r;
+            if (yl >= rows_here) break;
+            const int sh = (int)((sh0 + (uint32_t)(16 * b + yl) * shs) & 3u);
+            const int k0 = 4 * lane - sh;
+            uint8_t *a0 = D.dst + (int64_t)(16 * b + yl) * D.dst_stride + (int64_t)D.x0 * 3;
+            if (k0 >= 0 && k0 + 4 <= nb) {
+              *(g_u32 *)(a0 + k0) = wd[r];
+            } else if (k0 < nb && k0 + 4 > 0) {
+#pragma unroll
+              for (int j = 0; j < 4; j++)
+                if (k0 + j >= 0 && k0 + j < nb) *(g_u8 *)(a0 + k0 + j) = (uint8_t)(wd[r] >> (8 * j));
+            }
+          }
+        } else if (D.rot == 0) {
+          const int ndw = (nb + 3) / 4 + 1;
+          const float inv = 1.0f / (float)ndw;
+          for (int it = tid - 64 * (kVW + kHW); it < rows_here * ndw; it += 64 * kLW) {
+            const int yl = (int)(((float)it + 0.5f) * inv), d = it - yl * ndw;
+            uint8_t *a0 = D.dst + (int64_t)(16 * b + yl) * D.dst_stride + (int64_t)D.x0 * oc;
+            const int k0 = 4 * d - (int)((uintptr_t)a0 & 3u);
+            if (k0 >= nb) continue;
+            if (k0 >= 0 && k0 + 4 <= nb) {
+              const uint32_t wd = out_byte(yl, k0) | (out_byte(yl, k0 + 1) << 8) | (out_byte(yl, k0 + 2) << 16) |
+                                  (out_byte(yl, k0 + 3) << 24);
+              *(g_u32 *)(a0 + k0) = wd;
+            } else {
+              for (int k = max(k0, 0); k < min(k0 + 4, nb); k++) *(g_u8 *)(a0 + k) = (uint8_t)out_byte(yl, k);
+            }
+          }
+        } else {
+          for (int it = tid - 64 * (kVW + kHW); it < rows_here * nx; it += 64 * kLW) {
+            const int yl = it / nx, x = it - yl * nx, y = 16 * b + yl;
+            const int ox = D.x0 + x;
+            int dx, dy;
+            if (D.rot == 90) {
+              dx = D.eh - 1 - y;
+              dy = ox;
+            } else if (D.rot == 180) {
+              dx = D.ew - 1 - ox;
+              dy = D.eh - 1 - y;
+            } else {  // 270
+              dx = y;
+              dy = D.ew - 1 - ox;
+            }
+            g_u8 *out = (g_u8 *)(D.dst + (int64_t)dy * D.dst_stride) + dx * oc;
+            for (int c = 0; c < oc; c++) out[c] = (uint8_t)out_byte(yl, x * oc + c);
+          }
+        }
+      }
+      // A fragments of block p + 1 (its record was written last phase)
+      if (M != 1 && p + 1 < N) issue_a(P1, (p + 1) & 1);
+      stamp(0);
+      PI P2{};
+      if (p + 2 < N) P2 = next_phase(p + 2);
+      // source rows as far ahead as the ring allows: slots of rows < K0(p) are free
+      int nr = 0;
+      if (p < N) {
+        nr = issue_rows(min(P0.gk0 + R, gend));
+        n_issued += nr;
+      }
+      stamp(1);
+      // dword-aligned fast8 stores of block p - 2: rows li, li + 2, ... as dwords
+      int ns = 0;
+      if (st_fast) {
+        const int U = st_nb >> 2;
+        const float invU = 1.0f / (float)U;
+        for (int it0 = 0; it0 < st_nrow * U; it0 += 64, ns++) {
+          const int it = it0 + lane;
+          if (it < st_nrow * U) {
+            const int r = (int)(((float)it + 0.5f) * invU), u = it - r * U;
+            *(g_u32 *)(st_row0 + r * st_stride + 4 * u) =
+                *reinterpret_cast<const uint32_t *>(st_ot + r * kLW * kOt8Pitch + 4 * u);
+          }
+        }
+      }
+      // block p + 1's rows (every own pair starting below its Rend), A(p + 1) and
+      // the LUTs landed; younger row pairs and this phase's stores may stay in flight
+      if (p + 1 < N) {
+        const int after = max(0, n_issued - own_below(P1.grend));
+        wait_vm_le(min(after, nr) + ns);
+      } else {
+        wait_vm0();
+      }
+      stamp(2);
+      phase_barrier();
+      stamp(3);
+      P0 = P1;
+      P1 = P2;
+    }
+    stamp_out(4);
+    return;
+  }
+
+  if (wv < kVW) {
+    // =================== V role: block-major vertical MFMA + Q16 planes ===================
+    // wave w owns source bytes [64 w, 64 w + 64) of the strip = column tiles j < 4
+    const int w = wv;
+    constexpr int kT = 4;
+    // transposing reads: lane reads rows rA (and rA + 8) of a k-step, bytes 8 (lane & 1)
+    // of its tile's 16-byte chunk; the chunk swizzle of ring slot s is
+    // f(s) = (s & 7) | 8 ((s >> 4) & 1), and with the k-step start a multiple of 16
+    // f = fL ^ 8 bit4(start) for both rows
+    const int rA = 16 * (lane >> 4) + ((lane & 15) >> 1);
+    const int fL = (rA & 7) | (((rA >> 4) & 1) << 3);
+    uint32_t offj[kT];
+#pragma unroll
+    for (int j = 0; j < kT; j++) offj[j] = (uint32_t)(16 * ((4 * w + j) ^ fL) + 8 * (lane & 1));
+    uint32_t vcolp[kT / 2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    phase_barrier();
+    phase_barrier();
+    Rec rC = N > 0 ? read_rec(0) : Rec{};
+    if (kStamp) tprev = __builtin_amdgcn_s_memtime();
+    for (int p = 0; p < N + 2; p++) {
+      if (p < N && M != 1) {
+        const Rec C = rC;
+        if (C.flags & kFirst) {
+          // new tile: Q16-plane offsets of this lane's columns from the staged LUT
+          const VrTile T = ldc(tiles + C.t);
+          const MStrip S = ldc(strips + T.strip);
+          const int32_t *lt = lut + 256 * ((C.flags >> kTslotShift) & (kLutSlots - 1));
+#pragma unroll
+          for (int j = 0; j < kT; j++) {
+            const int col = 64 * w + 16 * j + (lane & 15);
+            const int abs = S.b0 + min(col, S.nbytes - 1), px = abs / 3, chn = abs - 3 * px;
+            const int ci = lt[px - S.lut_px0];
+            const uint32_t o = (col < S.nbytes && ci >= 0) ? (uint32_t)(chn * plane + col_off(ci) + 4 * (lane >> 4))
+                                                            : 0xFFFFu;
+            if (j & 1)
+              vcolp[j >> 1] = (vcolp[j >> 1] & 0xFFFFu) | (o << 16);
+            else
+              vcolp[j >> 1] = (vcolp[j >> 1] & 0xFFFF0000u) | o;
+          }
+        }
+        stamp(0);
+        const i32x4 *al = reinterpret_cast<const i32x4 *>(lds + O.a + (p & 1) * kABytes);
+        const i32x4 corr = al[384 + (lane >> 4)];  // 128 * weight sums of this lane's 4 output rows
+        i32x4 acc[3][kT];
+        const uint32_t RB = (uint32_t)R * 512u;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+          if (t >= C.ks) break;
+          int sb = C.slot0 + 64 * t;
+          if (sb >= R) sb -= R;
+          // ring rows sb + rA (+ 8), wrapped: min(y, y - RB) in unsigned arithmetic
+          const uint32_t y0 = (uint32_t)(sb + rA) * 512u, y1 = y0 + 8u * 512u;
+          const uint32_t Y0 = min(y0, y0 - RB), Y1 = min(y1, y1 - RB);
+          const uint32_t sx = (uint32_t)((sb >> 4) & 1) << 7;
+          i32x4 B[kT];
+#pragma unroll
+          for (int j = 0; j < kT; j++) {
+            const uint32_t o = offj[j] ^ sx;
+            const i32x2 lo = tr8(lds + O.ring + Y0 + o), hi = tr8(lds + O.ring + Y1 + o);
+            B[j] = i32x4{lo.x, lo.y, hi.x, hi.y} ^ i32x4{(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+          }
+          i32x4 A[3];
+#pragma unroll
+          for (int q = 0; q < 3; q++) A[q] = al[(t * 3 + q) * 64 + lane];
+          if (t == 0) {
+#pragma unroll
+            for (int j = 0; j < kT; j++) acc[0][j] = mfma(A[0], B[j], corr);
+#pragma unroll
+            for (int j = 0; j < kT; j++) acc[1][j] = mfma(A[1], B[j], i32x4{0, 0, 0, 0});
+#pragma unroll
+            for (int j = 0; j < kT; j++) acc[2][j] = mfma(A[2], B[j], i32x4{0, 0, 0, 0});
+          } else {
+#pragma unroll
+            for (int j = 0; j < kT; j++) acc[0][j] = mfma(A[0], B[j], acc[0][j]);
+#pragma unroll
+            for (int j = 0; j < kT; j++) acc[1][j] = mfma(A[1], B[j], acc[1][j]);
+#pragma unroll
+            for (int j = 0; j < kT; j++) acc[2][j] = mfma(A[2], B[j], acc[2][j]);
+          }
+        }
+        stamp(1);
+        // the H waves' reads of block p - 1's planes are done (single plane buffer)
+        if (M != 2) {
+          const uint32_t want = 6u * (uint32_t)(p + 1);
+          while (hcnt[0] < want) __builtin_amdgcn_s_sleep(1);
+        }
+        // block done: ClampToQuantum(257 acc / 2^22) -> Q16 hi / lo signed-byte planes
+#pragma unroll
+        for (int j = 0; j < kT; j++) {
+          const uint32_t o = (vcolp[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+          uint32_t q[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int32_t tot = fold3(acc[0][j][i], acc[1][j][i], acc[2][j][i]);
+            q[i] = __float2uint_rz(fmaf((float)tot, 257.0f / 4194304.0f, 0.5f));
+          }
+          const auto p01 = __builtin_amdgcn_cvt_pk_u16(q[0], q[1]);
+          const auto p23 = __builtin_amdgcn_cvt_pk_u16(q[2], q[3]);
+          const uint32_t x01 = __builtin_bit_cast(uint32_t, p01) ^ 0x80808080u;
+          const uint32_t x23 = __builtin_bit_cast(uint32_t, p23) ^ 0x80808080u;
+          if (o != 0xFFFFu) {
+            *reinterpret_cast<uint32_t *>(planes + o) = __builtin_amdgcn_perm(x23, x01, 0x07050301u);
+            *reinterpret_cast<uint32_t *>(planes + o + 3 * plane) = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
+          }
+        }
+        stamp(2);
+      }
+      if (p + 1 < N) rC = read_rec(p + 1);
+      phase_barrier();
+      stamp(3);
+    }
+    stamp_out(4);
+    return;
+  }
+
+  // ============ H role: horizontal MFMA of the previous block ============
+  const int hw = wv - kVW;  // 0 .. kHW - 1
+  int ftile = -1, h_nx = 0, h_items = 0;
+  bool h_fast8 = false;
+  uint32_t h_sh0 = 0, h_shs = 0;
+  i32x4 hb[2][2][3];
+  int hw0k[2] = {0, 0}, hksk[2] = {0, 0};
+  float hwsk[2] = {0.f, 0.f};
+  __builtin_amdgcn_s_setprio(1);
+  phase_barrier();
+  phase_barrier();
+  Rec rH{};  // record of the block this phase's horizontal pass takes (phase p - 1)
+  if (kStamp) tprev = __builtin_amdgcn_s_memtime();
+  for (int p = 0; p < N + 2; p++) {
+    stamp(0);
+    if (M != 1 && M != 2 && p >= 1 && p - 1 < N) {
+      const Rec rh = rH;
+      const int b = rh.blk;
+      if (ftile != rh.t) {
+        // a new tile: its strip's horizontal fragments and epilogue constants
+        ftile = rh.t;
+        const VrTile T = ldc(tiles + rh.t);
+        const VDesc D = ldc(descs + T.img);
+        const MStrip S = ldc(strips + T.strip);
+        h_nx = S.x1 - S.x0;
+        h_items = 3 * S.nocb;
+        h_fast8 = !D.gray && D.rot == 0;
+        h_sh0 = (uint32_t)(((uintptr_t)D.dst + (uint64_t)S.x0 * 3) & 3u);
+        h_shs = (uint32_t)(D.dst_stride & 3);
+        const int nx = h_nx;
+        const g_i32x4 *hf = (const g_i32x4 *)(ai + S.frag);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+          const int it = hw + kHW * k, ob = it / 3;
+          const bool ok = it < 3 * S.nocb;
+          hw0k[k] = ok ? ldc1(ai + S.s0 + 2 * ob) : 0;
+          hksk[k] = ok ? ldc1(ai + S.s0 + 2 * ob + 1) : 0;
+          const int hx = 16 * ob + (lane & 15);
+          hwsk[k] = (ok && hx < nx) ? 32896.0f * (float)ai[D.hwsum + S.x0 + hx] : 0.0f;
+#pragma unroll
+          for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+              hb[k][t][q] = (ok && t < S.ks) ? hf[((ob * S.ks + t) * 3 + q) * 64 + lane] : i32x4{0, 0, 0, 0};
+        }
+      }
+      stamp(1);
+      uint8_t *ot = otiles + ((rh.flags & kSlot) ? Lo.otile_bytes : 0);
+      uint16_t *otile = reinterpret_cast<uint16_t *>(ot);
+      const int nx = h_nx;
+      const bool fast8 = h_fast8;
+      const uint32_t sh0 = h_sh0, shs = h_shs;
+      // per item: plane reads + MFMAs, then its epilogue; once the last item's
+      // reads have returned, the LDS counter tells the V waves the planes are free
+      const int nk = (hw < h_items ? 1 : 0) + (hw + kHW < h_items ? 1 : 0);
+      auto signal = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0)
+          atomicAdd(static_cast<unsigned *>(__builtin_assume_aligned(lds + O.cnt, 16)), 1u);
+      };
+      if (nk == 0) signal();
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        if (k >= nk) break;
+        const int it = hw + kHW * k;
+        const int ob = it / 3, chn = it - 3 * ob;
+        const int hw0 = hw0k[k], hks = hksk[k];
+        i32x4 hh[3], hl[3];
+#pragma unroll
+        for (int q = 0; q < 3; q++) hh[q] = hl[q] = i32x4{0, 0, 0, 0};
+        const uint8_t *ph = planes + chn * plane, *pl = ph + 3 * plane;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+          if (t >= hks) break;
+          const int cA = hw0 + 64 * t + 16 * (lane >> 4) + ((lane & 15) >> 1);
+          const int o0 = col_off(cA) + 8 * (lane & 1), o1 = col_off(cA + 8) + 8 * (lane & 1);
+          const i32x2 h0 = tr8(ph + o0), h1 = tr8(ph + o1);
+          const i32x2 l0 = tr8(pl + o0), l1 = tr8(pl + o1);
+          const i32x4 Ah = {h0.x, h0.y, h1.x, h1.y}, Al = {l0.x, l0.y, l1.x, l1.y};
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            hh[q] = mfma(Ah, hb[k][t][q], hh[q]);
+            hl[q] = mfma(Al, hb[k][t][q], hl[q]);
+          }
+        }
+        if (k == nk - 1) signal();
+        const int hx = 16 * ob + (lane & 15);
+        if (hx < nx) {
+          const float hws = hwsk[k];
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const float tot = 256.0f * (float)fold3(hh[0][i], hh[1][i], hh[2][i]) +
+                              (float)fold3(hl[0][i], hl[1][i], hl[2][i]) + hws;
+            const uint32_t q = min(__float2uint_rz(fmaf(tot, 1.0f / 4194304.0f, 0.5f)), 65535u);
+            const int yl = 4 * (lane >> 4) + i;
+            if (fast8) {
+              const int sh = (int)((sh0 + (uint32_t)(16 * b + yl) * shs) & 3u);
+              ot[yl * kOt8Pitch + sh + 3 * hx + chn] = (uint8_t)q16_to_u8(q);
+            } else {
+              otile[yl * kVmOtilePitch + 3 * hx + chn] = (uint16_t)q;
+            }
+          }
+        }
+      }
+      stamp(2);
+    } else if (M != 1 && M != 2 && p < N + 1) {
+      // no block this phase (p == 0): count the (empty) plane reads
+      if (lane == 0) atomicAdd(static_cast<unsigned *>(__builtin_assume_aligned(lds + O.cnt, 16)), 1u);
+    }
+    stamp(3);
+    if (p < N) rH = read_rec(p);
+    phase_barrier();
+    stamp(4);
+  }
+  stamp_out(5);
+}
+
+int vr_read_stamps(uint64_t *out, int slots) {
+  if (slots > kVrStampSlots) slots = kVrStampSlots;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vr_stamps), (size_t)slots * kVrStampN * sizeof(uint64_t)) == hipSuccess
+             ? 0
+             : -1;
+}
+
+// LDS of a launch: the ring takes what the other regions leave (R a multiple
+// of 32, at most 256 rows); R = 0 when even the smallest ring does not fit
+VrLayout vr_lds_layout(int vpitch, bool q16) {
+  VrLayout L{};
+  L.plane = 16 * vpitch + kPlanePad;
+  L.otile_bytes = ((q16 ? kVmOtileBytes : 16 * kOt8Pitch) + 15) & ~15;
+  const int rest = 2 * kABytes + 8 * kRecBytes + 16 + kLutSlots * 1024 + 6 * L.plane;
+  const int fixed = ((rest + 15) & ~15) + 2 * L.otile_bytes;
+  int R = (kVpMaxLds - fixed) / 512 / 32 * 32;
+  if (R > 256) R = 256;
+  static const char *rmax = getenv("FI_VR_R");  // tuning: cap the ring
+  if (rmax && atoi(rmax) >= 160 && R > atoi(rmax) / 32 * 32) R = atoi(rmax) / 32 * 32;
+  if (R < 160) R = 0;
+  L.R = R;
+  L.otile_off = (R * 512 + rest + 15) & ~15;
+  L.total = L.otile_off + 2 * L.otile_bytes;
+  return L;
+}
+
+int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrTile *tiles, int ntiles,
+              const int32_t *wginfo, int G, const int32_t *ai, VrLayout L) {
+  if (ntiles <= 0 || G <= 0) return 0;
+  if (L.R <= 0 || L.total > kVpMaxLds) return -1;
+  static const char *variant = getenv("FI_VR_VARIANT");  // profiling ablations only
+  const int v = variant ? atoi(variant) : 0;
+#define FI_VR_LAUNCH(m) \
+  hipLaunchKernelGGL((k_rs_vr<m>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, wginfo, ai, L)
+  switch (v) {
+    case 1: FI_VR_LAUNCH(1); break;
+    case 2: FI_VR_LAUNCH(2); break;
+    case 3: FI_VR_LAUNCH(3); break;
+    case 9: FI_VR_LAUNCH(9); break;
+    case 11: FI_VR_LAUNCH(11); break;
+    case 12: FI_VR_LAUNCH(12); break;
+    case 13: FI_VR_LAUNCH(13); break;
+    default: FI_VR_LAUNCH(0); break;
+  }
+#undef FI_VR_LAUNCH
+  return 0;
+}
+
+}  // namespace fi

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""k_rs_vp vs k_rs_vm: the persistent warp-specialised resample must be
-bit-identical to the streaming kernel it replaces (same tables, same integer
-algebra) on every geometry class, and within +-1 LSB of the oracle.
+"""k_rs_vp / k_rs_vr vs k_rs_vm: the persistent resample kernels must be
+bit-identical to the streaming kernel they replace (same weights, same integer
+algebra) on every geometry class.
 
-  python tools/vp_check.py            (GPU; prints one line per case)
+  python tools/vp_check.py            (GPU; k_rs_vp)
+  VR=1 python tools/vp_check.py       (GPU; k_rs_vr, block-major)
 """
 import os
 import sys
@@ -43,19 +44,25 @@ CASES = [
     (2000, 1500, "w_640,h_480,c_1,mnchr_1", 1),
     (333, 517, "w_97", 4),
     (4000, 3000, "w_150", 2),
+    (3840, 2160, "w_512,h_512,c_1", 300),
+    (1920, 1080, "w_500", 300),
+    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", 24),
+    (640, 480, "w_320", 7),
 ]
 
-vm = ctx_with({"FI_VP_RS": "0"})
-vp = ctx_with({"FI_VP_RS": "1"})
+VR = os.environ.get("VR") == "1"
+KEY, PATH = ("FI_VR_RS", "path_vr") if VR else ("FI_VP_RS", "path_vp")
+vm = ctx_with({"FI_VP_RS": "0", "FI_VR_RS": "0"})
+vp = ctx_with({KEY: "1"})
 bad = 0
 for (W, H, opts, n) in CASES:
     op = ImageProcessor(OptionsBag(opts), W, H).to_op()
     srcs = [synth_rgb(W, H, 77 + k) for k in range(min(n, 4))]
     srcs = [srcs[k % len(srcs)] for k in range(n)]
-    before = vp.stats("path_vp")[1]
+    before = vp.stats(PATH)[1]
     oa, ra, rca = vm.process(srcs, [op] * n)
     ob, rb, rcb = vp.process(srcs, [op] * n)
-    ran = vp.stats("path_vp")[1] - before
+    ran = vp.stats(PATH)[1] - before
     same = all(a is not None and b is not None and np.array_equal(a, b) for a, b in zip(oa, ob))
     diff = 0
     if not same:

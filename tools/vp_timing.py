@@ -8,8 +8,9 @@ import ctypes
 import os
 import sys
 
-os.environ["FI_VP_VARIANT"] = os.environ.get("VP_STAMP_VARIANT", "9")
-os.environ["FI_VP_RS"] = "1"
+VR = os.environ.get("VR") == "1"  # k_rs_vr instead of k_rs_vp
+os.environ["FI_VR_VARIANT" if VR else "FI_VP_VARIANT"] = os.environ.get("VP_STAMP_VARIANT", "9")
+os.environ["FI_VR_RS" if VR else "FI_VP_RS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 
@@ -18,7 +19,7 @@ from flyimg_amd.processor import ImageProcessor, OptionsBag  # noqa: E402
 from flyimg_amd.runtime import Context  # noqa: E402
 from flyimg_amd.runtime import plan as fi_plan  # noqa: E402
 
-W, H, n = 1920, 1080, int(os.environ.get("NIMG", "1024"))
+W, H, n = int(os.environ.get("VP_W", "1920")), int(os.environ.get("VP_H", "1080")), int(os.environ.get("NIMG", "1024"))
 op = ImageProcessor(OptionsBag(os.environ.get("VP_OPTS", "w_500")), W, H).to_op()
 stride = (W * 3 + 15) // 16 * 16
 ow, oh, oc = fi_plan(W, H, op)
@@ -38,8 +39,9 @@ with Context(0) as ctx:
         L.check(ctx.process_device(arr, n))
     NS = 16 * 6
     buf = np.zeros(256 * NS, np.uint64)
-    L.lib().fi_debug_vp_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
-    L.check(L.lib().fi_debug_vp_stamps(ctx.h, buf.ctypes.data, 256))
+    fn = L.lib().fi_debug_vr_stamps if VR else L.lib().fi_debug_vp_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
+    L.check(fn(ctx.h, buf.ctypes.data, 256))
     a = buf.reshape(256, 16, 6).astype(np.float64)
     a = a[a[:, 0, 5] > 0]
     ph = a[:, 0, 5].mean()
