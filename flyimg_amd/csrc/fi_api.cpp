@@ -1541,7 +1541,10 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   bool q16 = false;
   int64_t nst = 0;
   for (const VrWork &w : work) {
-    for (int st = 0; st < w.nstrips; st++) vpitch = std::max(vpitch, Bp.vstrips[w.first_strip + st].vpitch);
+    for (int st = 0; st < w.nstrips; st++) {
+      vpitch = std::max(vpitch, Bp.vstrips[w.first_strip + st].vpitch);
+      if (Bp.vstrips[w.first_strip + st].nocb > 3) return false;  // five H waves, two items each
+    }
     const VDesc &d = Bp.vdescs[w.img];
     q16 = q16 || d.gray || d.rot != 0;
     nst += w.nstrips;

@@ -50,9 +50,10 @@ typedef __attribute__((address_space(3))) i32x2 l_i32x2;
 typedef __attribute__((address_space(3))) uint8_t l_u8;
 
 constexpr int kVW = 8;                   // V waves: 64 source bytes (4 column tiles) each
-constexpr int kHW = 6;                   // H waves 8-13
+constexpr int kHW = 5;                   // H waves 8-12: horizontal items hw, hw + 5 (3 nocb <= 10)
+constexpr int kSW = 1;                   // S wave 13: the stores of the output tile of phase p - 2
 constexpr int kLW = 2;                   // L waves 14-15
-static_assert(kVW + kHW + kLW == 16, "16 waves");
+static_assert(kVW + kHW + kSW + kLW == 16, "16 waves");
 constexpr int kABytes = 6144 + 64;       // [t][limb][64 lanes][16 B] + w128 of the block's 16 rows
 constexpr int kRecBytes = 32;
 constexpr int kLutSlots = 4;
@@ -114,21 +115,28 @@ __device__ __forceinline__ void dma16(uint32_t m0, const uint8_t *sbase, uint32_
       : "v"(voff), "s"(sbase), "s"(m0)
       : "memory");
 }
-// the same DMA with a different asm text: keeps hipcc from tail-merging the
-// row stream's load-free loop into the table-lookup path (whose scalar-load
-// wait would then run before every DMA)
-__device__ __forceinline__ void dma16_fast(uint32_t m0, const uint8_t *sbase, uint32_t voff) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2 ; row stream\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(m0)
-      : "memory");
-}
+// the row stream's DMA, one asm text per lane pattern: keeps hipcc from
+// tail-merging the four sites (a merged site selects its operand with VALU)
+// or merging them into the table-lookup path (whose scalar-load wait would
+// then run before every DMA)
+#define FI_VR_DMA_TAG(name, tag)                                                    \
+  __device__ __forceinline__ void name(uint32_t m0, const uint8_t *sbase, uint32_t voff) { \
+    unsigned keep;                                                                  \
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"                \
+                 "global_load_lds_dwordx4 %1, %2 ; " tag "\n\ts_mov_b32 m0, %0"       \
+                 : "=&s"(keep)                                                      \
+                 : "v"(voff), "s"(sbase), "s"(m0)                                   \
+                 : "memory");                                                       \
+  }
+FI_VR_DMA_TAG(dma16_p0, "p0")
+FI_VR_DMA_TAG(dma16_p1, "p1")
+FI_VR_DMA_TAG(dma16_p2, "p2")
+FI_VR_DMA_TAG(dma16_p3, "p3")
+FI_VR_DMA_TAG(dma16_p4, "p4")
+FI_VR_DMA_TAG(dma16_p5, "p5")
+FI_VR_DMA_TAG(dma16_p6, "p6")
+FI_VR_DMA_TAG(dma16_p7, "p7")
+#undef FI_VR_DMA_TAG
 __device__ __forceinline__ void phase_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // s_waitcnt vmcnt(n): the wave's n youngest vector-memory operations may stay
@@ -255,9 +263,9 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     return Rec{ufl(x.t), ufl(x.blk), ufl(x.flags), ufl(x.slot0), ufl(x.ks), ufl(x.grend), 0, 0};
   };
 
-  if (wv >= kVW + kHW) {
-    // ============ L role: phase records, row stream, A fragments, stores ============
-    const int li = wv - (kVW + kHW);
+  if (wv >= kVW + kHW + kSW) {
+    // ============ L role: phase records, row stream, A fragments ============
+    const int li = wv - (kVW + kHW + kSW);
     const int h = lane >> 5;  // half-wave: the two rows of one 1-KB DMA
     // ---- phase cursor (records, A fragments) ----
     struct PI {
@@ -336,6 +344,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     };
     if (rt < ntiles) rtile_load();
     const uint32_t lane_c = (uint32_t)((lane & 31) ^ h);  // chunk of this lane before the row swizzle
+    uint32_t pat[4] = {0, 0, 0, 0};                          // fast-path lane offsets of tile pat_tile
+    int pat_tile = -1;
     // issue this wave's pairs up to stream row `limit`; returns the DMAs issued.
     // Evenly spaced rows (rstep > 0) go through a loop with no loads: bases
     // linear in the pair index, the chunk swizzle from the ring slot.
@@ -354,15 +364,76 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           const int cnt = min((seg - rG + 3) >> 2, (r_nrows - 1 - k0 + 3) >> 2);
           const int64_t rs = (int64_t)r_rstep * r_stride;
           const uint8_t *base = r_src + (int64_t)(r_row0 + r_rstep * k0) * r_stride + r_b0;
-          const uint32_t hoff = h ? (uint32_t)rs : 0u;
-          for (int i = 0; i < cnt; i++) {
-            const uint32_t f = (uint32_t)((rslot & 7) | (((rslot >> 4) & 1) << 3));
-            uint32_t lc = lane_c ^ f;
-            if (16 * (int)lc >= r_nbytes) lc = 0;
-            dma16_fast(lds_addr(lds) + (uint32_t)(O.ring + rslot * 512), base, hoff + 16u * lc);
-            base += 4 * rs;
-            rslot += 4;
-            if (rslot >= R) rslot -= R;
+          if (pat_tile != rt) {
+            // this wave's own pair starts 2 li + 4 m have the chunk swizzle
+            // f = 2 li + 4 (m & 1) + 8 ((m >> 2) & 1): four lane patterns per tile
+            pat_tile = rt;
+            const uint32_t hoff = h ? (uint32_t)rs : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+              uint32_t lc = lane_c ^ (uint32_t)(2 * li + 4 * (q & 1) + 8 * (q >> 1));
+              if (16 * (int)lc >= r_nbytes) lc = 0;
+              pat[q] = hoff + 16u * lc;
+            }
+          }
+          // straight-line DMAs: own pair m of the 8-pair cycle (m & 7) has lane
+          // pattern (m & 1) | ((m >> 2) & 1) << 1, and a cycle never crosses the
+          // ring end (R is a multiple of 32 rows), so the wrap is checked per cycle
+          {
+            const int rslot0 = rslot;
+            uint32_t m0 = lds_addr(lds) + (uint32_t)(O.ring + rslot * 512);
+            int left = cnt, ph = (rslot >> 2) & 7;
+            for (;;) {
+              switch (ph) {
+              case 0:
+                dma16_p0(m0, base, pat[0]);
+                base += 4 * rs;
+                m0 += 2048;
+                if (--left == 0) goto stream_done;
+              case 1:
+                dma16_p1(m0, base, pat[1]);
+                base += 4 * rs;
+                m0 += 2048;
+                if (--left == 0) goto stream_done;
+              case 2:
+                dma16_p2(m0, base, pat[0]);
+                base += 4 * rs;
+                m0 += 2048;
+                if (--left == 0) goto stream_done;
+              case 3:
+                dma16_p3(m0, base, pat[1]);
+                base += 4 * rs;
+                m0 += 2048;
+                if (--left == 0) goto stream_done;
+              case 4:
+                dma16_p4(m0, base, pat[2]);
+                base += 4 * rs;
+                m0 += 2048;
+                if (--left == 0) goto stream_done;
+              case 5:
+                dma16_p5(m0, base, pat[3]);
+                base += 4 * rs;
+                m0 += 2048;
+                if (--left == 0) goto stream_done;
+              case 6:
+                dma16_p6(m0, base, pat[2]);
+                base += 4 * rs;
+                m0 += 2048;
+                if (--left == 0) goto stream_done;
+              case 7:
+                dma16_p7(m0, base, pat[3]);
+                base += 4 * rs;
+                m0 += 2048;
+                if (--left == 0) goto stream_done;
+              }
+              ph = 0;
+              int r2 = rslot0 + 4 * (cnt - left);  // the next cycle's first pair
+              while (r2 >= R) r2 -= R;
+              m0 = lds_addr(lds) + (uint32_t)(O.ring + r2 * 512);
+            }
+          stream_done:
+            rslot = rslot0 + 4 * cnt;
+            while (rslot >= R) rslot -= R;
           }
           n += cnt;
           rG += 4 * cnt;
@@ -403,118 +474,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     phase_barrier();  // records 0 / 1, A(0), the rows of block 0 and the first LUT visible
     phase_barrier();
     if (kStamp) tprev = __builtin_amdgcn_s_memtime();
-    int stile = -1;  // tile of the cached store descriptors
-    struct StoreD {
-      uint8_t *dst;
-      int64_t dst_stride;
-      int32_t ew, eh, rot, gray, x0, x1;
-    } sD{};
     for (int p = 0; p < N + 2; p++) {
-      // stores of the block of phase p - 2 (output tile slot (p - 2) & 1): dword-
-      // aligned 8-bit segments go after this phase's DMAs (their count enters the
-      // end-of-phase vmcnt), the other output kinds before them
-      bool st_fast = false;
-      uint8_t *st_row0 = nullptr;
-      int64_t st_stride = 0;
-      int st_nb = 0, st_nrow = 0;
-      const uint8_t *st_ot = nullptr;
-      if (p >= 2 && p - 2 < N && M != 3 && M != 1 && M != 2) {
-        const Rec rs = read_rec(p - 2);
-        if (stile != rs.t) {
-          stile = rs.t;
-          const VrTile T = ldc(tiles + rs.t);
-          const VDesc D0 = ldc(descs + T.img);
-          const MStrip S0 = ldc(strips + T.strip);
-          sD = StoreD{D0.dst, D0.dst_stride, D0.ew, D0.eh, D0.rot, D0.gray, S0.x0, S0.x1};
-        }
-        const StoreD &D = sD;
-        const int b = rs.blk;
-        const int nx = D.x1 - D.x0;
-        const int oc = D.gray ? 1 : 3;
-        const int rows_here = min(16, D.eh - 16 * b);
-        const int nb = nx * oc;
-        uint8_t *ot = otiles + ((rs.flags & kSlot) ? Lo.otile_bytes : 0);
-        const uint16_t *otile = reinterpret_cast<const uint16_t *>(ot);
-        const bool fastA = !D.gray && D.rot == 0 && (((uintptr_t)D.dst + (uint64_t)D.x0 * 3) & 3u) == 0 &&
-                           (D.dst_stride & 3) == 0 && (nb & 3) == 0;
-        auto out_byte = [&](int yl, int k) -> uint32_t {
-          const uint16_t *o = otile + yl * kVmOtilePitch;
-          if (!D.gray) return q16_to_u8(o[k]);
-          return q16_to_u8(gray_q16(o[3 * k], o[3 * k + 1], o[3 * k + 2]));
-        };
-        if (fastA) {
-          st_fast = true;
-          st_row0 = D.dst + (int64_t)(16 * b + li) * D.dst_stride + (int64_t)D.x0 * 3;
-          st_stride = (int64_t)kLW * D.dst_stride;
-          st_nb = nb;
-          st_nrow = (rows_here - li + kLW - 1) / kLW;
-          st_ot = ot + li * kOt8Pitch;
-        } else if (D.gray == 2) {
-          for (int it = tid - 64 * (kVW + kHW); it < rows_here * nx; it += 64 * kLW) {
-            const int yl = it / nx, x = it - yl * nx;
-            const uint16_t *o = otile + yl * kVmOtilePitch + 3 * x;
-            ((g_u16 *)(D.dst + (int64_t)(16 * b + yl) * D.dst_stride))[D.x0 + x] = (uint16_t)gray_q16(o[0], o[1], o[2]);
-          }
-        } else if (!D.gray && D.rot == 0) {
-          // 8-bit tile, rows shifted to the destination's address mod 4: L wave li
-          // copies rows li, li + 2, ..., one destination dword per lane
-          const uint32_t sh0 = (uint32_t)(((uintptr_t)D.dst + (uint64_t)D.x0 * 3) & 3u);
-          const uint32_t shs = (uint32_t)(D.dst_stride & 3);
-          constexpr int kRows = 16 / kLW;
-          uint32_t wd[kRows];
-#pragma unroll
-          for (int r = 0; r < kRows; r++) wd[r] = *reinterpret_cast<const uint32_t *>(ot + (li + kLW * r) * kOt8Pitch + 4 * lane);
-#pragma unroll
-          for (int r = 0; r < kRows; r++) {
-            const int yl = li + kLW * r;
-            if (yl >= rows_here) break;
-            const int sh = (int)((sh0 + (uint32_t)(16 * b + yl) * shs) & 3u);
-            const int k0 = 4 * lane - sh;
-            uint8_t *a0 = D.dst + (int64_t)(16 * b + yl) * D.dst_stride + (int64_t)D.x0 * 3;
-            if (k0 >= 0 && k0 + 4 <= nb) {
-              *(g_u32 *)(a0 + k0) = wd[r];
-            } else if (k0 < nb && k0 + 4 > 0) {
-#pragma unroll
-              for (int j = 0; j < 4; j++)
-                if (k0 + j >= 0 && k0 + j < nb) *(g_u8 *)(a0 + k0 + j) = (uint8_t)(wd[r] >> (8 * j));
-            }
-          }
-        } else if (D.rot == 0) {
-          const int ndw = (nb + 3) / 4 + 1;
-          const float inv = 1.0f / (float)ndw;
-          for (int it = tid - 64 * (kVW + kHW); it < rows_here * ndw; it += 64 * kLW) {
-            const int yl = (int)(((float)it + 0.5f) * inv), d = it - yl * ndw;
-            uint8_t *a0 = D.dst + (int64_t)(16 * b + yl) * D.dst_stride + (int64_t)D.x0 * oc;
-            const int k0 = 4 * d - (int)((uintptr_t)a0 & 3u);
-            if (k0 >= nb) continue;
-            if (k0 >= 0 && k0 + 4 <= nb) {
-              const uint32_t wd = out_byte(yl, k0) | (out_byte(yl, k0 + 1) << 8) | (out_byte(yl, k0 + 2) << 16) |
-                                  (out_byte(yl, k0 + 3) << 24);
-              *(g_u32 *)(a0 + k0) = wd;
-            } else {
-              for (int k = max(k0, 0); k < min(k0 + 4, nb); k++) *(g_u8 *)(a0 + k) = (uint8_t)out_byte(yl, k);
-            }
-          }
-        } else {
-          for (int it = tid - 64 * (kVW + kHW); it < rows_here * nx; it += 64 * kLW) {
-            const int yl = it / nx, x = it - yl * nx, y = 16 * b + yl;
-            const int ox = D.x0 + x;
-            int dx, dy;
-            if (D.rot == 90) {
-              dx = D.eh - 1 - y;
-              dy = ox;
-            } else if (D.rot == 180) {
-              dx = D.ew - 1 - ox;
-              dy = D.eh - 1 - y;
-            } else {  // 270
-              dx = y;
-              dy = D.ew - 1 - ox;
-            }
-            g_u8 *out = (g_u8 *)(D.dst + (int64_t)dy * D.dst_stride) + dx * oc;
-            for (int c = 0; c < oc; c++) out[c] = (uint8_t)out_byte(yl, x * oc + c);
-          }
-        }
-      }
       // A fragments of block p + 1 (its record was written last phase)
       if (M != 1 && p + 1 < N) issue_a(P1, (p + 1) & 1);
       stamp(0);
@@ -527,22 +487,9 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         n_issued += nr;
       }
       stamp(1);
-      // dword-aligned fast8 stores of block p - 2: rows li, li + 2, ... as dwords
-      int ns = 0;
-      if (st_fast) {
-        const int U = st_nb >> 2;
-        const float invU = 1.0f / (float)U;
-        for (int it0 = 0; it0 < st_nrow * U; it0 += 64, ns++) {
-          const int it = it0 + lane;
-          if (it < st_nrow * U) {
-            const int r = (int)(((float)it + 0.5f) * invU), u = it - r * U;
-            *(g_u32 *)(st_row0 + r * st_stride + 4 * u) =
-                *reinterpret_cast<const uint32_t *>(st_ot + r * kLW * kOt8Pitch + 4 * u);
-          }
-        }
-      }
+      const int ns = 0;
       // block p + 1's rows (every own pair starting below its Rend), A(p + 1) and
-      // the LUTs landed; younger row pairs and this phase's stores may stay in flight
+      // the LUTs landed; younger row pairs may stay in flight
       if (p + 1 < N) {
         const int after = max(0, n_issued - own_below(P1.grend));
         wait_vm_le(min(after, nr) + ns);
@@ -642,7 +589,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         stamp(1);
         // the H waves' reads of block p - 1's planes are done (single plane buffer)
         if (M != 2) {
-          const uint32_t want = 6u * (uint32_t)(p + 1);
+          const uint32_t want = (uint32_t)kHW * (uint32_t)(p + 1);
           while (hcnt[0] < want) __builtin_amdgcn_s_sleep(1);
         }
         // block done: ClampToQuantum(257 acc / 2^22) -> Q16 hi / lo signed-byte planes
@@ -671,6 +618,141 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       stamp(3);
     }
     stamp_out(4);
+    return;
+  }
+
+  if (wv == kVW + kHW) {
+    // =================== S role: the output stores ===================
+    const int sw = 0;
+    int stile = -1;  // tile of the cached store descriptors
+    struct StoreD {
+      uint8_t *dst;
+      int64_t dst_stride;
+      int32_t ew, eh, rot, gray, x0, x1;
+    } sD{};
+    phase_barrier();
+    phase_barrier();
+    for (int p = 0; p < N + 2; p++) {
+      // stores of the block of phase p - 2 (output tile slot (p - 2) & 1): on
+      // the loader waves their issue held back the row stream
+      bool st_fast = false;
+      uint8_t *st_row0 = nullptr;
+      int64_t st_stride = 0;
+      int st_nb = 0, st_nrow = 0;
+      const uint8_t *st_ot = nullptr;
+      if (p >= 2 && p - 2 < N && M != 3 && M != 1 && M != 2) {
+        const Rec rs = read_rec(p - 2);
+        if (stile != rs.t) {
+          stile = rs.t;
+          const VrTile T = ldc(tiles + rs.t);
+          const VDesc D0 = ldc(descs + T.img);
+          const MStrip S0 = ldc(strips + T.strip);
+          sD = StoreD{D0.dst, D0.dst_stride, D0.ew, D0.eh, D0.rot, D0.gray, S0.x0, S0.x1};
+        }
+        const StoreD &D = sD;
+        const int b = rs.blk;
+        const int nx = D.x1 - D.x0;
+        const int oc = D.gray ? 1 : 3;
+        const int rows_here = min(16, D.eh - 16 * b);
+        const int nb = nx * oc;
+        uint8_t *ot = otiles + ((rs.flags & kSlot) ? Lo.otile_bytes : 0);
+        const uint16_t *otile = reinterpret_cast<const uint16_t *>(ot);
+        const bool fastA = !D.gray && D.rot == 0 && (((uintptr_t)D.dst + (uint64_t)D.x0 * 3) & 3u) == 0 &&
+                           (D.dst_stride & 3) == 0 && (nb & 3) == 0;
+        auto out_byte = [&](int yl, int k) -> uint32_t {
+          const uint16_t *o = otile + yl * kVmOtilePitch;
+          if (!D.gray) return q16_to_u8(o[k]);
+          return q16_to_u8(gray_q16(o[3 * k], o[3 * k + 1], o[3 * k + 2]));
+        };
+        if (fastA) {
+          st_fast = true;
+          st_row0 = D.dst + (int64_t)(16 * b + sw) * D.dst_stride + (int64_t)D.x0 * 3;
+          st_stride = (int64_t)kSW * D.dst_stride;
+          st_nb = nb;
+          st_nrow = (rows_here - sw + kSW - 1) / kSW;
+          st_ot = ot + sw * kOt8Pitch;
+        } else if (D.gray == 2) {
+          for (int it = tid - 64 * (kVW + kHW); it < rows_here * nx; it += 64 * kSW) {
+            const int yl = it / nx, x = it - yl * nx;
+            const uint16_t *o = otile + yl * kVmOtilePitch + 3 * x;
+            ((g_u16 *)(D.dst + (int64_t)(16 * b + yl) * D.dst_stride))[D.x0 + x] = (uint16_t)gray_q16(o[0], o[1], o[2]);
+          }
+        } else if (!D.gray && D.rot == 0) {
+          // 8-bit tile, rows shifted to the destination's address mod 4: store wave
+          // sw copies rows sw, sw + kSW, ..., one destination dword per lane
+          const uint32_t sh0 = (uint32_t)(((uintptr_t)D.dst + (uint64_t)D.x0 * 3) & 3u);
+          const uint32_t shs = (uint32_t)(D.dst_stride & 3);
+          constexpr int kRows = (16 + kSW - 1) / kSW;
+          uint32_t wd[kRows];
+  #pragma unroll
+          for (int r = 0; r < kRows; r++) wd[r] = sw + kSW * r < 16 ? *reinterpret_cast<const uint32_t *>(ot + (sw + kSW * r) * kOt8Pitch + 4 * lane) : 0u;
+  #pragma unroll
+          for (int r = 0; r < kRows; r++) {
+            const int yl = sw + kSW * r;
+            if (yl >= rows_here) break;
+            const int sh = (int)((sh0 + (uint32_t)(16 * b + yl) * shs) & 3u);
+            const int k0 = 4 * lane - sh;
+            uint8_t *a0 = D.dst + (int64_t)(16 * b + yl) * D.dst_stride + (int64_t)D.x0 * 3;
+            if (k0 >= 0 && k0 + 4 <= nb) {
+              *(g_u32 *)(a0 + k0) = wd[r];
+            } else if (k0 < nb && k0 + 4 > 0) {
+  #pragma unroll
+              for (int j = 0; j < 4; j++)
+                if (k0 + j >= 0 && k0 + j < nb) *(g_u8 *)(a0 + k0 + j) = (uint8_t)(wd[r] >> (8 * j));
+            }
+          }
+        } else if (D.rot == 0) {
+          const int ndw = (nb + 3) / 4 + 1;
+          const float inv = 1.0f / (float)ndw;
+          for (int it = tid - 64 * (kVW + kHW); it < rows_here * ndw; it += 64 * kSW) {
+            const int yl = (int)(((float)it + 0.5f) * inv), d = it - yl * ndw;
+            uint8_t *a0 = D.dst + (int64_t)(16 * b + yl) * D.dst_stride + (int64_t)D.x0 * oc;
+            const int k0 = 4 * d - (int)((uintptr_t)a0 & 3u);
+            if (k0 >= nb) continue;
+            if (k0 >= 0 && k0 + 4 <= nb) {
+              const uint32_t wd = out_byte(yl, k0) | (out_byte(yl, k0 + 1) << 8) | (out_byte(yl, k0 + 2) << 16) |
+                                  (out_byte(yl, k0 + 3) << 24);
+              *(g_u32 *)(a0 + k0) = wd;
+            } else {
+              for (int k = max(k0, 0); k < min(k0 + 4, nb); k++) *(g_u8 *)(a0 + k) = (uint8_t)out_byte(yl, k);
+            }
+          }
+        } else {
+          for (int it = tid - 64 * (kVW + kHW); it < rows_here * nx; it += 64 * kSW) {
+            const int yl = it / nx, x = it - yl * nx, y = 16 * b + yl;
+            const int ox = D.x0 + x;
+            int dx, dy;
+            if (D.rot == 90) {
+              dx = D.eh - 1 - y;
+              dy = ox;
+            } else if (D.rot == 180) {
+              dx = D.ew - 1 - ox;
+              dy = D.eh - 1 - y;
+            } else {  // 270
+              dx = y;
+              dy = D.ew - 1 - ox;
+            }
+            g_u8 *out = (g_u8 *)(D.dst + (int64_t)dy * D.dst_stride) + dx * oc;
+            for (int c = 0; c < oc; c++) out[c] = (uint8_t)out_byte(yl, x * oc + c);
+          }
+        }
+      }
+      // dword-aligned fast8 stores of block p - 2: rows sw, sw + kSW, ... as dwords
+      if (st_fast) {
+        const int U = st_nb >> 2;
+        const float invU = 1.0f / (float)U;
+        for (int it0 = 0; it0 < st_nrow * U; it0 += 64) {
+          const int it = it0 + lane;
+          if (it < st_nrow * U) {
+            const int r = (int)(((float)it + 0.5f) * invU), u = it - r * U;
+            *(g_u32 *)(st_row0 + r * st_stride + 4 * u) =
+                *reinterpret_cast<const uint32_t *>(st_ot + r * kSW * kOt8Pitch + 4 * u);
+          }
+        }
+      }
+
+      phase_barrier();
+    }
     return;
   }
 

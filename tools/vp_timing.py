@@ -46,7 +46,7 @@ with Context(0) as ctx:
     a = a[a[:, 0, 5] > 0]
     ph = a[:, 0, 5].mean()
     roles = {"V": (range(0, 8), ["tile entry", "V-MFMA issue", "planes", "barrier"]),
-             "H": (range(8, 14), ["-", "rec+frags", "horizontal", "stores", "barrier"]),
+             "H": (range(8, 13 if VR else 14), ["-", "rec+frags", "horizontal", "stores", "barrier"]),
              "L": (range(14, 16), ["stores+A DMA", "piece DMA", "vmcnt wait", "barrier"])}
     print(f"{len(a)} workgroups, phases/WG {ph:.0f}; per-phase ticks by wave (mean over workgroups)")
     for r, (waves, names) in roles.items():
