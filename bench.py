@@ -67,10 +67,8 @@ def cfg4_list(n=65536, seed=20250112):
 
 KERNEL_OF_PATH = {
     "path_vm": "k_rs_vm (streaming exact-integer MFMA, vertical first)",
-    "path_vp": "k_rs_vp (persistent warp-specialised exact-integer MFMA, vertical first)",
     "path_vr": "k_rs_vr (persistent block-major exact-integer MFMA, vertical first)",
     "path_hv": "k_rs_hv (streaming exact-integer MFMA, horizontal first)",
-    "path_fused": "k_rs_fused (VALU, vertical first)",
     "path_generic_v": "k_rs_v_u8 + k_rs_h_final (two-pass)",
     "path_generic_h": "k_rs_h_u8 + k_rs_v_final (two-pass)",
     "path_copy": "k_rs_copy",

@@ -42,9 +42,7 @@ __global__ void k_sc_hpass(const ScDesc *, const int32_t *, int, const int32_t *
 __global__ void k_sc_vpass(const ScDesc *, const int32_t *, int, const int32_t *);
 __global__ void k_sc_maps(const ScDesc *, const int32_t *, int, const ScParamsDev);
 // per-image smartcrop kernels (fi_smartcrop.hip)
-int launch_sc_h(hipStream_t s, bool mfma, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai);
-int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
-                const ScParamsDev &P);
+int launch_sc_h(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai);
 int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
                  const ScParamsDev &P);
 int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
@@ -73,26 +71,19 @@ int launch_mono(hipStream_t s, const MonoDesc *descs, int n, const double *wts);
 // streaming exact-integer MFMA resample (fi_vm.hip)
 size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16);
 int vm_read_stamps(uint64_t *out, int slots);
-int vp_read_stamps(uint64_t *out, int slots);
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
 // its persistent warp-specialised form (fi_vp.hip)
-VpLayout vp_lds_layout(int vpitch, bool q16);
 VrLayout vr_lds_layout(int vpitch, bool q16);
 int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrTile *tiles, int ntiles,
               const int32_t *wginfo, int G, const int32_t *ai, VrLayout L);
 int vr_read_stamps(uint64_t *out, int slots);
-int launch_vp(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
-              const int32_t *nphase, int G, const int32_t *ai, VpLayout L);
 // streaming exact-integer MFMA resample, horizontal first (fi_hv.hip)
 size_t hv_lds_bytes(int pp, int nocb);
 int launch_hv(hipStream_t s, const HvDesc *descs, const HvStripD *strips, const HvTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
 // face-blur pixelation (fi_pixelate.hip)
 int launch_pix(hipStream_t s, int mode, const PixPass &P, const int32_t *ai, const double *ad);
-// fused vertical-first VALU resample (fi_fused.hip)
-int launch_fused(hipStream_t s, int K, const ResizeDesc *descs, const FusedTile *tiles, int ntiles,
-                 const int32_t *ai, const float *af, int hw_pitch, int max_taps, int max_nbytes);
 }  // namespace fi
 
 using namespace fi;
@@ -136,11 +127,6 @@ struct TimedRange {
   double bytes;
 };
 
-struct StripTab {
-  FusedTile t;
-  std::vector<int32_t> starts;  // [nx]
-  std::vector<float> wT;        // [htaps][nx]
-};
 // A host-buffer batch (fi_submit_batch / fi_process_batch): the caller's
 // records, the device-side records run_batch fills, and where each output
 // goes -- straight into a pinned caller dst, or through the slot's pinned
@@ -220,18 +206,10 @@ struct fi_ctx {
   std::map<std::tuple<int, uint64_t, int, int, int, int, int, int>, AxisTable> axis_cache;
   std::map<std::tuple<int, int, int, int, uint64_t>, ScPlan> sc_cache;
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
-  std::map<const AxisTable *, RingTable> ring_cache;
-  std::map<const AxisTable *, std::vector<StripTab>> strip_cache;
-  bool fused = true;    // FI_DISABLE_FUSED=1 forces the generic two-pass resample
-  bool vm_rs = true;     // FI_DISABLE_VM_RS=1: no k_rs_vm (streaming MFMA resample, the default)
-  bool vp_rs = false;    // FI_VP_RS=1: k_rs_vm's tiles run on the persistent k_rs_vp
-  bool vr_rs = false;    // FI_VR_RS=1: images with block-major tables take the persistent k_rs_vr
+  bool fast_rs = true;  // FI_FORCE_GENERIC=1: the generic two-pass resample (and smartcrop) kernels only
+  bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
   int n_cu = 256;        // compute units (k_rs_vp: one persistent workgroup per CU)
-  bool hv_rs = true;     // FI_DISABLE_HV_RS=1: horizontal-first geometries take the generic two-pass kernels
-  bool sc_lds_maps = true;  // FI_SC_LDS_MAPS=0: k_sc_score2 reads the maps from global memory
-  bool sc_vq = true;        // FI_DISABLE_SC_VQ=1: k_sc_vmaps (VALU vertical pass) instead of k_sc_vq
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
-  bool sc_skinsat = true;   // FI_DISABLE_SC_SKINSAT=1: k_sc_fz evaluates skin / saturation per pixel (f64)
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
   DevBuf jpeg[3];           // GPU JPEG decode: upload (compressed data + tables), -, coefficients + planes
   void *jpeg_host = nullptr;  // its pinned staging
@@ -263,8 +241,6 @@ struct fi_ctx {
   std::map<const AxisTable *, int32_t> axis_wd_at;  // f64 weights (RGBA path) in heap_d
   std::map<const ScPlan *, ScTabs> sc_at;
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_at;
-  std::map<const RingTable *, std::array<int32_t, 4>> ring_at;
-  std::map<const StripTab *, std::pair<int32_t, int32_t>> strip_at;
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
   std::map<const VrV *, std::array<int32_t, 4>> vr_at;    // rows, bmeta, w128, frag
   std::map<const MfmaH *, std::array<int32_t, 4>> mh_at;  // wsum, frag, s0, lut
@@ -272,7 +248,6 @@ struct fi_ctx {
   std::map<const HvH *, std::array<int32_t, 3>> hvh_at;   // w128, frag, s0
   int32_t mono_wts_at = -1;
   bool heap_retry = false;
-  bool sc_mfma = true;  // FI_DISABLE_SC_MFMA=1: VALU horizontal pass (k_sc_hrows) instead of k_sc_hmfma
 };
 
 static void sync_streams(fi_ctx *c) {
@@ -465,8 +440,6 @@ static void heap_reset(fi_ctx *c) {
   c->axis_wd_at.clear();
   c->sc_at.clear();
   c->imp_at.clear();
-  c->ring_at.clear();
-  c->strip_at.clear();
   c->vv_at.clear();
   c->vr_at.clear();
   c->mh_at.clear();
@@ -482,8 +455,6 @@ static int heap_prepare(fi_ctx *c, Exec &E) {
   if (c->axis_cache.size() > kAxisCacheMax || c->sc_cache.size() > kScCacheMax ||
       c->imp_cache.size() > kImpCacheMax) {
     c->axis_cache.clear();
-    c->ring_cache.clear();
-    c->strip_cache.clear();
     c->vmv_cache.clear();
     c->vrv_cache.clear();
     c->vmh_cache.clear();
@@ -591,48 +562,6 @@ static void add_axis_f64(fi_ctx *c, Exec &E, const AxisTable *t, DevAxis *d) {
   d->wd = it->second;
 }
 
-// Column strips of the fused kernel (fi_fused.hip): <= kFusedStripBytes
-// source bytes (256 streaming lanes x 8 B), <= 768 output columns, horizontal
-// tap table <= 32 KB of LDS.  Every column's window is padded (zero weights)
-// to the strip's longest, so the epilogue loop has a uniform trip count.
-static constexpr int kFusedStripBytes = 2048;
-static bool fused_strips(const AxisTable &H, int ew, std::vector<StripTab> *out) {
-  const int nx_max = std::max(1, std::min(768, 8192 / std::max(1, (int)H.maxtaps)));
-  for (int S = std::max(1, (ew + nx_max - 1) / nx_max); S <= ew; S++) {
-    out->clear();
-    bool ok = true;
-    for (int k = 0; k < S && ok; k++) {
-      StripTab st;
-      FusedTile &t = st.t;
-      t = FusedTile{};
-      t.x0 = (int)((int64_t)ew * k / S);
-      t.x1 = (int)((int64_t)ew * (k + 1) / S);
-      if (t.x1 <= t.x0) continue;
-      int lo = 1 << 30, hi = 0, T = 0;
-      for (int x = t.x0; x < t.x1; x++) {
-        lo = std::min(lo, H.start[x]);
-        hi = std::max(hi, H.start[x] + H.count[x]);
-        T = std::max(T, H.count[x]);
-      }
-      t.b0 = (3 * lo) / 16 * 16;
-      t.nbytes = (3 * hi + 15) / 16 * 16 - t.b0;
-      t.htaps = T;
-      ok = t.nbytes <= kFusedStripBytes;
-      const int nx = t.x1 - t.x0;
-      st.starts.resize(nx);
-      st.wT.assign((size_t)T * nx, 0.0f);
-      for (int x = t.x0; x < t.x1; x++) {
-        const int s0 = H.start[x], c = H.count[x];
-        const int sp = std::max(lo, std::min(s0, hi - T));
-        st.starts[x - t.x0] = sp;
-        for (int j = 0; j < c; j++) st.wT[(size_t)(s0 - sp + j) * nx + (x - t.x0)] = H.w[H.woff[x] + j];
-      }
-      out->push_back(std::move(st));
-    }
-    if (ok) return true;
-  }
-  return false;
-}
 
 struct ScLaunchData {
   std::vector<ScDesc> descs;
@@ -771,7 +700,9 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     }
     const Placed &q = pp->second;
     const fi_ctx::ScTabs &T = c->sc_at.at(&P);
-    const bool prep = c->sc_prep && P.prep_ok;
+    // the per-image MFMA kernels (k_sc_fz, or k_sc_hmfma + k_sc_vq), else the
+    // generic per-row kernels
+    const bool prep = c->sc_prep && P.prep_ok && P.hm_ok && P.vq_ok;
     d.img = it.img;
     d.stride = it.stride;
     d.W = it.W;
@@ -795,7 +726,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.vb = T.vb;
     d.vk = T.vk;
     d.prep = prep ? 1 : 0;
-    d.hm = prep && P.hm_ok && c->sc_mfma ? 1 : 0;
+    d.hm = prep ? 1 : 0;
     d.hm_rows = P.hm_rows;
     d.hm_ks = P.hm_ks;
     d.hm_pitch = P.hm_pitch;
@@ -803,8 +734,8 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.hmB = T.hmB;
     d.hmC = T.hmC;
     d.hmS0 = T.hmS0;
-    d.vq = prep && P.vq_ok && c->sc_vq ? 1 : 0;
-    d.fz = d.hm && d.vq && P.fz_ok && c->sc_fz ? 1 : 0;
+    d.vq = prep ? 1 : 0;
+    d.fz = prep && P.fz_ok && c->sc_fz ? 1 : 0;
     d.vqA = T.vqA;
     d.vqC = T.vqC;
     d.vqK0 = T.vqK0;
@@ -813,7 +744,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     // workspace (offsets; converted to pointers after allocation)
     auto take = [&](size_t n) { return (uint8_t *)(uintptr_t)(E.work.take(n) + 1); };
     if (P.fx > 1 || P.fy > 1) d.red = take((size_t)P.rw * P.rh * 3);
-    if (P.thumb && P.need_h && !d.fz)  // generic kernels: pitch aw*3; k_sc_hrows: pitch apitch
+    if (P.thumb && P.need_h && !d.fz)  // generic kernels: pitch aw*3; k_sc_hmfma: pitch apitch
       d.hbuf = take((size_t)(prep ? (P.aw * 3 + 15) / 16 * 16 : P.aw * 3) * std::max(P.hrows, 1));
     if (P.thumb && (!prep || want_pre)) d.pre = take((size_t)P.aw * P.ah * 3);
     d.maps = (uint32_t *)take((size_t)P.aw * P.ah * 4);
@@ -859,8 +790,8 @@ static Launch add_launch(Blob &blob, const std::vector<Desc> &all, const std::ve
 // otherwise.
 struct ScLaunches {
   Launch red, hp, vp, maps;        // generic (fi_kernels.hip)
-  size_t prep_off = 0, hv_off = 0, hm_off = 0, vq_off = 0;  // k_sc_vmaps / k_sc_hrows / k_sc_hmfma / k_sc_vq
-  int nprep = 0, nhv = 0, nhm = 0, h_chunks = 0, h_lds = 0, hm_chunks = 0, hm_lds = 0, v_chunks = 0, v_lds = 0;
+  size_t hm_off = 0, vq_off = 0;   // k_sc_hmfma / k_sc_vq
+  int nhm = 0, hm_chunks = 0, hm_lds = 0;
   size_t fz_off = 0;  // k_sc_fz
   int nfz = 0, fz_lds = 0;
   int nvq = 0, vq_chunks = 0, vq_lds = 0;
@@ -871,7 +802,7 @@ struct ScLaunches {
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> prep, hv, hm, sl, sg, vq, fz;
+  std::vector<ScDesc> hm, sl, sg, vq, fz;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
     const ScDesc &d = SL.descs[k];
@@ -881,32 +812,18 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
       fz.push_back(d);
       X->fz_lds = std::max(X->fz_lds, P.fz_lds);
     } else if (d.prep) {
-      if (d.vq) {
-        vq.push_back(d);
-        X->vq_chunks = std::max(X->vq_chunks, P.vq_chunks);
-        X->vq_lds = std::max(X->vq_lds, P.vq_lds);
-      } else {
-        prep.push_back(d);
-      }
-      if (d.hm) {
-        hm.push_back(d);
-        X->hm_chunks = std::max(X->hm_chunks, P.hm_chunks);
-        X->hm_lds = std::max(X->hm_lds, P.hm_lds);
-      } else if (d.need_h) {
-        hv.push_back(d);
-        X->h_chunks = std::max(X->h_chunks, P.h_chunks);
-        X->h_lds = std::max(X->h_lds, P.h_lds);
-      }
-      if (!d.vq) {
-        X->v_chunks = std::max(X->v_chunks, P.v_chunks);
-        X->v_lds = std::max(X->v_lds, P.v_lds);
-      }
+      vq.push_back(d);
+      X->vq_chunks = std::max(X->vq_chunks, P.vq_chunks);
+      X->vq_lds = std::max(X->vq_lds, P.vq_lds);
+      hm.push_back(d);
+      X->hm_chunks = std::max(X->hm_chunks, P.hm_chunks);
+      X->hm_lds = std::max(X->hm_lds, P.hm_lds);
     } else {
       if (d.hbuf) shp.push_back((int)k);
       if (d.pre) svp.push_back((int)k);
       smaps.push_back((int)k);
     }
-    if (c->sc_lds_maps && (int64_t)d.aw * d.ah * 4 <= kScoreLdsMaps) {
+    if ((int64_t)d.aw * d.ah * 4 <= kScoreLdsMaps) {
       sl.push_back(d);
       X->sl_px = std::max(X->sl_px, d.aw * d.ah);
     } else {
@@ -917,10 +834,6 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->hp = add_launch(B, SL.descs, shp, [](const ScDesc &d) { return d.hrows; });
   X->vp = add_launch(B, SL.descs, svp, [](const ScDesc &d) { return d.ah; });
   X->maps = add_launch(B, SL.descs, smaps, [](const ScDesc &d) { return d.ah; });
-  X->prep_off = B.addv(prep);
-  X->nprep = (int)prep.size();
-  X->hv_off = B.addv(hv);
-  X->nhv = (int)hv.size();
   X->hm_off = B.addv(hm);
   X->nhm = (int)hm.size();
   X->vq_off = B.addv(vq);
@@ -941,7 +854,7 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
   // on the stream that reads it, so batches queued before a parameter change
   // have read the old table first
   const uint16_t *skinsat = nullptr;
-  if (X.nfz > 0 && c->sc_skinsat) {
+  if (X.nfz > 0) {
     const std::string key(reinterpret_cast<const char *>(&PD), offsetof(ScParamsDev, pad));
     if (!c->skinsat.p || c->skinsat_key != key) {
       const int rc = ensure(c, &c->skinsat, (size_t)2 << 24);
@@ -955,12 +868,10 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
     Timer t(c, "sc_prep", 0, st, st);
     if (X.red.tiles)
       hipLaunchKernelGGL(k_sc_reduce, dim3(X.red.tiles), dim3(256), 0, st, desc(X.red), pre(X.red), X.red.n);
-    if (launch_sc_h(st, true, (const ScDesc *)(ab + X.hm_off), X.nhm, X.hm_chunks, X.hm_lds, ai) != 0 ||
-        launch_sc_h(st, false, (const ScDesc *)(ab + X.hv_off), X.nhv, X.h_chunks, X.h_lds, ai) != 0 ||
-        launch_sc_v(st, (const ScDesc *)(ab + X.prep_off), X.nprep, X.v_chunks, X.v_lds, ai, PD) != 0 ||
+    if (launch_sc_h(st, (const ScDesc *)(ab + X.hm_off), X.nhm, X.hm_chunks, X.hm_lds, ai) != 0 ||
         launch_sc_vq(st, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0 ||
         launch_sc_fz(st, (const ScDesc *)(ab + X.fz_off), X.nfz, X.fz_lds, ai, PD, skinsat) != 0)
-      return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d)", X.hm_lds, X.h_lds, X.v_lds);
+      return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d)", X.hm_lds, X.vq_lds, X.fz_lds);
     if (X.hp.tiles)
       hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, st, desc(X.hp), pre(X.hp), X.hp.n, ai);
     if (X.vp.tiles)
@@ -996,8 +907,8 @@ static void host_stat(fi_ctx *c, const char *name, double ms) {
 // batch pipeline.  run_batch strings the units together:
 //   plan_image (per image: geometry, descriptor, resample path + tables)
 //   -> plan_batch_sc (smartcrop stage) -> resolve_workspace (device pointers,
-//   -monochrome / convolution steps, crop apply) -> build_fused_tiles /
-//   build_vm_tiles -> pack_batch (one blob) -> launch_batch (both streams)
+//   -monochrome / convolution steps, crop apply) -> build_vm_tiles (k_rs_vr /
+//   k_rs_vm) / build_hv_tiles -> pack_batch (one blob) -> launch_batch
 //   -> queue_readback (pinned result records, the in-flight list).
 // ---------------------------------------------------------------------------
 struct MonoItem {
@@ -1007,11 +918,6 @@ struct MonoItem {
 struct ConvItem {
   int img;
   size_t a_off, b_off;
-};
-struct FusedGroup {  // fused tiles of one ring size K
-  std::vector<FusedTile> tiles;
-  int pitch = 0, max_taps = 0, max_nbytes = 0;
-  size_t off = 0;
 };
 // Everything a batch plans before it is packed and uploaded.
 struct BatchPlan {
@@ -1026,9 +932,6 @@ struct BatchPlan {
   std::vector<int> sc_of;      // image -> sitems index (-1: none)
   std::map<const AxisTable *, DevAxis> placed;
   // resample path members (indices into rd) and their tables
-  std::vector<int> fused_img;
-  std::vector<const RingTable *> fused_ring;
-  std::vector<const std::vector<StripTab> *> fused_strips_of;
   std::vector<int> vm_img;
   std::vector<const VmV *> vm_v;
   std::vector<const MfmaH *> vm_h;
@@ -1054,7 +957,6 @@ struct BatchPlan {
   std::vector<ConvStep> cst[6];  // U-H, U-V+combine, S-2D, B-H, B-V, to8
   std::vector<ApplyDesc> apply;
   // tiles
-  std::map<int, FusedGroup> fgroups;
   std::vector<VDesc> vdescs;
   std::vector<MStrip> vstrips;
   std::vector<VTile> vtiles;
@@ -1064,11 +966,6 @@ struct BatchPlan {
   int vr_G = 0, vr_images = 0;
   VrLayout vr_L{};
   size_t vm_lds = 0;
-  // k_rs_vp: persistent grid, per-workgroup piece counts, LDS layout (vp_G = 0: run k_rs_vm)
-  int vp_G = 0;
-  std::vector<int32_t> vp_nphase;
-  VpLayout vp_L{};
-  int vp_images = 0;
   std::vector<HvDesc> hdescs;
   std::vector<HvStripD> hstrips;
   std::vector<HvTile> htiles;
@@ -1076,7 +973,7 @@ struct BatchPlan {
 };
 // Blob offsets and launch lists of a packed batch.
 struct Packed {
-  size_t all_rd_off = 0, vdesc_off = 0, vstrip_off = 0, vtile_off = 0, vnph_off = 0, apply_off = 0, mono_off = 0;
+  size_t all_rd_off = 0, vdesc_off = 0, vstrip_off = 0, vtile_off = 0, apply_off = 0, mono_off = 0;
   size_t vrtile_off = 0, vrinfo_off = 0;
   size_t hdesc_off = 0, hstrip_off = 0, htile_off = 0;
   size_t ai_off = 0, af_off = 0, ad_off = 0, mono_wts = 0;
@@ -1109,18 +1006,18 @@ static const MfmaH *vm_strips(fi_ctx *c, const AxisTable *ht, bool q16) {
 }
 
 // Choose the resample kernel of one image (d.mode) and add its tables:
-//   5  k_rs_vm: RGB, vertical first, 16-byte aligned rows (the default);
-//   3  k_rs_fused: the VALU ring kernel (FI_DISABLE_VM_RS=1, or vm tables
-//      that do not fit);
+//   5  k_rs_vr / k_rs_vm: RGB, vertical first, 16-byte aligned rows (the
+//      default; build_vm_tiles picks the kernel);
+//   6  k_rs_hv: RGB, horizontal first, contiguous taps, 16-byte aligned rows;
 //   1 / 2  the generic two-pass kernels, vertical / horizontal first (RGBA,
-//      -monochrome and convolution inputs, horizontal-first geometries).
+//      convolution inputs, unaligned sources, tables that do not fit).
 // Returns the algorithmic source bytes the path reads.
 static int64_t plan_resample(fi_ctx *c, Exec &E, BatchPlan &Bp, const ImPlan &P, const fi_image &im,
                              ResizeDesc &d) {
   const AxisTable *vt = add_axis(c, E, P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &d.v, Bp.placed);
   const AxisTable *ht = add_axis(c, E, P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &d.h, Bp.placed);
   const bool rgb = P.C == 3;
-  const bool fast_ok = rgb && !P.conv;  // the streaming / fused kernels write 8-bit only
+  const bool fast_ok = rgb && !P.conv;  // the streaming kernels write 8-bit only
   if (!rgb) {
     // matte (RGBA) images: the alpha-weighted f64 generic passes (k_rs4_*)
     add_axis_f64(c, E, vt, &d.v);
@@ -1128,8 +1025,8 @@ static int64_t plan_resample(fi_ctx *c, Exec &E, BatchPlan &Bp, const ImPlan &P,
   }
   const bool aligned16 = ((uintptr_t)im.src % 16) == 0 && (im.src_stride % 16) == 0;
   const int64_t strip_bytes = (int64_t)vt->touched * (d.h.src_hi - d.h.src_lo) * 3;
-  const bool vfirst_fast = fast_ok && !P.hfirst && c->fused && aligned16;
-  if (vfirst_fast && c->vm_rs) {
+  const bool vfirst_fast = fast_ok && !P.hfirst && c->fast_rs && aligned16;
+  if (vfirst_fast) {
     auto vit = c->vmv_cache.find(vt);
     if (vit == c->vmv_cache.end()) {
       VmV m;
@@ -1148,7 +1045,7 @@ static int64_t plan_resample(fi_ctx *c, Exec &E, BatchPlan &Bp, const ImPlan &P,
     }
   }
   // horizontal first: contiguous tap ranges (no sample pre-step), 16-byte aligned rows
-  if (fast_ok && P.hfirst && !P.sample && c->fused && c->hv_rs && aligned16) {
+  if (fast_ok && P.hfirst && !P.sample && c->fast_rs && aligned16) {
     auto vit = c->hvv_cache.find(vt);
     if (vit == c->hvv_cache.end()) {
       HvV m;
@@ -1172,51 +1069,6 @@ static int64_t plan_resample(fi_ctx *c, Exec &E, BatchPlan &Bp, const ImPlan &P,
       int64_t cols = 0;
       for (const HvStrip &st : hit->second.strips) cols += std::min(st.pp, P.W - st.px0);
       return (int64_t)vit->second.nrows * cols * 3;
-    }
-  }
-  if (vfirst_fast && !P.mono && d.h.maxtaps <= 64) {
-    auto rit = c->ring_cache.find(vt);
-    if (rit == c->ring_cache.end()) {
-      RingTable rt;
-      if (!build_ring(*vt, &rt)) rt.K = 0;
-      rit = c->ring_cache.emplace(vt, std::move(rt)).first;
-    }
-    const RingTable *ring = (rit->second.K && rit->second.K <= 8) ? &rit->second : nullptr;  // K=16 would spill
-    const std::vector<StripTab> *strips = nullptr;
-    if (ring) {
-      auto sit = c->strip_cache.find(ht);
-      if (sit == c->strip_cache.end()) {
-        std::vector<StripTab> st;
-        if (!fused_strips(*ht, P.ew, &st)) st.clear();
-        sit = c->strip_cache.emplace(ht, std::move(st)).first;
-      }
-      if (!sit->second.empty()) strips = &sit->second;
-    }
-    if (strips) {
-      d.mode = 3;  // fused vertical-first
-      d.fused_k = ring->K;
-      d.ring_n = (int32_t)ring->rows.size();
-      auto pr = c->ring_at.find(ring);
-      if (pr == c->ring_at.end()) {
-        std::array<int32_t, 4> o;
-        o[0] = E.oi();
-        E.ai.insert(E.ai.end(), ring->rows.begin(), ring->rows.end());
-        o[1] = E.of();
-        E.af.insert(E.af.end(), ring->ringw.begin(), ring->ringw.end());
-        o[2] = E.oi();
-        E.ai.insert(E.ai.end(), ring->ringy.begin(), ring->ringy.end());
-        o[3] = E.oi();
-        E.ai.insert(E.ai.end(), ring->flush.begin(), ring->flush.end());
-        pr = c->ring_at.emplace(ring, o).first;
-      }
-      d.ring_rows = pr->second[0];
-      d.ring_w = pr->second[1];
-      d.ring_y = pr->second[2];
-      d.ring_flush = pr->second[3];
-      Bp.fused_ring.push_back(ring);
-      Bp.fused_strips_of.push_back(strips);
-      Bp.fused_img.push_back((int)Bp.rd.size());
-      return strip_bytes;
     }
   }
   if (!rgb && !P.hfirst) {
@@ -1341,7 +1193,7 @@ static void plan_image(fi_ctx *c, Exec &E, BatchPlan &Bp, int i) {
     src_bytes = plan_resample(c, E, Bp, P, im, d);
   }
   Bp.resize_bytes += (double)src_bytes + (double)need;
-  static const char *kPath[7] = {"path_copy", "path_generic_v", "path_generic_h", "path_fused", "path_none",
+  static const char *kPath[7] = {"path_copy", "path_generic_v", "path_generic_h", "path_none", "path_none",
                                  "path_vm", "path_hv"};
   c->stats[kPath[d.mode]].launches += 1;  // images per resample path (fi_kernel_stats)
   Bp.rd_of[i] = (int)Bp.rd.size();
@@ -1478,46 +1330,6 @@ static void resolve_workspace(Exec &E, BatchPlan &Bp, uint8_t *wb) {
   }
 }
 
-// k_rs_fused tiles: (image, column strip, row band), grouped by ring size K.
-static void build_fused_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
-  const int nf = (int)Bp.fused_img.size();
-  for (int q = 0; q < nf; q++) {
-    const ResizeDesc &d = Bp.rd[Bp.fused_img[q]];
-    const RingTable &R = *Bp.fused_ring[q];
-    FusedGroup &G = Bp.fgroups[d.fused_k];
-    const std::vector<StripTab> &strips = *Bp.fused_strips_of[q];
-    // row bands: enough work items to fill the chip (>= ~1024 per batch)
-    const int per_img = (int)strips.size();
-    int B = (1024 + nf * per_img - 1) / (nf * per_img);
-    B = std::max(1, std::min(B, d.eh / 16 > 0 ? d.eh / 16 : 1));
-    for (int b = 0; b < B; b++) {
-      const int y0 = (int)((int64_t)d.eh * b / B), y1 = (int)((int64_t)d.eh * (b + 1) / B);
-      if (y1 <= y0) continue;
-      for (const StripTab &st : strips) {
-        auto sp = c->strip_at.find(&st);
-        if (sp == c->strip_at.end()) {
-          const int32_t so = E.oi();
-          E.ai.insert(E.ai.end(), st.starts.begin(), st.starts.end());
-          const int32_t wo = E.of();
-          E.af.insert(E.af.end(), st.wT.begin(), st.wT.end());
-          sp = c->strip_at.emplace(&st, std::make_pair(so, wo)).first;
-        }
-        FusedTile t = st.t;
-        t.hstart = sp->second.first;
-        t.hw = sp->second.second;
-        t.image = Bp.fused_img[q];
-        t.y0 = y0;
-        t.y1 = y1;
-        t.i0 = R.first_i[y0];
-        t.i1 = R.last_i[y1 - 1] + 1;
-        G.tiles.push_back(t);
-        G.pitch = std::max(G.pitch, t.x1 - t.x0);
-        G.max_nbytes = std::max(G.max_nbytes, t.nbytes);
-        G.max_taps = std::max(G.max_taps, t.htaps);
-      }
-    }
-  }
-}
 
 // k_rs_vr: images (their k_rs_vm VDesc, strips) with block-major tables.
 struct VrWork {
@@ -1541,10 +1353,7 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   bool q16 = false;
   int64_t nst = 0;
   for (const VrWork &w : work) {
-    for (int st = 0; st < w.nstrips; st++) {
-      vpitch = std::max(vpitch, Bp.vstrips[w.first_strip + st].vpitch);
-      if (Bp.vstrips[w.first_strip + st].nocb > 3) return false;  // five H waves, two items each
-    }
+    for (int st = 0; st < w.nstrips; st++) vpitch = std::max(vpitch, Bp.vstrips[w.first_strip + st].vpitch);
     const VDesc &d = Bp.vdescs[w.img];
     q16 = q16 || d.gray || d.rot != 0;
     nst += w.nstrips;
@@ -1559,6 +1368,9 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     if (vp == c->vr_at.end()) {
       std::array<int32_t, 4> o;
       o[0] = put(V.rows);
+      // k_rs_vr reads the rows table 16 entries at a time from any list index
+      // below nrows: 32 copies of the last row keep those reads inside it
+      E.ai.insert(E.ai.end(), 32, V.rows.back());
       align4();
       o[1] = put(V.bmeta);
       o[2] = put(V.w128);
@@ -1758,7 +1570,9 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
       const VrV &V = it->second;
       int64_t gap = 0;  // widest gap between consecutive touched rows (the DMA's per-lane offset)
       for (size_t k = 1; k < V.rows.size(); k++) gap = std::max<int64_t>(gap, V.rows[k] - V.rows[k - 1]);
-      if (V.nblk > 0 && gap * Bp.vdescs[w.img].src_stride < ((int64_t)1 << 31))
+      bool narrow = true;  // five H waves take two horizontal items each: <= 3 16-px blocks per strip
+      for (int st = 0; st < w.nstrips; st++) narrow = narrow && Bp.vstrips[w.first_strip + st].nocb <= 3;
+      if (V.nblk > 0 && narrow && gap * Bp.vdescs[w.img].src_stride < ((int64_t)1 << 31))
         vr.push_back({w.img, w.first_strip, w.nstrips, &V});
       else
         rest.push_back(w);
@@ -1791,38 +1605,6 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   for (size_t i = 0; i < mx; i++)
     for (int x = 0; x < 8; x++)
       if (i < q8[x].size()) Bp.vtiles.push_back(q8[x][i]);
-  // k_rs_vp: one persistent workgroup per CU walks tiles g, g + G, ... (G a
-  // multiple of 8 keeps an image's strips on one XCD queue); it needs the
-  // launch's widest Q16 plane and output-tile kind to fit in LDS, and every
-  // image's row gaps x stride in 32 bits (the DMA's per-lane offset)
-  Bp.vp_G = 0;
-  if (c->vp_rs && !Bp.vtiles.empty()) {
-    int vpitch = 0;
-    bool q16 = false, ok = true;
-    for (const VTile &t : Bp.vtiles) {
-      vpitch = std::max(vpitch, Bp.vstrips[t.strip].vpitch);
-      const VDesc &d = Bp.vdescs[t.img];
-      q16 = q16 || d.gray || d.rot != 0;
-      ok = ok && t.p1 > t.p0;
-    }
-    for (const Work1 &w : work) {
-      const VDesc &d = Bp.vdescs[w.img];
-      const std::vector<int32_t> &rows = w.V->rows;
-      const int64_t gap = rows.size() > 1 ? (int64_t)(rows.back() - rows.front()) : 0;
-      ok = ok && gap * d.src_stride < ((int64_t)1 << 31);
-    }
-    const VpLayout L = vp_lds_layout(vpitch, q16);
-    if (ok && L.total <= kVpMaxLds) {
-      const int ntiles = (int)Bp.vtiles.size();
-      int G = std::min(ntiles, c->n_cu);
-      if (G > 8) G -= G % 8;
-      Bp.vp_G = G;
-      Bp.vp_L = L;
-      Bp.vp_nphase.assign(G, 0);
-      for (int t = 0; t < ntiles; t++) Bp.vp_nphase[t % G] += Bp.vtiles[t].p1 - Bp.vtiles[t].p0;
-      Bp.vp_images = (int)work.size();
-    }
-  }
 }
 
 // k_rs_hv workgroups: (image, strip, band of output blocks); bands only when
@@ -1938,13 +1720,11 @@ static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
   K.vdesc_off = B.addv(Bp.vdescs);
   K.vstrip_off = B.addv(Bp.vstrips);
   K.vtile_off = B.addv(Bp.vtiles);
-  K.vnph_off = B.addv(Bp.vp_nphase);
   K.vrtile_off = B.addv(Bp.vrtiles);
   K.vrinfo_off = B.addv(Bp.vr_info);
   K.hdesc_off = B.addv(Bp.hdescs);
   K.hstrip_off = B.addv(Bp.hstrips);
   K.htile_off = B.addv(Bp.htiles);
-  for (auto &g : Bp.fgroups) g.second.off = B.addv(g.second.tiles);
   auto eh_tiles = [](const ResizeDesc &d) { return d.eh; };
   auto mid_tiles = [](const ResizeDesc &d) { return d.mid_rows; };
   K.L0 = add_launch(B, Bp.rd, m0, eh_tiles);
@@ -2011,13 +1791,7 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
       c->stats["path_vr"].launches += Bp.vr_images;
       c->stats["path_vm"].launches -= Bp.vr_images;
     }
-    if (!Bp.vtiles.empty() && Bp.vp_G > 0) {
-      if (launch_vp(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
-                    (const VTile *)(ab + K.vtile_off), (int)Bp.vtiles.size(), (const int32_t *)(ab + K.vnph_off),
-                    Bp.vp_G, ai, Bp.vp_L) != 0)
-        return set_err(FI_EDEVICE, "persistent MFMA resample launch rejected (LDS %d)", Bp.vp_L.total);
-      c->stats["path_vp"].launches += Bp.vp_images;
-    } else if (!Bp.vtiles.empty() &&
+    if (!Bp.vtiles.empty() &&
                launch_vm(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
                          (const VTile *)(ab + K.vtile_off), (int)Bp.vtiles.size(), ai, Bp.vm_lds) != 0)
       return set_err(FI_EDEVICE, "streaming MFMA resample launch rejected (LDS %zu)", Bp.vm_lds);
@@ -2027,14 +1801,6 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
         launch_hv(c->stream, (const HvDesc *)(ab + K.hdesc_off), (const HvStripD *)(ab + K.hstrip_off),
                   (const HvTile *)(ab + K.htile_off), (int)Bp.htiles.size(), ai, Bp.hv_lds) != 0)
       return set_err(FI_EDEVICE, "horizontal-first MFMA resample launch rejected (LDS %zu)", Bp.hv_lds);
-    for (auto &g : Bp.fgroups) {
-      const FusedGroup &G = g.second;
-      if (G.tiles.empty()) continue;
-      const int pitch = (G.pitch + 3) & ~3;
-      if (launch_fused(c->stream, g.first, (const ResizeDesc *)(ab + K.all_rd_off), (const FusedTile *)(ab + G.off),
-                       (int)G.tiles.size(), ai, af, pitch, G.max_taps, G.max_nbytes) != 0)
-        return set_err(FI_EDEVICE, "fused resample launch rejected (K=%d, LDS budget)", g.first);
-    }
     if (K.Q0.tiles || K.Q1a.tiles || K.Q2a.tiles) {
       const ResizeDesc *dq0 = (const ResizeDesc *)desc_p(K.Q0), *dq1 = (const ResizeDesc *)desc_p(K.Q1a),
                        *dq2a = (const ResizeDesc *)desc_p(K.Q2a), *dq2b = (const ResizeDesc *)desc_p(K.Q2b);
@@ -2179,7 +1945,6 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async, std::shar
   uint8_t *wb = (uint8_t *)S.work.p;
   resolve_workspace(E, Bp, wb);
   const double t_sc = now_ms();
-  build_fused_tiles(c, E, Bp);
   const double t_tiles0 = now_ms();
   build_vm_tiles(c, E, Bp);
   build_hv_tiles(c, E, Bp);
@@ -2520,12 +2285,6 @@ int fi_debug_vm_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   return vm_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
 }
-int fi_debug_vp_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
-  if (!c || !out) return FI_EINVAL;
-  HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return vp_read_stamps(out, slots) == 0 ? FI_OK : FI_EDEVICE;
-}
 int fi_debug_vr_stamps(fi_ctx *c, uint64_t *out, int32_t slots) {
   if (!c || !out) return FI_EINVAL;
   HIP_TRY(hipSetDevice(c->device));
@@ -2743,40 +2502,23 @@ int fi_create(fi_ctx **out, int32_t device) {
     return set_err(FI_EDEVICE, "device %d is %s; libflyimg_hip.so is built for gfx950 only", device, prop.gcnArchName);
   fi_ctx *c = new fi_ctx();
   c->device = device;
-  if (const char *e = getenv("FI_DISABLE_FUSED")) c->fused = !(e[0] == '1');
-  if (const char *e = getenv("FI_DISABLE_VM_RS")) c->vm_rs = !(e[0] == '1');
-  // k_rs_vp: opt-in (FI_VP_RS=1) until it is faster than k_rs_vm
-  c->vp_rs = false;
-  if (const char *e = getenv("FI_VP_RS")) c->vp_rs = e[0] == '1';
-  // k_rs_vr: opt-in (FI_VR_RS=1) until measured
+  // Kernel selection is by geometry and LDS fit; three switches keep the
+  // fallbacks testable on geometries that would not reach them otherwise:
+  //   FI_FORCE_GENERIC=1   the generic two-pass resample and per-row smartcrop kernels
+  //   FI_VR_RS=0           k_rs_vm instead of k_rs_vr (vertical-first)
+  //   FI_DISABLE_SC_FZ=1   k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
+  if (const char *e = getenv("FI_FORCE_GENERIC")) c->fast_rs = c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
-  c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  if (const char *e = getenv("FI_DISABLE_HV_RS")) c->hv_rs = !(e[0] == '1');
-  if (const char *e = getenv("FI_SC_LDS_MAPS")) c->sc_lds_maps = !(e[0] == '0');
-  if (const char *e = getenv("FI_DISABLE_SC_VQ")) c->sc_vq = !(e[0] == '1');
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
-  if (const char *e = getenv("FI_DISABLE_SC_SKINSAT")) c->sc_skinsat = !(e[0] == '1');
-  if (const char *e = getenv("FI_DISABLE_SC_PREP")) c->sc_prep = !(e[0] == '1');
-  if (const char *e = getenv("FI_DISABLE_SC_MFMA")) c->sc_mfma = !(e[0] == '1');
-  // FI_SC_STREAM=1: the smartcrop stage of batch k on its own stream, beside
-  // batch k+1's resample.  Off by default: k_rs_vm fills every CU (LDS), so
-  // the overlap only stretches both (cfg2: step 3.79 vs 3.81 ms, sc_score
-  // 0.39 -> 2.06 ms, resize 2.47 -> 2.83 ms).
-  bool sc_stream = false;
-  if (const char *e = getenv("FI_SC_STREAM")) sc_stream = e[0] == '1';
-  // FI_SC_PRIO=1: the smartcrop stream at the highest priority, so its
-  // workgroups take CU slots as the resample's retire
-  int prio_lo = 0, prio_hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  const bool sc_prio = getenv("FI_SC_PRIO") && getenv("FI_SC_PRIO")[0] == '1';
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      (sc_stream && (sc_prio ? hipStreamCreateWithPriority(&c->sc_stream, hipStreamNonBlocking, prio_hi)
-                             : hipStreamCreateWithFlags(&c->sc_stream, hipStreamNonBlocking)) != hipSuccess)) {
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+  c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  // (the smartcrop stage on a stream of its own beside the next batch's
+  // resample was measured in round 2: the resample fills every CU, so the
+  // overlap only stretched both -- one stream)
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return set_err(FI_EDEVICE, "hipStreamCreate failed");
   }
-  if (!sc_stream) c->sc_stream = c->stream;
+  c->sc_stream = c->stream;
   if (hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking) != hipSuccess) {
     fi_destroy(c);

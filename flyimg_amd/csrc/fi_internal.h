@@ -18,7 +18,6 @@
 namespace fi {
 
 constexpr int kMaxChannels = 3;
-constexpr int kFusedLanes = 256;  // threads per workgroup of the fused resample kernel
 
 // One separable axis in the *source* index domain (the ImageMagick sample
 // pre-step is folded in by merging taps that map to one source index).
@@ -36,8 +35,8 @@ struct DevAxis {
                     // weight (o, j) = ad[wd + ai[woff + o] - wbase + j]
 };
 
-// Per-image descriptor of the resample path (generic two-pass kernels and
-// the fused vertical-first kernel).
+// Per-image descriptor of the resample path (the generic two-pass kernels and
+// the copy / epilogue kernel; the streaming kernels take VDesc / HvDesc).
 struct ResizeDesc {
   const uint8_t *src;
   int64_t src_stride;  // bytes
@@ -56,26 +55,6 @@ struct ResizeDesc {
   int64_t dst_stride;
   int32_t out_w, out_h, out_c;  // post-rotate dims
   int32_t q16out;               // 1: the epilogue writes rotated Q16 (u16) for the convolution stage
-  // fused vertical-first kernel: list of touched source rows and, per list
-  // row, the weight of each of the K ring slots and the output row owning it
-  int32_t fused_k;     // ring slots (0 = not fused)
-  int32_t ring_n;      // touched source rows
-  int32_t ring_rows;   // ai offset: source row index [ring_n]
-  int32_t ring_w;      // af offset: slot weights [ring_n][K]
-  int32_t ring_y;      // ai offset: slot owner output row or -1 [ring_n][K]
-  int32_t ring_flush;  // ai offset: output rows [lo, hi) completing at list row [ring_n][2]
-};
-
-// Fused-kernel work item: one (image, column strip, row band).
-struct FusedTile {
-  int32_t image;
-  int32_t x0, x1;      // output columns [x0, x1) of the extent window
-  int32_t y0, y1;      // output rows    [y0, y1)
-  int32_t b0, nbytes;  // source byte range (16-B aligned start, length) of the strip
-  int32_t i0, i1;      // range of the image's touched-row list streamed
-  int32_t htaps;       // horizontal taps of every column of the strip (zero padded)
-  int32_t hstart;      // ai offset: first source column of each column's window [nx]
-  int32_t hw;          // af offset: weights, transposed [htaps][nx]
 };
 
 // One step of the forwarded convolutions (fi_conv.hip) on one image's rotated
@@ -117,8 +96,8 @@ struct ScDesc {
   int32_t hb, hk, ksh; // arena offsets: H bounds (pairs), H coeffs (int32), ksize
   int32_t vb, vk, ksv;
   int32_t hkT;         // H coeffs transposed [ksh][aw] (k_sc_prep: lanes read consecutive x)
-  int32_t prep;        // 1: k_sc_hrows/k_sc_vmaps path (hbuf pitch apitch), 0: generic kernels
-  int32_t hm;          // 1: horizontal pass by k_sc_hmfma (tables below), 0: k_sc_hrows
+  int32_t prep;        // 1: per-image MFMA kernels (k_sc_fz, or k_sc_hmfma + k_sc_vq; hbuf pitch apitch), 0: generic kernels
+  int32_t hm;          // 1: horizontal pass by k_sc_hmfma / k_sc_fz (tables below)
   int32_t hm_rows, hm_ks, hm_pitch, hm_nb;
   int32_t hmB, hmC, hmS0;  // arena offsets (int32 units; hmB 16-B aligned)
   int32_t vq;              // 1: vertical pass + maps by k_sc_vq (tables below)
@@ -136,9 +115,9 @@ struct ScDesc {
   int32_t exact_all;
 };
 
-// k_sc_hrows / k_sc_vmaps (fi_smartcrop.hip): kPrepRows rows per workgroup;
-// apitch = 16-B rounded aw*3 (hbuf and LDS row pitch), spitch = 16-B rounded
-// source width*3.  LDS per workgroup <= kPrepMaxLds (host-checked).
+// smartcrop prescale planning (fi_plan.cpp plan_sc_prep): kPrepRows rows per
+// chunk; apitch = 16-B rounded aw*3 (hbuf and LDS row pitch), spitch = 16-B
+// rounded source width*3.  LDS per workgroup <= kPrepMaxLds (host-checked).
 constexpr int kPrepRows = 16;
 constexpr int kVqRows = 14;  // k_sc_vq: analysed rows per workgroup (16 prescaled rows with the edge halo)
 constexpr int kPrepMaxLds = 64 * 1024;
@@ -207,17 +186,8 @@ constexpr int kVmOtilePitch = 64 * 3 + 4;      // Q16 output tile row, u16 units
 constexpr int kVmOtileBytes = 16 * kVmOtilePitch * 2;
 constexpr int kVmOtile8Pitch = 64 * 3 + 4;     // 8-bit tile row (fast RGB path)
 constexpr int kVmOtile8Bytes = 16 * kVmOtile8Pitch;
-// k_rs_vp (fi_vp.hip): the persistent, warp-specialised form of k_rs_vm (same
-// tables, bit-identical output); one 1024-thread workgroup per CU.  LDS
-// layout from vp_lds_layout (Q16-plane stride and output-tile kind of the launch).
-struct VpLayout {
-  int32_t plane;        // bytes of one limb plane of one channel (16 vpitch + pad)
-  int32_t otile_off;    // output tiles [2][otile_bytes]
-  int32_t otile_bytes;
-  int32_t total;        // dynamic LDS of the launch
-};
-constexpr int kVpMaxLds = 160 * 1024;
-// k_rs_vr (fi_vr.hip): k_rs_vp's roles with a block-major vertical pass over a
+constexpr int kVrMaxLds = 160 * 1024;  // k_rs_vr: one 1024-thread workgroup per CU
+// k_rs_vr (fi_vr.hip): a persistent, warp-specialised resample with a block-major vertical pass over a
 // ring of R touched source rows (fi_plan.h VrV).  The VDesc fields rows /
 // nrows / row0 / rstep / w128 / frag / hwsum are VrV's, pmeta the per-block
 // {K0, ks, Rend, 0}.  A workgroup walks tiles g, g + G, ...; their touched rows

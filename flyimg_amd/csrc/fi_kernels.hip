@@ -10,7 +10,6 @@
 //     k_rs_h_u8     horizontal pass RGB8 src -> Q16 mid      (H-first images)
 //     k_rs_v_final  vertical pass  Q16 mid   -> dst + epilogue
 //     k_rs_copy     no resample (ResizeImage clone) -> dst + epilogue
-//     (the fused vertical-first kernel lives in fi_fused.hip)
 //   smartcrop (python/smartcrop.py:79-191):
 //     k_sc_reduce / k_sc_hpass / k_sc_vpass   Pillow thumbnail (integer, exact)
 //     k_sc_maps                               L, edge, skin, saturation

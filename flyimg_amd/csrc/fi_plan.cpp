@@ -748,86 +748,6 @@ bool build_hv_v(const AxisTable &v, HvV *m) {
 }
 
 
-bool build_ring(const AxisTable &v, RingTable *rt) {
-  *rt = RingTable();
-  const int ny = (int)v.start.size();
-  if (ny == 0) return false;
-  const int span = v.src_hi - v.src_lo;
-  std::vector<int32_t> idx(span, -1);
-  for (int y = 0; y < ny; y++)
-    for (int j = 0; j < v.count[y]; j++)
-      if (v.w[v.woff[y] + j] != 0.0f) idx[v.start[y] + j - v.src_lo] = 1;
-  for (int r = 0; r < span; r++)
-    if (idx[r] >= 0) {
-      idx[r] = (int32_t)rt->rows.size();
-      rt->rows.push_back(v.src_lo + r);
-    }
-  const int n = (int)rt->rows.size();
-  rt->first_i.assign(ny, -1);
-  rt->last_i.assign(ny, -1);
-  for (int y = 0; y < ny; y++) {
-    for (int j = 0; j < v.count[y]; j++)
-      if (v.w[v.woff[y] + j] != 0.0f) {
-        const int i = idx[v.start[y] + j - v.src_lo];
-        if (rt->first_i[y] < 0) rt->first_i[y] = i;
-        rt->last_i[y] = i;
-      }
-    if (rt->first_i[y] < 0) return false;  // all-zero row (cannot happen for normalised weights)
-    if (y > 0 && (rt->first_i[y] < rt->first_i[y - 1] || rt->last_i[y] < rt->last_i[y - 1])) return false;
-  }
-  std::vector<int> diff(n + 1, 0);
-  for (int y = 0; y < ny; y++) {
-    diff[rt->first_i[y]] += 1;
-    diff[rt->last_i[y] + 1] -= 1;
-  }
-  int act = 0, mx = 0;
-  for (int i = 0; i < n; i++) {
-    act += diff[i];
-    mx = std::max(mx, act);
-  }
-  const int K = mx <= 4 ? 4 : mx <= 8 ? 8 : mx <= 16 ? 16 : 0;
-  if (!K) return false;
-  rt->K = K;
-  rt->ringw.assign((size_t)n * K, 0.0f);
-  rt->ringy.assign((size_t)n * K, -1);
-  rt->flush.assign((size_t)n * 2, 0);
-  for (int y = 0; y < ny; y++) {
-    const int k = y % K;
-    for (int j = 0; j < v.count[y]; j++) {
-      const float w = v.w[v.woff[y] + j];
-      if (w == 0.0f) continue;
-      const int i = idx[v.start[y] + j - v.src_lo];
-      if (rt->ringy[(size_t)i * K + k] != -1) return false;
-      rt->ringy[(size_t)i * K + k] = y;
-      rt->ringw[(size_t)i * K + k] = w;
-    }
-    // rows of the active window without weight still own the slot
-    for (int i = rt->first_i[y]; i <= rt->last_i[y]; i++) {
-      int32_t &o = rt->ringy[(size_t)i * K + k];
-      if (o == -1) o = y;
-      else if (o != y) return false;
-    }
-    int32_t *f = &rt->flush[(size_t)rt->last_i[y] * 2];
-    if (f[0] == f[1]) {
-      f[0] = y;
-      f[1] = y + 1;
-    } else {
-      f[1] = y + 1;
-    }
-  }
-  // padding rows (fi_fused.hip kPad): zero weights, no flush, last source row
-  const int kPad = 32;  // >= 2 * DEPTH of fi_fused.hip
-  for (int q = 0; q < kPad; q++) {
-    rt->rows.push_back(rt->rows.back());
-    for (int k = 0; k < K; k++) {
-      rt->ringw.push_back(0.0f);
-      rt->ringy.push_back(-1);
-    }
-    rt->flush.push_back(0);
-    rt->flush.push_back(0);
-  }
-  return true;
-}
 
 // ---------------------------------------------------------------------------
 // Pillow

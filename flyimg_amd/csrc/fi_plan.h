@@ -51,18 +51,6 @@ struct AxisTable {
   std::vector<double> wd;  // the same weights in f64 (the RGBA path accumulates in f64 as IM does)
   int32_t maxtaps = 0, src_lo = 0, src_hi = 0, touched = 0;
 };
-// Ring table of the fused vertical-first kernel (fi_fused.hip): the list of
-// touched source rows, and per list row the weight for each of the K ring
-// slots (slot = output row % K) plus the output rows that complete there.
-struct RingTable {
-  int K = 0;
-  std::vector<int32_t> rows, ringy, flush;
-  std::vector<float> ringw;
-  std::vector<int32_t> first_i, last_i;  // per output row, list-row span
-};
-// false when the fused kernel cannot take this axis (more than 16 output rows
-// active on one source row, or a non-monotone tap layout).
-bool build_ring(const AxisTable &v, RingTable *rt);
 
 // Exact-integer MFMA resample tables (k_rs_vm, fi_vm.hip; k_sc_hmfma).
 // Weights are quantized to W = rint(w * 2^kMfmaWBits) and split into three

@@ -439,11 +439,38 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           rG += 4 * cnt;
           continue;
         }
-        // one pair: the rows table, or clamped at the list end
+        if (r_rstep == 0) {
+          // rows table (ThumbnailImage samples at uneven row gaps): 16 list rows
+          // per scalar load -- the table is padded with 32 copies of its last row,
+          // so the loads stay inside it and read the clamped rows -- for up to
+          // four own pairs, no wait between their DMAs
+          struct R16 {
+            int32_t r[16];
+          };
+          const R16 rw = ldc(reinterpret_cast<const R16 *>(ai + r_rows + min(k0, r_nrows - 1)));
+          const int np = min(4, (seg - rG + 3) >> 2);
+          const bool past = k0 >= r_nrows;  // tile padding past the list end: the last row
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            if (u >= np) break;
+            const int r0 = past ? rw.r[0] : rw.r[4 * u], r1 = past ? rw.r[0] : rw.r[4 * u + 1];
+            const uint8_t *base = r_src + (int64_t)r0 * r_stride + r_b0;
+            const uint32_t gap = (uint32_t)((int64_t)(r1 - r0) * r_stride);
+            const uint32_t f = (uint32_t)((rslot & 7) | (((rslot >> 4) & 1) << 3));
+            uint32_t lc = lane_c ^ f;
+            if (16 * (int)lc >= r_nbytes) lc = 0;
+            dma16(lds_addr(lds) + (uint32_t)(O.ring + rslot * 512), base, (h ? gap : 0u) + 16u * lc);
+            rslot += 4;
+            if (rslot >= R) rslot -= R;
+          }
+          n += np;
+          rG += 4 * np;
+          continue;
+        }
+        // one pair clamped at the list end
         k0 = min(k0, r_nrows - 1);
         const int k1 = min(k0 + 1, r_nrows - 1);
-        const int r0 = r_rstep > 0 ? r_row0 + r_rstep * k0 : ldc1(ai + r_rows + k0);
-        const int r1 = r_rstep > 0 ? r_row0 + r_rstep * k1 : ldc1(ai + r_rows + k1);
+        const int r0 = r_row0 + r_rstep * k0, r1 = r_row0 + r_rstep * k1;
         const uint8_t *base = r_src + (int64_t)r0 * r_stride + r_b0;
         const uint32_t f = (uint32_t)((rslot & 7) | (((rslot >> 4) & 1) << 3));  // chunk swizzle of row rslot (rslot + 1: f ^ 1)
         uint32_t lc = lane_c ^ f;
@@ -888,7 +915,7 @@ VrLayout vr_lds_layout(int vpitch, bool q16) {
   L.otile_bytes = ((q16 ? kVmOtileBytes : 16 * kOt8Pitch) + 15) & ~15;
   const int rest = 2 * kABytes + 8 * kRecBytes + 16 + kLutSlots * 1024 + 6 * L.plane;
   const int fixed = ((rest + 15) & ~15) + 2 * L.otile_bytes;
-  int R = (kVpMaxLds - fixed) / 512 / 32 * 32;
+  int R = (kVrMaxLds - fixed) / 512 / 32 * 32;
   if (R > 256) R = 256;
   static const char *rmax = getenv("FI_VR_R");  // tuning: cap the ring
   if (rmax && atoi(rmax) >= 160 && R > atoi(rmax) / 32 * 32) R = atoi(rmax) / 32 * 32;
@@ -902,7 +929,7 @@ VrLayout vr_lds_layout(int vpitch, bool q16) {
 int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrTile *tiles, int ntiles,
               const int32_t *wginfo, int G, const int32_t *ai, VrLayout L) {
   if (ntiles <= 0 || G <= 0) return 0;
-  if (L.R <= 0 || L.total > kVpMaxLds) return -1;
+  if (L.R <= 0 || L.total > kVrMaxLds) return -1;
   static const char *variant = getenv("FI_VR_VARIANT");  // profiling ablations only
   const int v = variant ? atoi(variant) : 0;
 #define FI_VR_LAUNCH(m) \

@@ -48,8 +48,8 @@ int main() {
         MfmaH mh;
         if (build_mfma_h(h, &mh, mx)) sum += (long)mh.strips.size() + (long)mh.frag.size();
       }
-      RingTable rt;
-      if (build_ring(v, &rt)) sum += rt.K;
+      VrV vr;
+      if (build_vr_v(v, &vr)) sum += vr.nblk + (long)vr.frag.size() + (long)vr.bmeta.size();
     }
     if (flags & FI_OP_SMARTCROP) {
       fi_smartcrop_options o{};

@@ -4,8 +4,8 @@ source offsets of the later images -- and the descriptor / tile / strip
 offsets derived from them -- run past 2^32, through fi_process_batch_device
 (the bench's path), spot-checked against the oracle: pixels within +-1 LSB,
 smart-crop box bit-exact on the GPU-resized pixels, applied crop == that box.
-Also the same batch on the k_rs_vm kernel (FI_VP_RS=0) is bitwise
-equal to k_rs_vp's."""
+Also the same batch on the k_rs_vm kernel (FI_VR_RS=0) is bitwise
+equal to k_rs_vr's (the default)."""
 import os
 
 import numpy as np
@@ -37,7 +37,7 @@ def _ctx(env):
 
 @pytest.fixture(scope="module")
 def pool_ctx():
-    ctx = _ctx({"FI_VP_RS": "1"})
+    ctx = _ctx({"FI_VR_RS": "1"})
     stride = (W * 3 + 15) // 16 * 16
     img = stride * H
     pool = ctx.malloc(img * N)
@@ -68,11 +68,11 @@ def test_full_cfg2_batch_past_4gb(pool_ctx, opts):
     ctx, pool, stride, img = pool_ctx
     assert img * N > (1 << 32)
     op = ImageProcessor(OptionsBag(opts), W, H).to_op()
-    before = ctx.stats("path_vp")[1]
+    before = ctx.stats("path_vr")[1]
     rc, arr, dst, cap = _run(ctx, pool, stride, img, op)
     try:
         assert rc == 0 and all(arr[i].status == 0 for i in range(N))
-        assert ctx.stats("path_vp")[1] == before + N  # the persistent kernel ran the batch
+        assert ctx.stats("path_vr")[1] == before + N  # the persistent block-major kernel ran the batch
         idxs = verify_sample(N, img)
         assert max(idxs) * img > (1 << 32)
         ok, tot, err = verify_batch(ctx, arr, idxs, lambda i: pool + i * img, lambda i: 0xB16 + i, W, H, stride, op,
@@ -88,12 +88,12 @@ def test_full_cfg2_batch_vp_equals_vm(pool_ctx):
     ctx, pool, stride, img = pool_ctx
     op = ImageProcessor(OptionsBag("w_500"), W, H).to_op()
     rc, arr, dst, cap = _run(ctx, pool, stride, img, op)
-    vm = _ctx({"FI_VP_RS": "0"})
+    vm = _ctx({"FI_VR_RS": "0"})
     try:
         assert rc == 0
         rc2, arr2, dst2, cap2 = _run(vm, pool, stride, img, op)
         try:
-            assert rc2 == 0 and vm.stats("path_vp")[1] == 0
+            assert rc2 == 0 and vm.stats("path_vr")[1] == 0
             a = ctx.d2h(dst, cap * N)
             b = vm.d2h(dst2, cap * N)
             assert np.array_equal(a, b), int((a != b).sum())

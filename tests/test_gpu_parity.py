@@ -44,22 +44,15 @@ def _context_with(env):
                 os.environ[k] = v
 
 
-_ENV = {"FI_DISABLE_FUSED": "0", "FI_DISABLE_SC_PREP": "0", "FI_DISABLE_SC_MFMA": "0",
-        "FI_DISABLE_VM_RS": "0", "FI_DISABLE_SC_VQ": "0", "FI_DISABLE_SC_FZ": "0", "FI_DISABLE_HV_RS": "0",
-        "FI_DISABLE_SC_SKINSAT": "0"}
+_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0"}
 PATHS = {
-    # default kernels: k_rs_vm / k_rs_hv streaming MFMA resample; k_sc_fz fused prescale + maps; k_sc_score2
-    "vm": dict(_ENV),
-    # the unfused MFMA prescale: k_sc_hmfma + k_sc_vq (H-stage rows through HBM)
-    "nofz": dict(_ENV, FI_DISABLE_SC_FZ="1"),
-    # k_sc_fz evaluating skin / saturation per pixel in f64 instead of the colour table
-    "fzf64": dict(_ENV, FI_DISABLE_SC_SKINSAT="1"),
-    # VALU fused resample (k_rs_fused); VALU vertical prescale + maps (k_sc_vmaps)
-    "valu": dict(_ENV, FI_DISABLE_VM_RS="1", FI_DISABLE_HV_RS="1", FI_DISABLE_SC_VQ="1"),
-    # default resample with the VALU horizontal prescale (k_sc_hrows)
-    "schrows": dict(_ENV, FI_DISABLE_SC_MFMA="1"),
+    # default kernels: k_rs_vr (block-major persistent MFMA resample; k_rs_vm
+    # where its tables do not fit) / k_rs_hv; k_sc_fz fused prescale + maps; k_sc_score2
+    "vr": dict(_ENV),
+    # the fallbacks: k_rs_vm streaming resample; k_sc_hmfma + k_sc_vq (H-stage rows through HBM)
+    "vm": dict(_ENV, FI_VR_RS="0", FI_DISABLE_SC_FZ="1"),
     # generic kernels: two-pass resample; per-row prescale/maps kernels
-    "generic": dict(_ENV, FI_DISABLE_FUSED="1", FI_DISABLE_SC_PREP="1", FI_DISABLE_SC_MFMA="1"),
+    "generic": dict(_ENV, FI_FORCE_GENERIC="1"),
 }
 
 
@@ -72,8 +65,7 @@ def rctx(request):
     c.close()
 
 
-EXPECTED_PATH = {"vm": "path_vm", "nofz": "path_vm", "fzf64": "path_vm", "schrows": "path_vm", "valu": "path_fused",
-                 "generic": "path_generic_v"}
+EXPECTED_PATH = {"vr": "path_vr", "vm": "path_vm", "generic": "path_generic_v"}
 
 
 @pytest.mark.parametrize("W,H,opts", [
@@ -348,7 +340,7 @@ def test_horizontal_first_within_one_lsb_of_oracle(rctx, case):
     before = {p: rctx.stats(p)[1] for p in ("path_hv", "path_generic_h")}
     outs, recs, rc = rctx.process([src], [Op(tw, th, flags, g, rot)])
     assert rc == 0 and recs[0].status == 0, L.lib().fi_last_error()
-    want = "path_hv" if hv and rctx.path_name in ("vm", "nofz", "fzf64", "schrows") else "path_generic_h"
+    want = "path_hv" if hv and rctx.path_name in ("vr", "vm") else "path_generic_h"
     assert rctx.stats(want)[1] == before[want] + 1, (want, {p: rctx.stats(p)[1] - before[p] for p in before})
     ref = orc.im_convert(src, tw, th, _oracle_flags(flags), gravity=g, rotate=rot)
     _cmp(outs[0], ref, name)
@@ -465,11 +457,11 @@ def test_cfg4_slice_one_batch(ctx):
         ops.append(Op(op.target_w, op.target_h, op.flags & ~L.FI_OP_SMARTCROP_APPLY, op.gravity, op.rotate,
                       100, 100))
     h_before = ctx.stats("path_hv")[1]
-    vm_before = ctx.stats("path_vm")[1]
+    v_before = ctx.stats("path_vm")[1] + ctx.stats("path_vr")[1]
     outs, recs, rc = ctx.process(srcs, ops)
     assert rc == 0, L.lib().fi_last_error()
     assert ctx.stats("path_hv")[1] > h_before, "no horizontal-first geometry in the slice"
-    assert ctx.stats("path_vm")[1] > vm_before
+    assert ctx.stats("path_vm")[1] + ctx.stats("path_vr")[1] > v_before
 
     def check(j):
         op = ops[j]

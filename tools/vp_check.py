@@ -1,10 +1,9 @@
 #!/usr/bin/env python3
-"""k_rs_vp / k_rs_vr vs k_rs_vm: the persistent resample kernels must be
-bit-identical to the streaming kernel they replace (same weights, same integer
-algebra) on every geometry class.
+"""k_rs_vr vs k_rs_vm: the persistent block-major resample must be
+bit-identical to the streaming kernel (same weights, same integer algebra) on
+every geometry class; cases k_rs_vr does not take print vr_images 0.
 
-  python tools/vp_check.py            (GPU; k_rs_vp)
-  VR=1 python tools/vp_check.py       (GPU; k_rs_vr, block-major)
+  python tools/vp_check.py            (GPU)
 """
 import os
 import sys
@@ -50,10 +49,9 @@ CASES = [
     (640, 480, "w_320", 7),
 ]
 
-VR = os.environ.get("VR") == "1"
-KEY, PATH = ("FI_VR_RS", "path_vr") if VR else ("FI_VP_RS", "path_vp")
-vm = ctx_with({"FI_VP_RS": "0", "FI_VR_RS": "0"})
-vp = ctx_with({KEY: "1"})
+PATH = "path_vr"
+vm = ctx_with({"FI_VR_RS": "0"})
+vp = ctx_with({"FI_VR_RS": "1"})
 bad = 0
 for (W, H, opts, n) in CASES:
     op = ImageProcessor(OptionsBag(opts), W, H).to_op()
@@ -70,7 +68,7 @@ for (W, H, opts, n) in CASES:
             if a is not None and b is not None and a.shape == b.shape:
                 diff = max(diff, int(np.abs(a.astype(int) - b.astype(int)).max()))
                 nb = int((a != b).sum())
-    print(f"{W}x{H} {opts} x{n}: rc {rca}/{rcb} vp_images {ran} identical {same}"
+    print(f"{W}x{H} {opts} x{n}: rc {rca}/{rcb} vr_images {ran} identical {same}"
           + ("" if same else f" maxdiff {diff} ndiff {nb}"), flush=True)
     bad += (not same) or rca != 0 or rcb != 0
 print("FAIL" if bad else "OK", bad)

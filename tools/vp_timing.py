@@ -1,16 +1,16 @@
 #!/usr/bin/env python3
-"""Per-phase cycle sums of k_rs_vp (FI_VP_VARIANT=9 stamps, s_memtime ticks)
+"""Per-phase cycle sums of k_rs_vr (FI_VP_VARIANT=9 stamps, s_memtime ticks)
 on a full cfg2 batch, averaged over the persistent workgroups.
-V wave 0: tile entry, vertical MFMA issue, block done (planes), barrier.
-H wave 8: LUT staging, record / fragment reload, horizontal pass, stores, barrier.
-L wave 14: A-record DMA issue, piece DMA issue, vmcnt wait, barrier."""
+V waves 0-7: tile entry, vertical MFMA issue, block done (planes), barrier.
+H waves 8-12: -, record / fragment reload, horizontal pass, -, barrier.
+L waves 14-15: A-fragment DMA issue, row DMA issue, vmcnt wait, barrier."""
 import ctypes
 import os
 import sys
 
-VR = os.environ.get("VR") == "1"  # k_rs_vr instead of k_rs_vp
-os.environ["FI_VR_VARIANT" if VR else "FI_VP_VARIANT"] = os.environ.get("VP_STAMP_VARIANT", "9")
-os.environ["FI_VR_RS" if VR else "FI_VP_RS"] = "1"
+VR = True  # k_rs_vr (k_rs_vp was retired in round 3)
+os.environ["FI_VR_VARIANT"] = os.environ.get("VP_STAMP_VARIANT", "9")
+os.environ["FI_VR_RS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 
@@ -39,7 +39,7 @@ with Context(0) as ctx:
         L.check(ctx.process_device(arr, n))
     NS = 16 * 6
     buf = np.zeros(256 * NS, np.uint64)
-    fn = L.lib().fi_debug_vr_stamps if VR else L.lib().fi_debug_vp_stamps
+    fn = L.lib().fi_debug_vr_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
     L.check(fn(ctx.h, buf.ctypes.data, 256))
     a = buf.reshape(256, 16, 6).astype(np.float64)
