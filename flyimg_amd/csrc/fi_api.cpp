@@ -43,6 +43,8 @@ __global__ void k_sc_vpass(const ScDesc *, const int32_t *, int, const int32_t *
 __global__ void k_sc_maps(const ScDesc *, const int32_t *, int, const ScParamsDev);
 // per-image smartcrop kernels (fi_smartcrop.hip)
 int launch_sc_h(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai);
+int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
+                const ScParamsDev &P);
 int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
                  const ScParamsDev &P);
 int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
@@ -700,9 +702,9 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     }
     const Placed &q = pp->second;
     const fi_ctx::ScTabs &T = c->sc_at.at(&P);
-    // the per-image MFMA kernels (k_sc_fz, or k_sc_hmfma + k_sc_vq), else the
-    // generic per-row kernels
-    const bool prep = c->sc_prep && P.prep_ok && P.hm_ok && P.vq_ok;
+    // the per-image kernels (k_sc_fz; k_sc_hmfma + k_sc_vq, or k_sc_vmaps when the
+    // vertical window exceeds one MFMA block), else the generic per-row kernels
+    const bool prep = c->sc_prep && P.prep_ok && P.hm_ok;
     d.img = it.img;
     d.stride = it.stride;
     d.W = it.W;
@@ -734,8 +736,8 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.hmB = T.hmB;
     d.hmC = T.hmC;
     d.hmS0 = T.hmS0;
-    d.vq = prep ? 1 : 0;
-    d.fz = prep && P.fz_ok && c->sc_fz ? 1 : 0;
+    d.vq = prep && P.vq_ok ? 1 : 0;
+    d.fz = d.vq && P.fz_ok && c->sc_fz ? 1 : 0;
     d.vqA = T.vqA;
     d.vqC = T.vqC;
     d.vqK0 = T.vqK0;
@@ -790,8 +792,8 @@ static Launch add_launch(Blob &blob, const std::vector<Desc> &all, const std::ve
 // otherwise.
 struct ScLaunches {
   Launch red, hp, vp, maps;        // generic (fi_kernels.hip)
-  size_t hm_off = 0, vq_off = 0;   // k_sc_hmfma / k_sc_vq
-  int nhm = 0, hm_chunks = 0, hm_lds = 0;
+  size_t hm_off = 0, vq_off = 0, vm_off = 0;   // k_sc_hmfma / k_sc_vq / k_sc_vmaps
+  int nhm = 0, hm_chunks = 0, hm_lds = 0, nvm = 0, v_chunks = 0, v_lds = 0;
   size_t fz_off = 0;  // k_sc_fz
   int nfz = 0, fz_lds = 0;
   int nvq = 0, vq_chunks = 0, vq_lds = 0;
@@ -802,7 +804,7 @@ struct ScLaunches {
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> hm, sl, sg, vq, fz;
+  std::vector<ScDesc> hm, sl, sg, vq, vm, fz;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
     const ScDesc &d = SL.descs[k];
@@ -812,9 +814,15 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
       fz.push_back(d);
       X->fz_lds = std::max(X->fz_lds, P.fz_lds);
     } else if (d.prep) {
-      vq.push_back(d);
-      X->vq_chunks = std::max(X->vq_chunks, P.vq_chunks);
-      X->vq_lds = std::max(X->vq_lds, P.vq_lds);
+      if (d.vq) {
+        vq.push_back(d);
+        X->vq_chunks = std::max(X->vq_chunks, P.vq_chunks);
+        X->vq_lds = std::max(X->vq_lds, P.vq_lds);
+      } else {
+        vm.push_back(d);
+        X->v_chunks = std::max(X->v_chunks, P.v_chunks);
+        X->v_lds = std::max(X->v_lds, P.v_lds);
+      }
       hm.push_back(d);
       X->hm_chunks = std::max(X->hm_chunks, P.hm_chunks);
       X->hm_lds = std::max(X->hm_lds, P.hm_lds);
@@ -837,6 +845,8 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->hm_off = B.addv(hm);
   X->nhm = (int)hm.size();
   X->vq_off = B.addv(vq);
+  X->vm_off = B.addv(vm);
+  X->nvm = (int)vm.size();
   X->nvq = (int)vq.size();
   X->fz_off = B.addv(fz);
   X->nfz = (int)fz.size();
@@ -870,6 +880,7 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
       hipLaunchKernelGGL(k_sc_reduce, dim3(X.red.tiles), dim3(256), 0, st, desc(X.red), pre(X.red), X.red.n);
     if (launch_sc_h(st, (const ScDesc *)(ab + X.hm_off), X.nhm, X.hm_chunks, X.hm_lds, ai) != 0 ||
         launch_sc_vq(st, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0 ||
+        launch_sc_v(st, (const ScDesc *)(ab + X.vm_off), X.nvm, X.v_chunks, X.v_lds, ai, PD) != 0 ||
         launch_sc_fz(st, (const ScDesc *)(ab + X.fz_off), X.nfz, X.fz_lds, ai, PD, skinsat) != 0)
       return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d)", X.hm_lds, X.vq_lds, X.fz_lds);
     if (X.hp.tiles)
@@ -1414,24 +1425,41 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   if (G > 8) G -= G % 8;
   // the streams: tile t -> workgroup t % G; every phase's rows [K0, Rend) and the
   // next phase's must be resident together
+  // per (tables, band): glen, the rows the band needs resident at once inside
+  // it, Rend(b0) - kbase and K0(b1 - 1) - kbase (the seams between tiles)
+  struct Span {
+    int32_t glen, inner, head, tail;
+  };
+  std::map<std::tuple<const VrV *, int, int>, Span> spans;
+  auto span_of = [&](const VrV &V, int b0, int b1) -> const Span & {
+    auto it = spans.find(std::make_tuple(&V, b0, b1));
+    if (it != spans.end()) return it->second;
+    const int32_t *bm = V.bmeta.data();
+    const int kbase = bm[4 * b0];
+    Span sp{};
+    sp.glen = (bm[4 * (b1 - 1) + 2] - kbase + 15) / 16 * 16;
+    sp.head = bm[4 * b0 + 2] - kbase;
+    sp.tail = bm[4 * (b1 - 1)] - kbase;
+    sp.inner = sp.head;
+    for (int b = b0; b + 1 < b1; b++) sp.inner = std::max(sp.inner, bm[4 * (b + 1) + 2] - bm[4 * b]);
+    return spans.emplace(std::make_tuple(&V, b0, b1), sp).first->second;
+  };
   std::vector<int32_t> info(2 * (size_t)G, 0);
-  std::vector<int64_t> gpos(G, 0), prev_gk0(G, -1);
+  std::vector<int64_t> gpos(G, 0), prev_tail(G, -1);
   for (int t = 0; t < ntiles; t++) {
     VrTile &T = tiles[t];
     const VrV &V = *work[T.pad].V;
     const int g = t % G;
-    const int32_t *bm = V.bmeta.data();
-    T.kbase = bm[4 * T.b0];
-    const int kend = bm[4 * (T.b1 - 1) + 2];
-    T.glen = (kend - T.kbase + 15) / 16 * 16;
+    const Span &sp = span_of(V, T.b0, T.b1);
+    T.kbase = V.bmeta[4 * T.b0];
+    T.glen = sp.glen;
     T.g0 = (int32_t)gpos[g];
-    for (int b = T.b0; b < T.b1; b++) {
-      const int64_t gk0 = T.g0 + bm[4 * b] - T.kbase, grend = T.g0 + bm[4 * b + 2] - T.kbase;
-      if (grend - gk0 > L.R) return false;
-      if (prev_gk0[g] >= 0 && grend - prev_gk0[g] > L.R) return false;
-      prev_gk0[g] = gk0;
-      info[2 * g]++;
-    }
+    if (sp.inner > L.R) return false;
+    // the seam: this tile's first block's rows and the previous tile's last
+    // block's window resident together
+    if (prev_tail[g] >= 0 && T.g0 + sp.head - prev_tail[g] > L.R) return false;
+    prev_tail[g] = T.g0 + sp.tail;
+    info[2 * g] += T.b1 - T.b0;
     gpos[g] += T.glen;
     if (gpos[g] >= ((int64_t)1 << 30)) return false;
     T.pad = 0;
@@ -1568,8 +1596,7 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
         it = c->vrv_cache.emplace(w.vt, std::move(m)).first;
       }
       const VrV &V = it->second;
-      int64_t gap = 0;  // widest gap between consecutive touched rows (the DMA's per-lane offset)
-      for (size_t k = 1; k < V.rows.size(); k++) gap = std::max<int64_t>(gap, V.rows[k] - V.rows[k - 1]);
+      const int64_t gap = V.maxgap;  // the DMA's per-lane row offset
       bool narrow = true;  // five H waves take two horizontal items each: <= 3 16-px blocks per strip
       for (int st = 0; st < w.nstrips; st++) narrow = narrow && Bp.vstrips[w.first_strip + st].nocb <= 3;
       if (V.nblk > 0 && narrow && gap * Bp.vdescs[w.img].src_stride < ((int64_t)1 << 31))

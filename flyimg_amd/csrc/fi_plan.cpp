@@ -626,6 +626,7 @@ bool build_vr_v(const AxisTable &v, VrV *m) {
   m->rstep = nl > 1 ? m->rows[1] - m->rows[0] : 1;
   for (int k = 1; k < nl && m->rstep > 0; k++)
     if (m->rows[k] != m->row0 + m->rstep * k) m->rstep = 0;
+  for (int k = 1; k < nl; k++) m->maxgap = std::max(m->maxgap, m->rows[k] - m->rows[k - 1]);
   return true;
 }
 

@@ -144,6 +144,7 @@ struct VrV {
   std::vector<int32_t> bmeta;          // [nblk][4] {K0, ks, Rend, 0}
   std::vector<int32_t> frag;           // [nblk][2][3][256]
   std::vector<int32_t> w128;           // [16 nblk]
+  int32_t maxgap = 0;                  // widest gap between consecutive touched rows
 };
 bool build_vr_v(const AxisTable &v, VrV *m);
 

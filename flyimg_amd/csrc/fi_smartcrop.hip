@@ -9,6 +9,9 @@
 //   k_sc_hmfma + k_sc_vq  the same two passes as two kernels (H-stage rows
 //                 through HBM) where k_sc_fz's LDS does not fit (reduced
 //                 sources, wide analysed images).
+//   k_sc_vmaps    the vertical pass + maps on the VALU, where a 16-row
+//                 MFMA block's window exceeds 64 H-stage rows (prescale
+//                 factors > ~3: cfg5's 400 -> 111).
 //   k_sc_score2   every crop's score (smartcrop.py:300-338) + the argmax
 //                 (:116-133), maps resident in LDS: fast f64 pass with a
 //                 rigorous error bound, exact sequential re-score of the
@@ -175,6 +178,104 @@ __global__ __launch_bounds__(kPrepThreads) void k_sc_hmfma(const ScDesc *__restr
   }
 }
 
+
+// ---- k_sc_vmaps: Pillow's vertical pass + analyse() maps, one workgroup per
+// (image, chunk of kPrepRows output rows).  The H-stage rows the chunk and its
+// one-row halo need are staged in LDS (from hbuf, or from the source when no
+// horizontal pass runs), the prescaled rows [y0-1, y1+1) are computed into
+// LDS, then the maps of [y0, y1) are written.
+__global__ __launch_bounds__(kPrepThreads) void k_sc_vmaps(const ScDesc *__restrict__ descs,
+                                                           const int32_t *__restrict__ ai, const ScParamsDev P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const ScDesc &D = descs[blockIdx.x];
+  const int aw = D.aw, ah = D.ah;
+  const int y0 = blockIdx.y * kPrepRows;
+  if (y0 >= ah) return;
+  const int y1 = min(y0 + kPrepRows, ah);
+  const int pa = max(0, y0 - 1), pb = min(ah, y1 + 1);
+  const int tid = threadIdx.x;
+  const int apitch = (aw * 3 + 15) & ~15;
+  const int32_t *vb = ai + D.vb, *vk = ai + D.vk;
+  const bool need_v = D.need_v;
+  int lo = pa, hi = pb;
+  if (need_v) {
+    lo = vb[2 * pa];
+    hi = 0;
+    for (int y = pa; y < pb; y++) hi = max(hi, vb[2 * y] + vb[2 * y + 1]);
+  }
+  uint8_t *rows = lds8;                        // [hi - lo][apitch] H-stage rows
+  uint8_t *prer = lds8 + (hi - lo) * apitch;   // [pb - pa][apitch] prescaled rows
+  if (D.need_h) {
+    const int nq = apitch >> 4;
+    for (int it = tid; it < (hi - lo) * nq; it += kPrepThreads) {
+      const int rr = it / nq, k = it - rr * nq;
+      reinterpret_cast<uint4 *>(rows + rr * apitch)[k] =
+          reinterpret_cast<const uint4 *>(D.hbuf + (int64_t)(lo + rr) * apitch)[k];
+    }
+  } else {
+    const bool reduced = D.fx > 1 || D.fy > 1;
+    const uint8_t *src = reduced ? D.red : D.img;
+    const int64_t sstride = reduced ? (int64_t)D.rw * 3 : D.stride;
+    const int sC = reduced ? 3 : D.C;
+    for (int it = tid; it < (hi - lo) * aw; it += kPrepThreads) {
+      const int rr = it / aw, x = it - rr * aw;
+      const uint8_t *s = src + (int64_t)(lo + rr) * sstride + x * sC;
+      uint8_t *o = rows + rr * apitch + 3 * x;
+      o[0] = s[0];
+      o[1] = s[sC == 3 ? 1 : 0];
+      o[2] = s[sC == 3 ? 2 : 0];
+    }
+  }
+  __syncthreads();
+  for (int it = tid; it < (pb - pa) * aw; it += kPrepThreads) {
+    const int yr = it / aw, x = it - yr * aw, y = pa + yr;
+    uint8_t *q = prer + yr * apitch + 3 * x;
+    if (need_v) {
+      const int ymin = vb[2 * y], cnt = vb[2 * y + 1];
+      const int32_t *k = vk + y * D.ksv;
+      const uint8_t *p = rows + (ymin - lo) * apitch + 3 * x;
+      int32_t s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+      for (int j = 0; j < cnt; j++) {
+        const int32_t kj = k[j];
+        s0 += (int32_t)p[j * apitch] * kj;
+        s1 += (int32_t)p[j * apitch + 1] * kj;
+        s2 += (int32_t)p[j * apitch + 2] * kj;
+      }
+      q[0] = pil_clip8(s0);
+      q[1] = pil_clip8(s1);
+      q[2] = pil_clip8(s2);
+    } else {
+      const uint8_t *p = rows + (y - lo) * apitch + 3 * x;
+      q[0] = p[0];
+      q[1] = p[1];
+      q[2] = p[2];
+    }
+  }
+  __syncthreads();
+  for (int it = tid; it < (y1 - y0) * aw; it += kPrepThreads) {
+    const int yr = it / aw, x = it - yr * aw, y = y0 + yr;
+    const uint8_t *row = prer + (y - pa) * apitch;
+    const uint32_t r = row[3 * x], g = row[3 * x + 1], b = row[3 * x + 2];
+    if (D.pre) {
+      uint8_t *o = D.pre + ((int64_t)y * aw + x) * 3;
+      o[0] = (uint8_t)r;
+      o[1] = (uint8_t)g;
+      o[2] = (uint8_t)b;
+    }
+    const uint32_t L = sc_luma(r, g, b);
+    // detect_edge: ImagingFilter3x3 interior, border copies L
+    uint32_t E = L;
+    if (aw >= 3 && ah >= 3 && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
+      const uint8_t *up = row - apitch, *dn = row + apitch;
+      const int v = 4 * (int)L - (int)sc_luma(up[3 * x], up[3 * x + 1], up[3 * x + 2]) -
+                    (int)sc_luma(dn[3 * x], dn[3 * x + 1], dn[3 * x + 2]) -
+                    (int)sc_luma(row[3 * x - 3], row[3 * x - 2], row[3 * x - 1]) -
+                    (int)sc_luma(row[3 * x + 3], row[3 * x + 4], row[3 * x + 5]) + 1;
+      E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
+    }
+    D.maps[(int64_t)y * aw + x] = sc_skin_sat(r, g, b, L, P) | (E << 8);
+  }
+}
 
 // ---- k_sc_vq: Pillow's vertical pass (Resample.c ImagingResampleVertical_8bpc)
 // as exact integer MFMA, fused with analyse()'s maps.  One workgroup per
@@ -959,6 +1060,13 @@ int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds,
   if (n <= 0) return 0;
   if (lds > kPrepMaxLds) return -1;
   hipLaunchKernelGGL(k_sc_vq, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai, P);
+  return 0;
+}
+int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,
+                const ScParamsDev &P) {
+  if (n <= 0) return 0;
+  if (lds > kPrepMaxLds) return -1;
+  hipLaunchKernelGGL(k_sc_vmaps, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai, P);
   return 0;
 }
 int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, int max_px, const DevCrop *crops,
