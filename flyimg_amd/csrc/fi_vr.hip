@@ -196,7 +196,7 @@ __device__ __forceinline__ void wait_vm_le(int n) {
 }
 
 struct Rec {  // 32 B in LDS
-  int32_t t, blk, flags, slot0, ks, grend, pad0, pad1;
+  int32_t t, blk, flags, slot0, ks, grend, frag, w128;  // frag / w128: int32 offsets into ai
 };
 struct Lds {  // offsets of the launch's LDS regions
   int ring, a, rec, cnt, lut, planes, otile;
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
   };
   auto read_rec = [&](int s) -> Rec {
     const Rec x = recs[s & 7];
-    return Rec{ufl(x.t), ufl(x.blk), ufl(x.flags), ufl(x.slot0), ufl(x.ks), ufl(x.grend), 0, 0};
+    return Rec{ufl(x.t), ufl(x.blk), ufl(x.flags), ufl(x.slot0), ufl(x.ks), ufl(x.grend), ufl(x.frag), ufl(x.w128)};
   };
 
   if (wv >= kVW + kHW + kSW) {
@@ -299,7 +299,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       r.w128 = c_w128 + 16 * cb;
       r.flags = (cb == CT.b0 ? kFirst : 0) | ((s & 1) ? kSlot : 0) | ((ck & (kLutSlots - 1)) << kTslotShift);
       if (li == 0) {
-        if (lane == 0) recs[s & 7] = Rec{r.t, r.blk, r.flags, r.gk0 % R, r.ks, r.grend, 0, 0};
+        if (lane == 0) recs[s & 7] = Rec{r.t, r.blk, r.flags, r.gk0 % R, r.ks, r.grend, r.frag, r.w128};
         if ((r.flags & kFirst) && lane < (c_lut_n + 3) / 4)
           dma16(lds_addr(lds) + (uint32_t)(O.lut + (ck & (kLutSlots - 1)) * 1024),
                 reinterpret_cast<const uint8_t *>(ai + c_lut), 16u * lane);
@@ -835,24 +835,15 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       const int nx = h_nx;
       const bool fast8 = h_fast8;
       const uint32_t sh0 = h_sh0, shs = h_shs;
-      // per item: plane reads + MFMAs, then its epilogue; once the last item's
-      // reads have returned, the LDS counter tells the V waves the planes are free
+      // both items' plane reads first, then the LDS counter frees the planes for
+      // the V waves' next block; MFMAs and epilogues run on registers after that
       const int nk = (hw < h_items ? 1 : 0) + (hw + kHW < h_items ? 1 : 0);
-      auto signal = [&]() {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0)
-          atomicAdd(static_cast<unsigned *>(__builtin_assume_aligned(lds + O.cnt, 16)), 1u);
-      };
-      if (nk == 0) signal();
+      i32x4 Ahk[2][2], Alk[2][2];
 #pragma unroll
       for (int k = 0; k < 2; k++) {
-        if (k >= nk) break;
         const int it = hw + kHW * k;
-        const int ob = it / 3, chn = it - 3 * ob;
-        const int hw0 = hw0k[k], hks = hksk[k];
-        i32x4 hh[3], hl[3];
-#pragma unroll
-        for (int q = 0; q < 3; q++) hh[q] = hl[q] = i32x4{0, 0, 0, 0};
+        const int chn = it - 3 * (it / 3);
+        const int hw0 = hw0k[k], hks = k < nk ? hksk[k] : 0;
         const uint8_t *ph = planes + chn * plane, *pl = ph + 3 * plane;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
@@ -861,14 +852,30 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           const int o0 = col_off(cA) + 8 * (lane & 1), o1 = col_off(cA + 8) + 8 * (lane & 1);
           const i32x2 h0 = tr8(ph + o0), h1 = tr8(ph + o1);
           const i32x2 l0 = tr8(pl + o0), l1 = tr8(pl + o1);
-          const i32x4 Ah = {h0.x, h0.y, h1.x, h1.y}, Al = {l0.x, l0.y, l1.x, l1.y};
+          Ahk[k][t] = i32x4{h0.x, h0.y, h1.x, h1.y};
+          Alk[k][t] = i32x4{l0.x, l0.y, l1.x, l1.y};
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) atomicAdd(static_cast<unsigned *>(__builtin_assume_aligned(lds + O.cnt, 16)), 1u);
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        if (k >= nk) break;
+        const int it = hw + kHW * k;
+        const int ob = it / 3, chn = it - 3 * ob;
+        const int hks = hksk[k];
+        i32x4 hh[3], hl[3];
+#pragma unroll
+        for (int q = 0; q < 3; q++) hh[q] = hl[q] = i32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+          if (t >= hks) break;
 #pragma unroll
           for (int q = 0; q < 3; q++) {
-            hh[q] = mfma(Ah, hb[k][t][q], hh[q]);
-            hl[q] = mfma(Al, hb[k][t][q], hl[q]);
+            hh[q] = mfma(Ahk[k][t], hb[k][t][q], hh[q]);
+            hl[q] = mfma(Alk[k][t], hb[k][t][q], hl[q]);
           }
         }
-        if (k == nk - 1) signal();
         const int hx = 16 * ob + (lane & 15);
         if (hx < nx) {
           const float hws = hwsk[k];
