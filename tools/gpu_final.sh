@@ -19,10 +19,10 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
   python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/profile_bench.json" 2> "$OUT/prof.err"; rc=$?
 echo "rocprof rc=$rc"; ok $rc || exit $rc
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex "k_rs_vm" --output-format csv -d "$OUT/pmc_$c" -o run -- \
+  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex "k_rs_vr" --output-format csv -d "$OUT/pmc_$c" -o run -- \
     python3 "$ROOT/bench.py" --steps 1 --warmup 1 --images 512 --no-cpu-baseline > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err" || exit $?
 done
-python3 "$ROOT/tools/pmc_to_json.py" "$OUT" k_rs_vm 512 "$OUT/traffic_cfg2_k_rs_vm.json"
+python3 "$ROOT/tools/pmc_to_json.py" "$OUT" k_rs_vr 512 "$OUT/traffic_cfg2_k_rs_vr.json"
 cd "$ROOT"
 NIMG=1024 timeout -k 10 300 python tools/jpeg_bench.py > "$OUT/jpeg_bench.json" 2> "$OUT/jpeg_bench.err"; rc=$?
 echo "jpeg rc=$rc"; cat "$OUT/jpeg_bench.json"; ok $rc || exit $rc
