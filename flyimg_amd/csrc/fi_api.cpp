@@ -21,6 +21,8 @@
 #include <cstdlib>
 #include <cmath>
 #include <map>
+#include <queue>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -1401,30 +1403,6 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     desc_of[k] = (int32_t)Bp.vdescs.size();
     Bp.vdescs.push_back(m);
   }
-  std::vector<std::vector<VrTile>> q8(8);
-  for (size_t k = 0; k < work.size(); k++) {
-    const VrWork &w = work[k];
-    const int nblk = w.V->nblk;
-    int bands = nst > 0 ? (int)((2048 + nst - 1) / nst) : 1;
-    bands = std::max(1, std::min(bands, nblk));
-    for (int bnd = 0; bnd < bands; bnd++) {
-      const int b0 = (int)((int64_t)nblk * bnd / bands), b1 = (int)((int64_t)nblk * (bnd + 1) / bands);
-      if (b1 <= b0) continue;
-      for (int st = 0; st < w.nstrips; st++)
-        q8[k % 8].push_back(VrTile{desc_of[k], w.first_strip + st, b0, b1, 0, 0, 0, (int32_t)k});
-    }
-  }
-  std::vector<VrTile> tiles;
-  size_t mx = 0;
-  for (auto &q : q8) mx = std::max(mx, q.size());
-  for (size_t i = 0; i < mx; i++)
-    for (int x = 0; x < 8; x++)
-      if (i < q8[x].size()) tiles.push_back(q8[x][i]);
-  const int ntiles = (int)tiles.size();
-  int G = std::min(ntiles, c->n_cu);
-  if (G > 8) G -= G % 8;
-  // the streams: tile t -> workgroup t % G; every phase's rows [K0, Rend) and the
-  // next phase's must be resident together
   // per (tables, band): glen, the rows the band needs resident at once inside
   // it, Rend(b0) - kbase and K0(b1 - 1) - kbase (the seams between tiles)
   struct Span {
@@ -1444,27 +1422,93 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     for (int b = b0; b + 1 < b1; b++) sp.inner = std::max(sp.inner, bm[4 * (b + 1) + 2] - bm[4 * b]);
     return spans.emplace(std::make_tuple(&V, b0, b1), sp).first->second;
   };
-  std::vector<int32_t> info(2 * (size_t)G, 0);
-  std::vector<int64_t> gpos(G, 0), prev_tail(G, -1);
-  for (int t = 0; t < ntiles; t++) {
-    VrTile &T = tiles[t];
-    const VrV &V = *work[T.pad].V;
-    const int g = t % G;
-    const Span &sp = span_of(V, T.b0, T.b1);
-    T.kbase = V.bmeta[4 * T.b0];
-    T.glen = sp.glen;
-    T.g0 = (int32_t)gpos[g];
-    if (sp.inner > L.R) return false;
-    // the seam: this tile's first block's rows and the previous tile's last
-    // block's window resident together
-    if (prev_tail[g] >= 0 && T.g0 + sp.head - prev_tail[g] > L.R) return false;
-    prev_tail[g] = T.g0 + sp.tail;
-    info[2 * g] += T.b1 - T.b0;
-    gpos[g] += T.glen;
-    if (gpos[g] >= ((int64_t)1 << 30)) return false;
-    T.pad = 0;
+  // tiles (image, strip, band of blocks), costed as the rows they stream plus
+  // a per-phase overhead of 16 rows
+  struct TC {
+    VrTile t;
+    int64_t cost;
+  };
+  std::vector<TC> all;
+  std::vector<int64_t> img_cost(work.size(), 0);
+  for (size_t k = 0; k < work.size(); k++) {
+    const VrWork &w = work[k];
+    const int nblk = w.V->nblk;
+    int bands = nst > 0 ? (int)((2048 + nst - 1) / nst) : 1;
+    bands = std::max(1, std::min(bands, nblk));
+    for (int bnd = 0; bnd < bands; bnd++) {
+      const int b0 = (int)((int64_t)nblk * bnd / bands), b1 = (int)((int64_t)nblk * (bnd + 1) / bands);
+      if (b1 <= b0) continue;
+      const Span &sp = span_of(*w.V, b0, b1);
+      if (sp.inner > L.R) return false;
+      const int64_t cost = sp.glen + 16 * (b1 - b0);
+      for (int st = 0; st < w.nstrips; st++) {
+        all.push_back(TC{VrTile{desc_of[k], w.first_strip + st, b0, b1, 0, 0, 0, (int32_t)k}, cost});
+        img_cost[k] += cost;
+      }
+    }
   }
-  for (int g = 0; g < G; g++) info[2 * g + 1] = (int32_t)gpos[g];
+  const int ntiles = (int)all.size();
+  int G = std::min(ntiles, c->n_cu);
+  if (G > 8) G -= G % 8;
+  const int nx = G >= 8 ? 8 : 1;  // workgroup g runs on XCD g % 8
+  // images -> XCDs by LPT on their cost (an image's strips share halo columns
+  // in that XCD's L2), then each XCD's tiles -> its workgroups by LPT
+  std::vector<int> order(work.size());
+  for (size_t k = 0; k < work.size(); k++) order[k] = (int)k;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return img_cost[x] > img_cost[y]; });
+  std::vector<int> xcd_of(work.size(), 0);
+  {
+    std::vector<int64_t> load(nx, 0);
+    for (int k : order) {
+      const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      xcd_of[k] = x;
+      load[x] += img_cost[k];
+    }
+  }
+  std::stable_sort(all.begin(), all.end(), [](const TC &x, const TC &y) { return x.cost > y.cost; });
+  std::vector<std::vector<VrTile>> per(G);
+  {
+    // per XCD: a min-heap of (load, workgroup)
+    std::vector<std::priority_queue<std::pair<int64_t, int>, std::vector<std::pair<int64_t, int>>,
+                                    std::greater<std::pair<int64_t, int>>>>
+        heap(nx);
+    for (int g = 0; g < G; g++) heap[g % nx].push({0, g});
+    for (const TC &tc : all) {
+      auto &h = heap[xcd_of[tc.t.pad]];
+      auto top = h.top();
+      h.pop();
+      per[top.second].push_back(tc.t);
+      top.first += tc.cost;
+      h.push(top);
+    }
+  }
+  // the streams: workgroup g walks tiles [t0(g), t1(g)); every phase's rows
+  // [K0, Rend) and the next phase's must be resident together
+  std::vector<VrTile> tiles;
+  tiles.reserve(ntiles);
+  std::vector<int32_t> info(4 * (size_t)G, 0);
+  for (int g = 0; g < G; g++) {
+    int64_t gpos = 0, prev_tail = -1;
+    info[4 * g + 2] = (int32_t)tiles.size();
+    for (VrTile T : per[g]) {
+      const VrV &V = *work[T.pad].V;
+      const Span &sp = span_of(V, T.b0, T.b1);
+      T.kbase = V.bmeta[4 * T.b0];
+      T.glen = sp.glen;
+      T.g0 = (int32_t)gpos;
+      // the seam: this tile's first block's rows and the previous tile's last
+      // block's window resident together
+      if (prev_tail >= 0 && T.g0 + sp.head - prev_tail > L.R) return false;
+      prev_tail = T.g0 + sp.tail;
+      info[4 * g] += T.b1 - T.b0;
+      gpos += T.glen;
+      if (gpos >= ((int64_t)1 << 30)) return false;
+      T.pad = 0;
+      tiles.push_back(T);
+    }
+    info[4 * g + 1] = (int32_t)gpos;
+    info[4 * g + 3] = (int32_t)tiles.size();
+  }
   Bp.vrtiles = std::move(tiles);
   Bp.vr_info = std::move(info);
   Bp.vr_G = G;
@@ -1582,7 +1626,7 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     work.push_back({(int32_t)Bp.vdescs.size(), hp->second.first, (int32_t)H.strips.size(), &V, Bp.vm_vt[q]});
     Bp.vdescs.push_back(m);
   }
-  // k_rs_vr (FI_VR_RS=1): the images whose vertical axis has block-major
+  // k_rs_vr (default; FI_VR_RS=0 turns it off): the images whose vertical axis has block-major
   // tables (fi_plan.h VrV) run on the persistent block-major kernel
   Bp.vr_G = 0;
   if (c->vr_rs) {
@@ -1604,7 +1648,14 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
       else
         rest.push_back(w);
     }
-    if (!vr.empty() && build_vr_tiles(c, E, Bp, vr)) work.swap(rest);
+    // a persistent launch with static tile lists pays for mixed geometries
+    // (uneven tiles, per-tile table changes): measured on cfg4's mix (384 size
+    // classes x five ops) k_rs_vm took 385 ms against 432 with k_rs_vr, so a
+    // batch with more than kVrMaxClasses vertical tables stays on k_rs_vm
+    constexpr size_t kVrMaxClasses = 8;
+    std::set<const VrV *> classes;
+    for (const VrWork &w : vr) classes.insert(w.V);
+    if (!vr.empty() && classes.size() <= kVrMaxClasses && build_vr_tiles(c, E, Bp, vr)) work.swap(rest);
   }
   // bands of blocks only when the batch is too small to fill the chip
   int64_t nst = 0;

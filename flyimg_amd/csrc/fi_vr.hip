@@ -231,9 +231,11 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = ufl(tid >> 6);
-  const int G = (int)gridDim.x, g = (int)blockIdx.x;
-  const int N = ldc1(wginfo + 2 * g);         // phases (blocks) of this workgroup's stream
-  const int gend = ldc1(wginfo + 2 * g + 1);  // stream rows
+  const int g = (int)blockIdx.x;
+  // this workgroup's stream: tiles [t0, t1) (host LPT over the XCD's workgroups)
+  const int N = ldc1(wginfo + 4 * g);         // phases (blocks)
+  const int gend = ldc1(wginfo + 4 * g + 1);  // stream rows
+  const int t0 = ldc1(wginfo + 4 * g + 2), t1 = ldc1(wginfo + 4 * g + 3);
   const int R = Lo.R;
   const Lds O = lds_of(Lo);
   Rec *recs = reinterpret_cast<Rec *>(lds + O.rec);
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     struct PI {
       int t, blk, gk0, grend, ks, frag, w128, flags;
     };
-    int ct = g, ck = 0, cb = 0, c_bmeta = 0, c_frag = 0, c_w128 = 0, c_lut = 0, c_lut_n = 0;
+    int ct = t0, ck = 0, cb = 0, c_bmeta = 0, c_frag = 0, c_w128 = 0, c_lut = 0, c_lut_n = 0;
     VrTile CT{};
     auto ptile_load = [&]() {
       CT = ldc(tiles + ct);
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       c_lut_n = S.lut_n;
       cb = CT.b0;
     };
-    if (ct < ntiles) ptile_load();
+    if (ct < t1) ptile_load();
     // the phase at the cursor; writes its record (slot s) and stages its tile's
     // LUT (first block of a tile) -- L wave 0 only; advances the cursor
     auto next_phase = [&](int s) -> PI {
@@ -307,8 +309,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       cb++;
       if (cb >= CT.b1) {
         ck++;
-        ct += G;
-        if (ct < ntiles) ptile_load();
+        ct++;
+        if (ct < t1) ptile_load();
       }
       return r;
     };
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       }
     };
     // ---- row cursor: this wave's row pairs G = 4 m + 2 li of the stream ----
-    int rt = g, rG = 2 * li, rslot = 2 * li, n_issued = 0;
+    int rt = t0, rG = 2 * li, rslot = 2 * li, n_issued = 0;
     VrTile RT{};
     const uint8_t *r_src = nullptr;
     int64_t r_stride = 0;
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       r_rows = D.rows;
       r_nrows = D.nrows;
     };
-    if (rt < ntiles) rtile_load();
+    if (rt < t1) rtile_load();
     const uint32_t lane_c = (uint32_t)((lane & 31) ^ h);  // chunk of this lane before the row swizzle
     uint32_t pat[4] = {0, 0, 0, 0};                          // fast-path lane offsets of tile pat_tile
     int pat_tile = -1;
@@ -353,8 +355,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       int n = 0;
       while (rG < limit) {
         if (rG >= RT.g0 + RT.glen) {
-          rt += G;
-          rtile_load();  // the host makes the stream cover [0, gend): rt < ntiles here
+          rt++;
+          rtile_load();  // the host makes the stream cover [0, gend): rt < t1 here
           continue;
         }
         const int seg = min(limit, RT.g0 + RT.glen);
