@@ -1002,7 +1002,7 @@ static const MfmaH *vm_strips(fi_ctx *c, const AxisTable *ht, bool q16) {
   auto hit = c->vmh_cache.find({ht, q16});
   if (hit == c->vmh_cache.end()) {
     MfmaH m;
-    static const int first_nx = getenv("FI_VM_MAXNX") ? atoi(getenv("FI_VM_MAXNX")) : kVmMaxNx;  // tuning
+    const int first_nx = kVmMaxNx;
     for (int mx : {first_nx, 48, 32}) {
       if (!build_mfma_h(*ht, &m, mx)) {
         m = MfmaH();
@@ -1427,6 +1427,7 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   struct TC {
     VrTile t;
     int64_t cost;
+    const Span *sp;
   };
   std::vector<TC> all;
   std::vector<int64_t> img_cost(work.size(), 0);
@@ -1442,7 +1443,7 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
       if (sp.inner > L.R) return false;
       const int64_t cost = sp.glen + 16 * (b1 - b0);
       for (int st = 0; st < w.nstrips; st++) {
-        all.push_back(TC{VrTile{desc_of[k], w.first_strip + st, b0, b1, 0, 0, 0, (int32_t)k}, cost});
+        all.push_back(TC{VrTile{desc_of[k], w.first_strip + st, b0, b1, 0, 0, 0, (int32_t)k}, cost, &sp});
         img_cost[k] += cost;
       }
     }
@@ -1465,8 +1466,11 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
       load[x] += img_cost[k];
     }
   }
-  std::stable_sort(all.begin(), all.end(), [](const TC &x, const TC &y) { return x.cost > y.cost; });
-  std::vector<std::vector<VrTile>> per(G);
+  // equal costs (a uniform batch) keep the list order: no sort needed
+  bool uniform = true;
+  for (const TC &tc : all) uniform = uniform && tc.cost == all[0].cost;
+  if (!uniform) std::stable_sort(all.begin(), all.end(), [](const TC &x, const TC &y) { return x.cost > y.cost; });
+  std::vector<std::vector<const TC *>> per(G);
   {
     // per XCD: a min-heap of (load, workgroup)
     std::vector<std::priority_queue<std::pair<int64_t, int>, std::vector<std::pair<int64_t, int>>,
@@ -1477,7 +1481,7 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
       auto &h = heap[xcd_of[tc.t.pad]];
       auto top = h.top();
       h.pop();
-      per[top.second].push_back(tc.t);
+      per[top.second].push_back(&tc);
       top.first += tc.cost;
       h.push(top);
     }
@@ -1490,9 +1494,10 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   for (int g = 0; g < G; g++) {
     int64_t gpos = 0, prev_tail = -1;
     info[4 * g + 2] = (int32_t)tiles.size();
-    for (VrTile T : per[g]) {
+    for (const TC *tc : per[g]) {
+      VrTile T = tc->t;
       const VrV &V = *work[T.pad].V;
-      const Span &sp = span_of(V, T.b0, T.b1);
+      const Span &sp = *tc->sp;
       T.kbase = V.bmeta[4 * T.b0];
       T.glen = sp.glen;
       T.g0 = (int32_t)gpos;
@@ -1766,7 +1771,7 @@ static void build_hv_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   std::vector<std::vector<HvTile>> q8(8);  // XCD-aware order, as build_vm_tiles
   for (size_t k = 0; k < work.size(); k++) {
     const Work1 &w = work[k];
-    static const int64_t target = getenv("FI_HV_WGS") ? atoi(getenv("FI_HV_WGS")) : 8192;  // tuning
+    constexpr int64_t target = 8192;  // workgroups the bands aim for
     int bands = nst > 0 ? (int)((target + nst - 1) / nst) : 1;
     bands = std::max(1, std::min(bands, w.nblk / 6));
     for (int bnd = 0; bnd < bands; bnd++) {

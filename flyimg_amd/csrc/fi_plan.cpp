@@ -475,7 +475,6 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
     // plane pitch = 8 (mod 32) bytes: the fold's byte writes of rows 4 apart and the
     // fragment reads of rows 1 apart spread over the LDS banks
     S.pitch = pitch + ((8 - pitch % 32) + 32) % 32;
-    if (getenv("FI_DEBUG_MFMA_PITCH")) fprintf(stderr, "strip %d..%d ncols %d pitch %d\n", x0, x1, S.ncols, S.pitch);
     if (S.pitch > kMfmaMaxPitch) return false;
     S.vpitch = (pitch + 15) / 16 * 16;
     S.lut_px0 = S.b0 / 3;

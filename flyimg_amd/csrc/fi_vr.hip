@@ -926,8 +926,6 @@ VrLayout vr_lds_layout(int vpitch, bool q16) {
   const int fixed = ((rest + 15) & ~15) + 2 * L.otile_bytes;
   int R = (kVrMaxLds - fixed) / 512 / 32 * 32;
   if (R > 256) R = 256;
-  static const char *rmax = getenv("FI_VR_R");  // tuning: cap the ring
-  if (rmax && atoi(rmax) >= 160 && R > atoi(rmax) / 32 * 32) R = atoi(rmax) / 32 * 32;
   if (R < 160) R = 0;
   L.R = R;
   L.otile_off = (R * 512 + rest + 15) & ~15;

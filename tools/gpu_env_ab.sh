@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of one environment switch on the bench workload: runs with "$AB_ENV"
-# (e.g. FI_SC_LDS_MAPS=0) exported (B) and without (A), alternating.
+# (e.g. FI_VR_RS=0) exported (B) and without (A), alternating.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/envab

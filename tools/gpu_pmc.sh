@@ -1,17 +1,17 @@
 #!/bin/bash
 # PMC passes (counters only + kernel trace; no sys/runtime trace) for the
-# fused resample kernel on a reduced bench run.  One pass per counter group.
+# resample kernel (k_rs_vr by default) on a reduced bench run.  One pass per counter group.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out/pmc
+OUT=$ROOT/gpurun_out/pmc/${PMC_TAG:-run}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-REGEX=${REGEX:-k_rs_fused}
+REGEX=${REGEX:-k_rs_vr}
 ARGS=${PMC_BENCH_ARGS:---steps 1 --warmup 1 --images 512 --no-cpu-baseline}
 pass() {
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "$REGEX" --output-format csv -d "$OUT/$name" -o run -- \
+  timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-include-regex "$REGEX" --output-format csv -d "$OUT/$name" -o run -- \
     python "$ROOT/bench.py" $ARGS > "$OUT/$name.bench.json" 2> "$OUT/$name.err"; local rc=$?
   echo "pass $name rc=$rc"; return $rc
 }
