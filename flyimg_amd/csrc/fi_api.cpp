@@ -1381,9 +1381,6 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     if (vp == c->vr_at.end()) {
       std::array<int32_t, 4> o;
       o[0] = put(V.rows);
-      // k_rs_vr reads the rows table 16 entries at a time from any list index
-      // below nrows: 32 copies of the last row keep those reads inside it
-      E.ai.insert(E.ai.end(), 32, V.rows.back());
       align4();
       o[1] = put(V.bmeta);
       o[2] = put(V.w128);

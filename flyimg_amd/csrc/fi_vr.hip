@@ -330,7 +330,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     VrTile RT{};
     const uint8_t *r_src = nullptr;
     int64_t r_stride = 0;
-    int r_b0 = 0, r_nbytes = 0, r_row0 = 0, r_rstep = 0, r_rows = 0, r_nrows = 0;
+    int r_b0 = 0, r_nbytes = 0, r_row0 = 0, r_rstep = 0, r_nrows = 0;
     auto rtile_load = [&]() {
       RT = ldc(tiles + rt);
       const VDesc D = ldc(descs + RT.img);
@@ -341,7 +341,6 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       r_nbytes = S.nbytes;
       r_row0 = D.row0;
       r_rstep = D.rstep;
-      r_rows = D.rows;
       r_nrows = D.nrows;
     };
     if (rt < t1) rtile_load();
@@ -349,8 +348,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     uint32_t pat[4] = {0, 0, 0, 0};                          // fast-path lane offsets of tile pat_tile
     int pat_tile = -1;
     // issue this wave's pairs up to stream row `limit`; returns the DMAs issued.
-    // Evenly spaced rows (rstep > 0) go through a loop with no loads: bases
-    // linear in the pair index, the chunk swizzle from the ring slot.
+    // The touched rows are evenly spaced (rstep > 0, build_vr_v): a loop with
+    // no loads, bases linear in the pair index, the chunk swizzle from the ring slot.
     auto issue_rows = [&](int limit) -> int {
       int n = 0;
       while (rG < limit) {
@@ -361,7 +360,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         }
         const int seg = min(limit, RT.g0 + RT.glen);
         int k0 = RT.kbase + (rG - RT.g0);
-        if (r_rstep > 0 && k0 + 1 < r_nrows) {
+        if (k0 + 1 < r_nrows) {
           // pairs with k0 + 1 < nrows and rG < seg
           const int cnt = min((seg - rG + 3) >> 2, (r_nrows - 1 - k0 + 3) >> 2);
           const int64_t rs = (int64_t)r_rstep * r_stride;
@@ -439,34 +438,6 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           }
           n += cnt;
           rG += 4 * cnt;
-          continue;
-        }
-        if (r_rstep == 0) {
-          // rows table (ThumbnailImage samples at uneven row gaps): 16 list rows
-          // per scalar load -- the table is padded with 32 copies of its last row,
-          // so the loads stay inside it and read the clamped rows -- for up to
-          // four own pairs, no wait between their DMAs
-          struct R16 {
-            int32_t r[16];
-          };
-          const R16 rw = ldc(reinterpret_cast<const R16 *>(ai + r_rows + min(k0, r_nrows - 1)));
-          const int np = min(4, (seg - rG + 3) >> 2);
-          const bool past = k0 >= r_nrows;  // tile padding past the list end: the last row
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            if (u >= np) break;
-            const int r0 = past ? rw.r[0] : rw.r[4 * u], r1 = past ? rw.r[0] : rw.r[4 * u + 1];
-            const uint8_t *base = r_src + (int64_t)r0 * r_stride + r_b0;
-            const uint32_t gap = (uint32_t)((int64_t)(r1 - r0) * r_stride);
-            const uint32_t f = (uint32_t)((rslot & 7) | (((rslot >> 4) & 1) << 3));
-            uint32_t lc = lane_c ^ f;
-            if (16 * (int)lc >= r_nbytes) lc = 0;
-            dma16(lds_addr(lds) + (uint32_t)(O.ring + rslot * 512), base, (h ? gap : 0u) + 16u * lc);
-            rslot += 4;
-            if (rslot >= R) rslot -= R;
-          }
-          n += np;
-          rG += 4 * np;
           continue;
         }
         // one pair clamped at the list end

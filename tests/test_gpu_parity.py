@@ -68,20 +68,24 @@ def rctx(request):
 EXPECTED_PATH = {"vr": "path_vr", "vm": "path_vm", "generic": "path_generic_v"}
 
 
-@pytest.mark.parametrize("W,H,opts", [
-    (1920, 1080, "w_500"),                       # cfg2
-    (3840, 2160, "w_512,h_512,c_1"),             # cfg3
-    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray"),  # cfg5
-    (3000, 2000, "w_300,h_250,c_1"),             # cfg1
+@pytest.mark.parametrize("W,H,opts,even_rows", [
+    (1920, 1080, "w_500", True),                       # cfg2
+    (3840, 2160, "w_512,h_512,c_1", True),             # cfg3
+    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", True),  # cfg5 (sampled rows 2 apart)
+    (3000, 2000, "w_300,h_250,c_1", False),            # cfg1 (sampled rows at uneven gaps)
 ])
-def test_baseline_geometries_take_the_path(rctx, W, H, opts):
+def test_baseline_geometries_take_the_path(rctx, W, H, opts, even_rows):
     """The BASELINE geometries run on the kernel the path names (no silent
-    fallback to another resample kernel)."""
+    fallback to another resample kernel); k_rs_vr takes evenly spaced touched
+    rows only, so cfg1's thumbnail-sampled rows run on k_rs_vm on every
+    vertical-first MFMA path."""
     from flyimg_amd.processor import ImageProcessor, OptionsBag
 
     op = ImageProcessor(OptionsBag(opts), W, H).to_op()
     src = synth_rgb(W, H, 7)
     want = EXPECTED_PATH[rctx.path_name]
+    if want == "path_vr" and not even_rows:
+        want = "path_vm"
     before = rctx.stats(want)[1]
     outs, recs, rc = rctx.process([src], [op])
     assert rc == 0 and recs[0].status == 0
