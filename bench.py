@@ -261,7 +261,8 @@ def main():
     ctx.set_timing(False)
     el = t1 - t0
     stats = {k: ctx.stats(k) for k in ("batch", "resize", "sc_prep", "sc_score", "crop_apply",
-                                      "host_plan", "host_launch", "host_wait", "host_total")}
+                                      "host_plan", "host_plan_images", "host_plan_sc", "host_plan_tiles",
+                                      "host_plan_blob", "host_launch", "host_wait", "host_total")}
     # images per resample kernel over the timed steps (counts kept by the library)
     paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in KERNEL_OF_PATH}
     last = arrs[(args.warmup + args.steps - 1) % 2]

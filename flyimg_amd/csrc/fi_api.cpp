@@ -1448,7 +1448,9 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   const int ntiles = (int)all.size();
   int G = std::min(ntiles, c->n_cu);
   if (G > 8) G -= G % 8;
-  const int nx = G >= 8 ? 8 : 1;  // workgroup g runs on XCD g % 8
+  // workgroup g runs on XCD g % 8; with fewer than 4 images per XCD (small
+  // batches, the serving shape) the tiles spread over every workgroup instead
+  const int nx = G >= 8 && work.size() >= 32 ? 8 : 1;
   // images -> XCDs by LPT on their cost (an image's strips share halo columns
   // in that XCD's L2), then each XCD's tiles -> its workgroups by LPT
   std::vector<int> order(work.size());
