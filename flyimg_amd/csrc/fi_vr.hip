@@ -551,40 +551,38 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         const i32x4 corr = al[384 + (lane >> 4)];  // 128 * weight sums of this lane's 4 output rows
         i32x4 acc[3][kT];
         const uint32_t RB = (uint32_t)R * 512u;
+        // both k-steps' ring and A reads in flight before the first MFMA
+        i32x4 Bt[2][kT], At[2][3];
 #pragma unroll
         for (int t = 0; t < 2; t++) {
           if (t >= C.ks) break;
           int sb = C.slot0 + 64 * t;
           if (sb >= R) sb -= R;
-          // ring rows sb + rA (+ 8), wrapped: min(y, y - RB) in unsigned arithmetic
           const uint32_t y0 = (uint32_t)(sb + rA) * 512u, y1 = y0 + 8u * 512u;
           const uint32_t Y0 = min(y0, y0 - RB), Y1 = min(y1, y1 - RB);
           const uint32_t sx = (uint32_t)((sb >> 4) & 1) << 7;
-          i32x4 B[kT];
 #pragma unroll
           for (int j = 0; j < kT; j++) {
             const uint32_t o = offj[j] ^ sx;
             const i32x2 lo = tr8(lds + O.ring + Y0 + o), hi = tr8(lds + O.ring + Y1 + o);
-            B[j] = i32x4{lo.x, lo.y, hi.x, hi.y} ^ i32x4{(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+            Bt[t][j] = i32x4{lo.x, lo.y, hi.x, hi.y} ^ i32x4{(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
           }
-          i32x4 A[3];
 #pragma unroll
-          for (int q = 0; q < 3; q++) A[q] = al[(t * 3 + q) * 64 + lane];
-          if (t == 0) {
+          for (int q = 0; q < 3; q++) At[t][q] = al[(t * 3 + q) * 64 + lane];
+        }
 #pragma unroll
-            for (int j = 0; j < kT; j++) acc[0][j] = mfma(A[0], B[j], corr);
+        for (int j = 0; j < kT; j++) acc[0][j] = mfma(At[0][0], Bt[0][j], corr);
 #pragma unroll
-            for (int j = 0; j < kT; j++) acc[1][j] = mfma(A[1], B[j], i32x4{0, 0, 0, 0});
+        for (int j = 0; j < kT; j++) acc[1][j] = mfma(At[0][1], Bt[0][j], i32x4{0, 0, 0, 0});
 #pragma unroll
-            for (int j = 0; j < kT; j++) acc[2][j] = mfma(A[2], B[j], i32x4{0, 0, 0, 0});
-          } else {
+        for (int j = 0; j < kT; j++) acc[2][j] = mfma(At[0][2], Bt[0][j], i32x4{0, 0, 0, 0});
+        if (C.ks > 1) {
 #pragma unroll
-            for (int j = 0; j < kT; j++) acc[0][j] = mfma(A[0], B[j], acc[0][j]);
+          for (int j = 0; j < kT; j++) acc[0][j] = mfma(At[1][0], Bt[1][j], acc[0][j]);
 #pragma unroll
-            for (int j = 0; j < kT; j++) acc[1][j] = mfma(A[1], B[j], acc[1][j]);
+          for (int j = 0; j < kT; j++) acc[1][j] = mfma(At[1][1], Bt[1][j], acc[1][j]);
 #pragma unroll
-            for (int j = 0; j < kT; j++) acc[2][j] = mfma(A[2], B[j], acc[2][j]);
-          }
+          for (int j = 0; j < kT; j++) acc[2][j] = mfma(At[1][2], Bt[1][j], acc[2][j]);
         }
         stamp(1);
         // the H waves' reads of block p - 1's planes are done (single plane buffer)
