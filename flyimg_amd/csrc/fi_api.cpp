@@ -1406,9 +1406,14 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     int32_t glen, inner, head, tail;
   };
   std::map<std::tuple<const VrV *, int, int>, Span> spans;
+  std::tuple<const VrV *, int, int> last_key{nullptr, -1, -1};
+  const Span *last_sp = nullptr;
   auto span_of = [&](const VrV &V, int b0, int b1) -> const Span & {
-    auto it = spans.find(std::make_tuple(&V, b0, b1));
-    if (it != spans.end()) return it->second;
+    const auto key = std::make_tuple(&V, b0, b1);
+    if (last_sp && key == last_key) return *last_sp;  // consecutive images mostly share tables
+    last_key = key;
+    auto it = spans.find(key);
+    if (it != spans.end()) return *(last_sp = &it->second);
     const int32_t *bm = V.bmeta.data();
     const int kbase = bm[4 * b0];
     Span sp{};
@@ -1417,7 +1422,8 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     sp.tail = bm[4 * (b1 - 1)] - kbase;
     sp.inner = sp.head;
     for (int b = b0; b + 1 < b1; b++) sp.inner = std::max(sp.inner, bm[4 * (b + 1) + 2] - bm[4 * b]);
-    return spans.emplace(std::make_tuple(&V, b0, b1), sp).first->second;
+    last_sp = &spans.emplace(key, sp).first->second;
+    return *last_sp;
   };
   // tiles (image, strip, band of blocks), costed as the rows they stream plus
   // a per-phase overhead of 16 rows
@@ -1470,7 +1476,15 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   for (const TC &tc : all) uniform = uniform && tc.cost == all[0].cost;
   if (!uniform) std::stable_sort(all.begin(), all.end(), [](const TC &x, const TC &y) { return x.cost > y.cost; });
   std::vector<std::vector<const TC *>> per(G);
-  {
+  if (uniform) {
+    // equal costs: LPT is a round robin over each XCD's workgroups
+    std::vector<int> next(nx, 0);
+    const int per_x = G / nx;
+    for (const TC &tc : all) {
+      const int x = xcd_of[tc.t.pad];
+      per[x + nx * (next[x]++ % per_x)].push_back(&tc);
+    }
+  } else {
     // per XCD: a min-heap of (load, workgroup)
     std::vector<std::priority_queue<std::pair<int64_t, int>, std::vector<std::pair<int64_t, int>>,
                                     std::greater<std::pair<int64_t, int>>>>
