@@ -1804,6 +1804,12 @@ static void build_hv_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
 // the upload blob E.blob.
 static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
   Blob &B = E.blob;
+  // one allocation for the whole blob (no regrowth copies of megabytes of tiles)
+  auto bytes = [](const auto &v) { return v.size() * sizeof(v[0]) + 256; };
+  B.b.reserve(B.b.size() + bytes(Bp.rd) + bytes(Bp.vdescs) + bytes(Bp.vstrips) + bytes(Bp.vtiles) +
+              bytes(Bp.vrtiles) + bytes(Bp.vr_info) + bytes(Bp.hdescs) + bytes(Bp.hstrips) + bytes(Bp.htiles) +
+              bytes(Bp.apply) + bytes(E.ai) + bytes(E.af) + bytes(E.ad) + 32 * sizeof(int32_t) * Bp.rd.size() +
+              (size_t)1 << 20);
   std::vector<int> m0, m1, m2, q0, q1, q2;  // q*: RGBA (matte) images of modes 0 / 1 / 2
   for (size_t k = 0; k < Bp.rd.size(); k++) {
     if (Bp.rd[k].mode >= 3) continue;
