@@ -1452,6 +1452,7 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     }
   }
   const int ntiles = (int)all.size();
+  if (ntiles == 0) return false;
   int G = std::min(ntiles, c->n_cu);
   if (G > 8) G -= G % 8;
   // workgroup g runs on XCD g % 8; with fewer than 4 images per XCD (small
