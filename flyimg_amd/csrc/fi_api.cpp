@@ -212,7 +212,7 @@ struct fi_ctx {
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
   bool fast_rs = true;  // FI_FORCE_GENERIC=1: the generic two-pass resample (and smartcrop) kernels only
   bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
-  int n_cu = 256;        // compute units (k_rs_vp: one persistent workgroup per CU)
+  int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
   DevBuf jpeg[3];           // GPU JPEG decode: upload (compressed data + tables), -, coefficients + planes
@@ -1592,7 +1592,7 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
         align4();
         o[1] = put(H.frag);
         o[2] = put(H.s0);
-        align4();  // 16-byte aligned LUT rows (k_rs_vp's LDS-DMA)
+        align4();  // 16-byte aligned LUT rows (k_rs_vr's LDS-DMA)
         o[3] = put(H.lut);
         ht = c->mh_at.emplace(&H, o).first;
       }

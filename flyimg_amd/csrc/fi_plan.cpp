@@ -486,7 +486,7 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
       if (px >= h.src_lo && px < h.src_hi && idx[px - h.src_lo] >= 0) ci = idx[px - h.src_lo] - S.c_lo;
       m->lut.push_back(ci >= 0 && ci < S.ncols ? ci : -1);
     }
-    while (m->lut.size() % 4) m->lut.push_back(-1);  // 16-byte rows: k_rs_vp stages the LUT by LDS-DMA
+    while (m->lut.size() % 4) m->lut.push_back(-1);  // 16-byte rows: k_rs_vr stages the LUT by LDS-DMA
     S.frag = m->frag.size();
     m->frag.resize(m->frag.size() + (size_t)S.nocb * S.ks * 3 * 256, 0);
     for (int ob = 0; ob < S.nocb; ob++)

@@ -3,11 +3,11 @@
 // warp-specialised, exact-integer matrix-core pipeline with a BLOCK-MAJOR
 // vertical pass: v_mfma_i32_16x16x64_i8.
 //
-// Same weights, limbs and float conversions as k_rs_vm / k_rs_vp (bit-identical
+// Same weights, limbs and float conversions as k_rs_vm (bit-identical
 // outputs); what differs is how the vertical pass walks the source rows
 // (fi_plan.h VrV):
 //
-//  * k_rs_vm / k_rs_vp cut the touched rows into pieces of <= 64 rows aligned to
+//  * k_rs_vm cuts the touched rows into pieces of <= 64 rows aligned to
 //    the 16-row output blocks, and every piece feeds two accumulator slots (its
 //    own block and the next) -- so a block whose rows do not fit one piece
 //    (every ThumbnailImage geometry: 80 sampled rows per block, 67-80 touched
@@ -19,18 +19,20 @@
 //    ks <= 2 k-steps x 3 weight limbs into three separate accumulators per
 //    column tile (no shifts; folded once per block), then the Q16 planes.
 //
-//  Roles per phase (one workgroup barrier per phase, as k_rs_vp):
-//    V waves 0-7   block p: vertical MFMAs from the ring, fold, Q16 planes
-//                  (single plane buffer: a wave writes it only after the six
-//                  H waves have counted their reads of block p - 1 off an LDS
-//                  counter);
-//    H waves 8-13  block p - 1: horizontal MFMAs from the planes -> output
-//                  tile slot (p - 1) & 1;
+//  Roles per phase (one workgroup barrier per phase):
+//    V waves 0-7   block p: vertical MFMAs from the ring (both k-steps' reads
+//                  issued first), fold, Q16 planes (single plane buffer: a wave
+//                  writes it only after the five H waves have counted their
+//                  reads of block p - 1 off an LDS counter);
+//    H waves 8-12  block p - 1: both items' plane reads, the counter, then the
+//                  horizontal MFMAs -> output tile slot (p - 1) & 1;
+//    S wave 13     the stores of block p - 2;
 //    L waves 14-15 the stream cursor: source row pairs by LDS-DMA (ring slot
 //                  G mod R, G < K0(p) + R), A fragments of block p + 1, the
-//                  record of phase p + 2 (+ the strip's LUT), the stores of
-//                  block p - 2; the end-of-phase vmcnt waits exactly for the
-//                  rows of block p + 1.
+//                  record of phase p + 2 (+ the strip's LUT); the end-of-phase
+//                  vmcnt waits exactly for the rows of block p + 1.
+//  Each workgroup walks its own tile range [t0, t1) (host: LPT over the
+//  XCD's workgroups); the touched rows are evenly spaced (build_vr_v).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
