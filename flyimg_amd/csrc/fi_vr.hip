@@ -56,8 +56,8 @@ constexpr int kHW = 5;                   // H waves 8-12: horizontal items hw, h
 constexpr int kSW = 1;                   // S wave 13: the stores of the output tile of phase p - 2
 constexpr int kLW = 2;                   // L waves 14-15
 static_assert(kVW + kHW + kSW + kLW == 16, "16 waves");
-constexpr int kABytes = 6144 + 64;       // [t][limb][64 lanes][16 B] + w128 of the block's 16 rows
-constexpr int kRecBytes = 32;
+constexpr int kABytes = 6144;            // [t][limb][64 lanes][16 B]
+constexpr int kRecBytes = 96;
 constexpr int kLutSlots = 4;
 constexpr int kPlanePad = 176;           // 44 (mod 64) dwords: see fi_vm.hip kVmPlanePad
 constexpr int kOt8Pitch = 200;           // 8-bit output tile row (<= 64 px x 3 + the row shift)
@@ -199,6 +199,10 @@ __device__ __forceinline__ void wait_vm_le(int n) {
 
 struct Rec {  // 32 B in LDS
   int32_t t, blk, flags, slot0, ks, grend, frag, w128;  // frag / w128: int32 offsets into ai
+  int32_t corr[16];  // 128 * weight sums of the block's 16 output rows (the MFMA bias)
+};
+struct W16 {
+  int32_t v[16];
 };
 struct Lds {  // offsets of the launch's LDS regions
   int ring, a, rec, cnt, lut, planes, otile;
@@ -303,7 +307,15 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       r.w128 = c_w128 + 16 * cb;
       r.flags = (cb == CT.b0 ? kFirst : 0) | ((s & 1) ? kSlot : 0) | ((ck & (kLutSlots - 1)) << kTslotShift);
       if (li == 0) {
-        if (lane == 0) recs[s & 7] = Rec{r.t, r.blk, r.flags, r.gk0 % R, r.ks, r.grend, r.frag, r.w128};
+        // the bias row rides in the record (scalar loads two phases ahead) instead
+        // of a 64-byte DMA in the loader's stream
+        const W16 wc = ldc(reinterpret_cast<const W16 *>(ai + r.w128));
+        if (lane == 0) {
+          Rec rr{r.t, r.blk, r.flags, r.gk0 % R, r.ks, r.grend, r.frag, r.w128, {}};
+#pragma unroll
+          for (int k = 0; k < 16; k++) rr.corr[k] = wc.v[k];
+          recs[s & 7] = rr;
+        }
         if ((r.flags & kFirst) && lane < (c_lut_n + 3) / 4)
           dma16(lds_addr(lds) + (uint32_t)(O.lut + (ck & (kLutSlots - 1)) * 1024),
                 reinterpret_cast<const uint8_t *>(ai + c_lut), 16u * lane);
@@ -316,16 +328,12 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       }
       return r;
     };
-    // A fragments (ks k-steps x 3 limbs x 1 KB) + the block's w128 row into A slot `slot`
+    // A fragments (ks k-steps x 3 limbs x 1 KB) into A slot `slot`
     auto issue_a = [&](const PI &r, int slot) {
       const uint32_t m0 = lds_addr(lds) + (uint32_t)(O.a + slot * kABytes);
       const int nf = 3 * r.ks;
-      for (int i = li; i <= nf; i += kLW) {
-        if (i < nf)
-          dma16(m0 + 1024 * i, reinterpret_cast<const uint8_t *>(ai + r.frag) + 1024 * i, 16u * lane);
-        else if (lane < 4)
-          dma16(m0 + 6144, reinterpret_cast<const uint8_t *>(ai + r.w128), 16u * lane);
-      }
+      for (int i = li; i < nf; i += kLW)
+        dma16(m0 + 1024 * i, reinterpret_cast<const uint8_t *>(ai + r.frag) + 1024 * i, 16u * lane);
     };
     // ---- row cursor: this wave's row pairs G = 4 m + 2 li of the stream ----
     int rt = t0, rG = 2 * li, rslot = 2 * li, n_issued = 0;
@@ -550,7 +558,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         }
         stamp(0);
         const i32x4 *al = reinterpret_cast<const i32x4 *>(lds + O.a + (p & 1) * kABytes);
-        const i32x4 corr = al[384 + (lane >> 4)];  // 128 * weight sums of this lane's 4 output rows
+        // 128 * weight sums of this lane's 4 output rows, from block p's record
+        const i32x4 corr = *reinterpret_cast<const i32x4 *>(&recs[p & 7].corr[4 * (lane >> 4)]);
         i32x4 acc[3][kT];
         const uint32_t RB = (uint32_t)R * 512u;
         // both k-steps' ring and A reads in flight before the first MFMA
