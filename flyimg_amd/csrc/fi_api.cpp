@@ -77,7 +77,7 @@ size_t vm_lds_bytes(int vpitch, int nocb, int ks, bool q16);
 int vm_read_stamps(uint64_t *out, int slots);
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
-// its persistent warp-specialised form (fi_vp.hip)
+// its persistent block-major form (fi_vr.hip)
 VrLayout vr_lds_layout(int vpitch, bool q16);
 int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrTile *tiles, int ntiles,
               const int32_t *wginfo, int G, const int32_t *ai, VrLayout L);
@@ -247,7 +247,7 @@ struct fi_ctx {
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_at;
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
   std::map<const VrV *, std::array<int32_t, 4>> vr_at;    // rows, bmeta, w128, frag
-  std::map<const MfmaH *, std::array<int32_t, 4>> mh_at;  // wsum, frag, s0, lut
+  std::map<const MfmaH *, std::array<int32_t, 6>> mh_at;  // wsum, frag, s0, lut, frag2, wsum2
   std::map<const HvV *, std::array<int32_t, 3>> hvv_at;   // k0ks, frag, wsum
   std::map<const HvH *, std::array<int32_t, 3>> hvh_at;   // w128, frag, s0
   int32_t mono_wts_at = -1;
@@ -1348,6 +1348,7 @@ static void resolve_workspace(Exec &E, BatchPlan &Bp, uint8_t *wb) {
 struct VrWork {
   int32_t img, first_strip, nstrips;
   const VrV *V;
+  int32_t hwsum2, hsh;  // the horizontal two-limb tables (fi_plan.h MfmaH::wsum2 / shift2)
 };
 // k_rs_vr workgroups: tiles (image, strip, band of blocks) in the XCD-aware
 // order of k_rs_vm, dealt round-robin to one persistent workgroup per CU; the
@@ -1397,6 +1398,9 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     m.w128 = vp->second[2];
     m.frag = vp->second[3];
     m.nblk = V.nblk;
+    m.vsh = V.shift;
+    m.hsh = work[k].hsh;
+    m.hwsum = work[k].hwsum2;
     desc_of[k] = (int32_t)Bp.vdescs.size();
     Bp.vdescs.push_back(m);
   }
@@ -1547,11 +1551,12 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     E.ai.insert(E.ai.end(), v.begin(), v.end());
     return o;
   };
-  std::map<const MfmaH *, std::pair<int32_t, int32_t>> hplaced;  // first strip, hwsum
+  std::map<const MfmaH *, std::array<int32_t, 3>> hplaced;  // first strip, hwsum, hwsum2
   struct Work1 {
     int32_t img, first_strip, nstrips;
     const VmV *V;
     const AxisTable *vt;
+    int32_t hwsum2, hsh;
   };
   std::vector<Work1> work;
   const int nv = (int)Bp.vm_img.size();
@@ -1587,16 +1592,20 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
       const int32_t first = (int32_t)Bp.vstrips.size();
       auto ht = c->mh_at.find(&H);
       if (ht == c->mh_at.end()) {
-        std::array<int32_t, 4> o;
+        std::array<int32_t, 6> o;
         o[0] = put(H.wsum);
         align4();
         o[1] = put(H.frag);
         o[2] = put(H.s0);
         align4();  // 16-byte aligned LUT rows (k_rs_vr's LDS-DMA)
         o[3] = put(H.lut);
+        align4();
+        o[4] = put(H.frag2);
+        o[5] = put(H.wsum2);
         ht = c->mh_at.emplace(&H, o).first;
       }
       const int32_t hw = ht->second[0], frag = ht->second[1], s0 = ht->second[2], lut = ht->second[3];
+      const int32_t frag2 = ht->second[4], hw2 = ht->second[5];
       for (const MfmaStrip &st : H.strips) {
         MStrip m{};
         m.x0 = st.x0;
@@ -1614,9 +1623,10 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
         m.s0 = s0 + (int32_t)st.s0;
         m.lut = lut + (int32_t)st.lut;
         m.vpitch = st.vpitch;
+        m.frag2 = frag2 + (int32_t)st.frag2;
         Bp.vstrips.push_back(m);
       }
-      hp = hplaced.emplace(&H, std::make_pair(first, hw)).first;
+      hp = hplaced.emplace(&H, std::array<int32_t, 3>{first, hw, hw2}).first;
     }
     for (const MfmaStrip &st : H.strips)  // the workgroup's LDS layout follows its strip and tile kind
       Bp.vm_lds = std::max(Bp.vm_lds, vm_lds_bytes(st.vpitch, st.nocb, st.ks, d.gray || d.rot != 0));
@@ -1640,9 +1650,10 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     m.w128 = vp->second[5];
     m.frag = vp->second[6];
     m.pmeta = vp->second[7];
-    m.hwsum = hp->second.second;
+    m.hwsum = hp->second[1];
     m.nblk = V.nblk;
-    work.push_back({(int32_t)Bp.vdescs.size(), hp->second.first, (int32_t)H.strips.size(), &V, Bp.vm_vt[q]});
+    work.push_back({(int32_t)Bp.vdescs.size(), hp->second[0], (int32_t)H.strips.size(), &V, Bp.vm_vt[q], hp->second[2],
+                    H.shift2});
     Bp.vdescs.push_back(m);
   }
   // k_rs_vr (default; FI_VR_RS=0 turns it off): the images whose vertical axis has block-major
@@ -1662,8 +1673,8 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
       const int64_t gap = V.maxgap;  // the DMA's per-lane row offset
       bool narrow = true;  // five H waves take two horizontal items each: <= 3 16-px blocks per strip
       for (int st = 0; st < w.nstrips; st++) narrow = narrow && Bp.vstrips[w.first_strip + st].nocb <= 3;
-      if (V.nblk > 0 && narrow && gap * Bp.vdescs[w.img].src_stride < ((int64_t)1 << 31))
-        vr.push_back({w.img, w.first_strip, w.nstrips, &V});
+      if (V.nblk > 0 && w.hsh > 0 && narrow && gap * Bp.vdescs[w.img].src_stride < ((int64_t)1 << 31))
+        vr.push_back({w.img, w.first_strip, w.nstrips, &V, w.hwsum2, w.hsh});
       else
         rest.push_back(w);
     }

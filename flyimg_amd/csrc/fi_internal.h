@@ -149,6 +149,7 @@ struct MStrip {               // one column strip (fi_plan.h MfmaStrip) placed i
   int32_t lut_px0, lut_n;
   int32_t frag, s0, lut;      // arena offsets (int32 units; frag 16-B aligned)
   int32_t vpitch;             // k_rs_vm: Q16 plane columns (multiple of 16)
+  int32_t frag2;              // k_rs_vr: arena offset of the two-limb fragments (fi_plan.h MfmaH::frag2)
 };
 // k_sc_hmfma (fi_smartcrop.hip): Pillow's horizontal pass as exact integer
 // MFMA.  Per 16-column output block b: source window [s0(b), s0(b) + 64 KS),
@@ -170,6 +171,7 @@ struct VDesc {                // one image
   int32_t w128;                      // ai offset (16-B aligned): 128 * sum of quantized weights per output row
   int32_t hwsum;                     // ai offset of the horizontal per-px weight sums
   int32_t nblk;
+  int32_t vsh, hsh;                  // k_rs_vr: weight shifts of the two-limb tables (fi_plan.h VrV)
 };
 struct VTile {                // one workgroup: image x strip x pieces [p0, p1); blocks < emit0 are halo only
   int32_t img, strip, p0, p1, emit0, pad;

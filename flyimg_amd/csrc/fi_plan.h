@@ -68,12 +68,17 @@ struct MfmaStrip {                     // one column strip of the horizontal pas
   int32_t nocb, ks;                    // 16-px output blocks, k-steps of 64 columns
   int32_t lut_px0, lut_n;              // px -> compact column LUT over [lut_px0, lut_px0 + lut_n)
   size_t frag, s0, lut;                // offsets into MfmaH::frag / s0 / lut
+  size_t frag2;                        // offset into MfmaH::frag2 (two-limb fragments of k_rs_vr)
 };
 struct MfmaH {
   std::vector<int32_t> cols;           // touched source columns, ascending
   std::vector<MfmaStrip> strips;
   std::vector<int32_t> frag, s0, lut;  // B fragments [strip][nocb][ks][3]; (w0, ks) per block; LUTs
   std::vector<int32_t> wsum;           // [ew] sum of quantized weights per output px
+  // k_rs_vr's horizontal pass: W = rint(w * 2^shift2) in TWO signed-byte limbs
+  // (vr_quant), fragments [strip][nocb][ks][2]; shift2 = 0: no two-limb form
+  int32_t shift2 = 0;
+  std::vector<int32_t> frag2, wsum2;
 };
 bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx = kMfmaMaxNx);
 
@@ -130,22 +135,38 @@ struct HvV {
 bool build_hv_v(const AxisTable &v, HvV *m);
 
 // Block-major vertical tables of k_rs_vr (fi_vr.hip): the vertical-first pass
-// of k_rs_vm with each 16-row output block computed in one go from a ring of
-// touched source rows.  Per block b: window start K0(b) (touched-row list
-// index, a multiple of 16, nondecreasing), ks(b) <= 2 k-steps of 64 list rows,
-// Rend(b) = one past its last non-zero tap, A fragments [b][t][limb] (zero past
-// ks and past the taps) and 128 * the quantized weight sum of every output row
-// (pixels enter the MFMA as p - 128).  Same weights, limbs and float
-// conversions as k_rs_vm, so the two kernels are bit-identical.
+// with each 16-row output block computed in one go from a ring of touched
+// source rows.  Per block b: window start K0(b) (touched-row list index, a
+// multiple of 16, nondecreasing), ks(b) <= 2 k-steps of 64 list rows, Rend(b) =
+// one past its last non-zero tap, A fragments [b][t][limb] (zero past ks and
+// past the taps) and 128 * the quantized weight sum of every output row (pixels
+// enter the MFMA as p - 128).
+//
+// Two weight limbs, not k_rs_vm's three: W = rint(w * 2^shift) with the largest
+// shift <= kVrMaxShift whose W all fit two signed bytes (vr_quant; the shift
+// follows the largest weight, so the precision relative to it is ~15 bits at
+// any factor), each output's W adjusted to keep its sum (quant_axis), so a
+// block costs 4 MFMAs per column tile instead of 6.  shift >= kVrMinShift,
+// else no k_rs_vr.  Outputs stay within +-1 LSB of the f64 resample and
+// >= 99.9 % identical to it in the model of tools/limbs_eval.py;
+// tests/test_gpu_vr.py checks every k_rs_vr class against k_rs_vm's 22-bit
+// path and the oracle.
+constexpr int kVrMaxShift = 22;
+constexpr int kVrMinShift = 15;
 struct VrV {
   std::vector<int32_t> rows;           // touched source rows, ascending
   int32_t row0 = 0, rstep = 0;         // rstep > 0: rows[k] == row0 + rstep * k
   int nblk = 0;
+  int32_t shift = 0;                   // W = rint(w * 2^shift)
   std::vector<int32_t> bmeta;          // [nblk][4] {K0, ks, Rend, 0}
-  std::vector<int32_t> frag;           // [nblk][2][3][256]
+  std::vector<int32_t> frag;           // [nblk][2][2][256]
   std::vector<int32_t> w128;           // [16 nblk]
   int32_t maxgap = 0;                  // widest gap between consecutive touched rows
 };
+// the largest shift in [kVrMinShift, kVrMaxShift] at which every sum-kept
+// quantised weight of the axis fits two signed-byte limbs (hi * 256 + lo, both
+// in [-128, 127]), the weights in *wq (AxisTable::w order); 0 if none
+int vr_quant(const AxisTable &t, std::vector<int32_t> *wq);
 bool build_vr_v(const AxisTable &v, VrV *m);
 
 // Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)

@@ -56,7 +56,7 @@ constexpr int kHW = 5;                   // H waves 8-12: horizontal items hw, h
 constexpr int kSW = 1;                   // S wave 13: the stores of the output tile of phase p - 2
 constexpr int kLW = 2;                   // L waves 14-15
 static_assert(kVW + kHW + kSW + kLW == 16, "16 waves");
-constexpr int kABytes = 6144;            // [t][limb][64 lanes][16 B]
+constexpr int kABytes = 4096;            // [t][limb][64 lanes][16 B]: two limbs, <= 2 k-steps
 constexpr int kRecBytes = 96;
 constexpr int kLutSlots = 4;
 constexpr int kPlanePad = 176;           // 44 (mod 64) dwords: see fi_vm.hip kVmPlanePad
@@ -66,6 +66,7 @@ constexpr int kOt8Pitch = 200;           // 8-bit output tile row (<= 64 px x 3 
 constexpr int kFirst = 1;                // first block of a tile
 constexpr int kSlot = 2;                 // output-tile slot of the block (phase parity)
 constexpr int kTslotShift = 4;           // bits 4-5: LUT slot (tile sequence number mod 4)
+constexpr int kVshShift = 8;             // bits 8-12: the vertical weight shift (fi_plan.h VrV::shift)
 
 __device__ __forceinline__ i32x2 tr8(const uint8_t *p) { return __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2 *)(p)); }
 __device__ __forceinline__ i32x4 mfma(i32x4 a, i32x4 b, i32x4 c) {
@@ -81,11 +82,9 @@ __device__ __forceinline__ uint32_t gray_q16(uint32_t r, uint32_t g, uint32_t b)
   const double gv = 0.212656 * (double)r + 0.715158 * (double)g + 0.072186 * (double)b;
   return !(gv > 0.0) ? 0u : (gv >= 65535.0 ? 65535u : (uint32_t)(gv + 0.5));
 }
-__device__ __forceinline__ int32_t fold3(int32_t d0, int32_t d1, int32_t d2) {
-  return (int32_t)((uint32_t)d0 + ((uint32_t)d1 << 8) + ((uint32_t)d2 << 16));
-}
+__device__ __forceinline__ int32_t fold2(int32_t d0, int32_t d1) { return (int32_t)((uint32_t)d0 + ((uint32_t)d1 << 8)); }
 __device__ __forceinline__ uint32_t lds_addr(const uint8_t *p) { return (uint32_t)(uintptr_t)(const l_u8 *)p; }
-// read-only tables through the constant address space (scalar loads; see fi_vp.hip)
+// read-only tables through the constant address space (scalar loads)
 template <class T>
 __device__ __forceinline__ T ldc(const T *p) {
   static_assert(sizeof(T) % 4 == 0, "dword records");
@@ -197,7 +196,7 @@ __device__ __forceinline__ void wait_vm_le(int n) {
   }
 }
 
-struct Rec {  // 32 B in LDS
+struct Rec {  // 96 B in LDS (kRecBytes)
   int32_t t, blk, flags, slot0, ks, grend, frag, w128;  // frag / w128: int32 offsets into ai
   int32_t corr[16];  // 128 * weight sums of the block's 16 output rows (the MFMA bias)
 };
@@ -220,7 +219,7 @@ __device__ __forceinline__ Lds lds_of(const VrLayout &L) {
 }
 }  // namespace
 
-// per-wave phase sums of MODE 9 (fi_debug_vr_stamps, tools/vp_timing.py VR=1)
+// per-wave phase sums of MODE 9 (fi_debug_vr_stamps, tools/vr_timing.py VR=1)
 constexpr int kVrStampSlots = 256;
 constexpr int kVrStampN = 16 * 6;
 __device__ uint64_t g_vr_stamps[kVrStampSlots * kVrStampN];
@@ -279,7 +278,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     struct PI {
       int t, blk, gk0, grend, ks, frag, w128, flags;
     };
-    int ct = t0, ck = 0, cb = 0, c_bmeta = 0, c_frag = 0, c_w128 = 0, c_lut = 0, c_lut_n = 0;
+    int ct = t0, ck = 0, cb = 0, c_bmeta = 0, c_frag = 0, c_w128 = 0, c_lut = 0, c_lut_n = 0, c_vsh = 0;
     VrTile CT{};
     auto ptile_load = [&]() {
       CT = ldc(tiles + ct);
@@ -288,6 +287,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       c_bmeta = D.pmeta;
       c_frag = D.frag;
       c_w128 = D.w128;
+      c_vsh = D.vsh;
       c_lut = S.lut;
       c_lut_n = S.lut_n;
       cb = CT.b0;
@@ -303,9 +303,10 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       r.gk0 = CT.g0 + (m.x - CT.kbase);
       r.grend = CT.g0 + (m.z - CT.kbase);
       r.ks = m.y;
-      r.frag = c_frag + cb * 6 * 256;
+      r.frag = c_frag + cb * 4 * 256;
       r.w128 = c_w128 + 16 * cb;
-      r.flags = (cb == CT.b0 ? kFirst : 0) | ((s & 1) ? kSlot : 0) | ((ck & (kLutSlots - 1)) << kTslotShift);
+      r.flags = (cb == CT.b0 ? kFirst : 0) | ((s & 1) ? kSlot : 0) | ((ck & (kLutSlots - 1)) << kTslotShift) |
+                (c_vsh << kVshShift);
       if (li == 0) {
         // the bias row rides in the record (scalar loads two phases ahead) instead
         // of a 64-byte DMA in the loader's stream
@@ -328,10 +329,10 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       }
       return r;
     };
-    // A fragments (ks k-steps x 3 limbs x 1 KB) into A slot `slot`
+    // A fragments (ks k-steps x 2 limbs x 1 KB) into A slot `slot`
     auto issue_a = [&](const PI &r, int slot) {
       const uint32_t m0 = lds_addr(lds) + (uint32_t)(O.a + slot * kABytes);
-      const int nf = 3 * r.ks;
+      const int nf = 2 * r.ks;
       for (int i = li; i < nf; i += kLW)
         dma16(m0 + 1024 * i, reinterpret_cast<const uint8_t *>(ai + r.frag) + 1024 * i, 16u * lane);
     };
@@ -560,10 +561,10 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         const i32x4 *al = reinterpret_cast<const i32x4 *>(lds + O.a + (p & 1) * kABytes);
         // 128 * weight sums of this lane's 4 output rows, from block p's record
         const i32x4 corr = *reinterpret_cast<const i32x4 *>(&recs[p & 7].corr[4 * (lane >> 4)]);
-        i32x4 acc[3][kT];
+        i32x4 acc[2][kT];
         const uint32_t RB = (uint32_t)R * 512u;
         // both k-steps' ring and A reads in flight before the first MFMA
-        i32x4 Bt[2][kT], At[2][3];
+        i32x4 Bt[2][kT], At[2][2];
 #pragma unroll
         for (int t = 0; t < 2; t++) {
           if (t >= C.ks) break;
@@ -579,21 +580,17 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
             Bt[t][j] = i32x4{lo.x, lo.y, hi.x, hi.y} ^ i32x4{(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
           }
 #pragma unroll
-          for (int q = 0; q < 3; q++) At[t][q] = al[(t * 3 + q) * 64 + lane];
+          for (int q = 0; q < 2; q++) At[t][q] = al[(t * 2 + q) * 64 + lane];
         }
 #pragma unroll
         for (int j = 0; j < kT; j++) acc[0][j] = mfma(At[0][0], Bt[0][j], corr);
 #pragma unroll
         for (int j = 0; j < kT; j++) acc[1][j] = mfma(At[0][1], Bt[0][j], i32x4{0, 0, 0, 0});
-#pragma unroll
-        for (int j = 0; j < kT; j++) acc[2][j] = mfma(At[0][2], Bt[0][j], i32x4{0, 0, 0, 0});
         if (C.ks > 1) {
 #pragma unroll
           for (int j = 0; j < kT; j++) acc[0][j] = mfma(At[1][0], Bt[1][j], acc[0][j]);
 #pragma unroll
           for (int j = 0; j < kT; j++) acc[1][j] = mfma(At[1][1], Bt[1][j], acc[1][j]);
-#pragma unroll
-          for (int j = 0; j < kT; j++) acc[2][j] = mfma(At[1][2], Bt[1][j], acc[2][j]);
         }
         stamp(1);
         // the H waves' reads of block p - 1's planes are done (single plane buffer)
@@ -601,15 +598,16 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           const uint32_t want = (uint32_t)kHW * (uint32_t)(p + 1);
           while (hcnt[0] < want) __builtin_amdgcn_s_sleep(1);
         }
-        // block done: ClampToQuantum(257 acc / 2^22) -> Q16 hi / lo signed-byte planes
+        // block done: ClampToQuantum(257 acc / 2^shift) -> Q16 hi / lo signed-byte planes
+        const float vscale = __builtin_amdgcn_ldexpf(257.0f, -((C.flags >> kVshShift) & 31));
 #pragma unroll
         for (int j = 0; j < kT; j++) {
           const uint32_t o = (vcolp[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
           uint32_t q[4];
 #pragma unroll
           for (int i = 0; i < 4; i++) {
-            const int32_t tot = fold3(acc[0][j][i], acc[1][j][i], acc[2][j][i]);
-            q[i] = __float2uint_rz(fmaf((float)tot, 257.0f / 4194304.0f, 0.5f));
+            const int32_t tot = fold2(acc[0][j][i], acc[1][j][i]);
+            q[i] = __float2uint_rz(fmaf((float)tot, vscale, 0.5f));
           }
           const auto p01 = __builtin_amdgcn_cvt_pk_u16(q[0], q[1]);
           const auto p23 = __builtin_amdgcn_cvt_pk_u16(q[2], q[3]);
@@ -770,9 +768,9 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
   int ftile = -1, h_nx = 0, h_items = 0;
   bool h_fast8 = false;
   uint32_t h_sh0 = 0, h_shs = 0;
-  i32x4 hb[2][2][3];
+  i32x4 hb[2][2][2];
   int hw0k[2] = {0, 0}, hksk[2] = {0, 0};
-  float hwsk[2] = {0.f, 0.f};
+  float hwsk[2] = {0.f, 0.f}, hscale = 0.f;
   __builtin_amdgcn_s_setprio(1);
   phase_barrier();
   phase_barrier();
@@ -794,8 +792,9 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         h_fast8 = !D.gray && D.rot == 0;
         h_sh0 = (uint32_t)(((uintptr_t)D.dst + (uint64_t)S.x0 * 3) & 3u);
         h_shs = (uint32_t)(D.dst_stride & 3);
+        hscale = __builtin_amdgcn_ldexpf(1.0f, -D.hsh);
         const int nx = h_nx;
-        const g_i32x4 *hf = (const g_i32x4 *)(ai + S.frag);
+        const g_i32x4 *hf = (const g_i32x4 *)(ai + S.frag2);
 #pragma unroll
         for (int k = 0; k < 2; k++) {
           const int it = hw + kHW * k, ob = it / 3;
@@ -807,8 +806,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
 #pragma unroll
           for (int t = 0; t < 2; t++)
 #pragma unroll
-            for (int q = 0; q < 3; q++)
-              hb[k][t][q] = (ok && t < S.ks) ? hf[((ob * S.ks + t) * 3 + q) * 64 + lane] : i32x4{0, 0, 0, 0};
+            for (int q = 0; q < 2; q++)
+              hb[k][t][q] = (ok && t < S.ks) ? hf[((ob * S.ks + t) * 2 + q) * 64 + lane] : i32x4{0, 0, 0, 0};
         }
       }
       stamp(1);
@@ -846,14 +845,14 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         const int it = hw + kHW * k;
         const int ob = it / 3, chn = it - 3 * ob;
         const int hks = hksk[k];
-        i32x4 hh[3], hl[3];
+        i32x4 hh[2], hl[2];
 #pragma unroll
-        for (int q = 0; q < 3; q++) hh[q] = hl[q] = i32x4{0, 0, 0, 0};
+        for (int q = 0; q < 2; q++) hh[q] = hl[q] = i32x4{0, 0, 0, 0};
 #pragma unroll
         for (int t = 0; t < 2; t++) {
           if (t >= hks) break;
 #pragma unroll
-          for (int q = 0; q < 3; q++) {
+          for (int q = 0; q < 2; q++) {
             hh[q] = mfma(Ahk[k][t], hb[k][t][q], hh[q]);
             hl[q] = mfma(Alk[k][t], hb[k][t][q], hl[q]);
           }
@@ -863,9 +862,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           const float hws = hwsk[k];
 #pragma unroll
           for (int i = 0; i < 4; i++) {
-            const float tot = 256.0f * (float)fold3(hh[0][i], hh[1][i], hh[2][i]) +
-                              (float)fold3(hl[0][i], hl[1][i], hl[2][i]) + hws;
-            const uint32_t q = min(__float2uint_rz(fmaf(tot, 1.0f / 4194304.0f, 0.5f)), 65535u);
+            const float tot = 256.0f * (float)fold2(hh[0][i], hh[1][i]) + (float)fold2(hl[0][i], hl[1][i]) + hws;
+            const uint32_t q = min(__float2uint_rz(fmaf(tot, hscale, 0.5f)), 65535u);
             const int yl = 4 * (lane >> 4) + i;
             if (fast8) {
               const int sh = (int)((sh0 + (uint32_t)(16 * b + yl) * shs) & 3u);

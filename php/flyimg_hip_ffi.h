@@ -18,6 +18,25 @@ typedef struct fi_image {
   double sharpen[2];
   double blur[2];
 } fi_image;
+typedef struct fi_smartcrop_params {
+  double detail_weight;
+  double edge_radius;
+  double edge_weight;
+  double outside_importance;
+  int32_t rule_of_thirds;
+  double saturation_bias;
+  double saturation_brightness_max;
+  double saturation_brightness_min;
+  double saturation_threshold;
+  double saturation_weight;
+  int32_t score_down_sample;
+  double skin_bias;
+  double skin_brightness_max;
+  double skin_brightness_min;
+  double skin_color[3];
+  double skin_threshold;
+  double skin_weight;
+} fi_smartcrop_params;
 typedef struct fi_ctx fi_ctx;
 int32_t fi_abi_version(void);
 const char *fi_last_error(void);
@@ -27,3 +46,7 @@ int fi_plan(fi_image *imgs, int32_t n);
 int fi_pixelate_regions(fi_ctx *ctx, uint8_t *img, int32_t w, int32_t h, int32_t stride, int32_t channels,
                         const int32_t *boxes, int32_t nboxes);
 int fi_process_batch(fi_ctx *ctx, fi_image *imgs, int32_t n);
+void fi_smartcrop_default_params(fi_smartcrop_params *p);
+int fi_smartcrop(fi_ctx *ctx, const uint8_t *rgb, int32_t w, int32_t h, int32_t stride,
+                 int32_t target_w, int32_t target_h, const fi_smartcrop_params *params,
+                 int32_t out_xywh[4], double *out_score);

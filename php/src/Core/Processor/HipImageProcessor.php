@@ -7,9 +7,18 @@ use Core\Exception\ExecFailedException;
 
 /**
  * Drop-in for ImageProcessor (src/Core/Processor/ImageProcessor.php) that runs
- * the resample step -- and smc_1, when set -- on an MI355X through
- * libflyimg_hip.so over PHP FFI instead of exec'ing `convert`
- * (ImageProcessor.php:49-57, Processor.php:44-62).
+ * the resample step on an MI355X through libflyimg_hip.so over PHP FFI instead
+ * of exec'ing `convert` (ImageProcessor.php:49-57, Processor.php:44-62).
+ *
+ * smc_1 keeps the reference's order by default: this processor resamples and
+ * MozJPEG-encodes the output file, then ImageHandler::smartCropProcess
+ * (ImageHandler.php:125-133) runs HipSmartCropProcessor, which takes the box
+ * on the decoded output FILE -- the bytes smartcrop.py reads
+ * (SmartCropProcessor.php:24) -- on the GPU and crops with `convert -crop` as
+ * the reference does.  FLYIMG_HIP_FUSED_SMARTCROP=1 opts into the fused form
+ * (FI_OP_SMARTCROP_APPLY: box and crop on the raw resized pixels in the same
+ * call, one encode); its box differs from the reference's on ~11 % of images
+ * (INTEGRATION.md).
  *
  * Geometry and option semantics are the parent's: the same OptionsBag keys,
  * the same calculateSize() decision (:115-130) and updateTargetDimensions()
@@ -48,6 +57,36 @@ class HipImageProcessor extends ImageProcessor
     /** @var \FFI|null one library handle and one fi_ctx per PHP-FPM worker */
     private static $ffi = null;
     private static $ctx = null;
+    /** @var array<string, bool> output paths the fused smc_1 already cropped */
+    private static $fusedCropped = [];
+
+    /** The FFI handle and the worker's fi_ctx (shared with HipSmartCropProcessor). */
+    public static function ffi(): \FFI
+    {
+        return self::lib();
+    }
+
+    public static function context()
+    {
+        self::lib();
+        return self::$ctx;
+    }
+
+    /** FLYIMG_HIP_FUSED_SMARTCROP=1: box and crop inside fi_process_batch (opt-in). */
+    public static function fusedSmartCrop(): bool
+    {
+        return getenv('FLYIMG_HIP_FUSED_SMARTCROP') === '1';
+    }
+
+    /** True once, for an output the fused smc_1 already cropped. */
+    public static function takeFusedCrop(string $outputPath): bool
+    {
+        if (isset(self::$fusedCropped[$outputPath])) {
+            unset(self::$fusedCropped[$outputPath]);
+            return true;
+        }
+        return false;
+    }
 
     private static function lib(): \FFI
     {
@@ -78,7 +117,7 @@ class HipImageProcessor extends ImageProcessor
         if (!$this->gpuEligible($outputImage, $path)) {
             return parent::processNewImage($outputImage);
         }
-        $decoded = $this->decodeRgb($path);
+        $decoded = self::decodeRgb($path);
         if ($decoded === null) {  // not a 3-component JPEG after all
             return parent::processNewImage($outputImage);
         }
@@ -103,6 +142,9 @@ class HipImageProcessor extends ImageProcessor
         self::check($img->status);
         $this->encode($outputImage, \FFI::string($dst, $img->out_h * $img->out_stride),
             $img->out_w, $img->out_h, $img->out_channels);
+        if ($img->flags & self::FI_OP_SMARTCROP_APPLY) {
+            self::$fusedCropped[$outputImage->getOutputImagePath()] = true;
+        }
         \FFI::free($src);
         \FFI::free($dst);
         return $outputImage;
@@ -213,7 +255,9 @@ class HipImageProcessor extends ImageProcessor
         if ($rotate % 360 !== 0) {
             $flags |= self::FI_OP_ROTATE;
         }
-        if (!empty($outputImage->extractKey('smart-crop'))) {                   // ImageHandler.php:125-133
+        if (!empty($outputImage->extractKey('smart-crop')) && self::fusedSmartCrop()) {
+            // opt-in fused smc_1 (ImageHandler.php:125-133 in the same call); by
+            // default HipSmartCropProcessor runs on the encoded file afterwards
             $flags |= self::FI_OP_SMARTCROP | self::FI_OP_SMARTCROP_APPLY;
         }
         // forwarded -unsharp / -sharpen / -blur (:303-315), after -rotate in this order;
@@ -245,7 +289,7 @@ class HipImageProcessor extends ImageProcessor
 
     /** Host decode to packed RGB8 (libjpeg-turbo's djpeg, PPM output); null for a
      *  gray JPEG (PGM: IM reads it as a PseudoClass image -- the parent handles it). */
-    private function decodeRgb(string $path): ?array
+    public static function decodeRgb(string $path): ?array
     {
         $ppm = shell_exec('/opt/mozjpeg/bin/djpeg -pnm ' . escapeshellarg($path));
         if (is_string($ppm) && strncmp($ppm, 'P5', 2) === 0) {

@@ -104,15 +104,15 @@ def test_monochrome_plans_one_channel():
     assert plan(400, 300, ImageProcessor(OptionsBag("w_100,h_50,c_1,r_90,mnchr_1"), 400, 300).to_op()) == (50, 100, 1)
 
 
-def _norm_decls(text):
-    """Function prototypes and fi_image fields of a C header, whitespace-normalised."""
+def _norm_decls(text, struct="fi_image"):
+    """Function prototypes and the fields of one struct of a C header, whitespace-normalised."""
     import re
 
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     protos = {}
     for m in re.finditer(r"([A-Za-z_][A-Za-z0-9_ \*]*?\b(fi_[a-z0-9_]+)\s*\([^;{]*\))\s*;", text):
         protos[m.group(2)] = re.sub(r"\s+", " ", m.group(1)).replace("( ", "(").strip()
-    body = re.search(r"typedef struct fi_image \{(.*?)\} fi_image;", text, flags=re.S).group(1)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (struct, struct), text, flags=re.S).group(1)
     fields = []
     for decl in body.split(";"):
         decl = re.sub(r"\s+", " ", decl).strip()
@@ -141,6 +141,9 @@ def test_php_ffi_cdef_matches_header():
     for name, proto in pp.items():
         assert proto == hp[name], (proto, hp[name])
     assert pf == hf
+    with open(os.path.join(root, "include", "flyimg_hip.h")) as f:
+        h2 = _norm_decls(f.read(), "fi_smartcrop_params")[1]
+    assert _norm_decls(text, "fi_smartcrop_params")[1] == h2  # HipSmartCropProcessor passes it by pointer
 
 
 def test_codec_decode_ex_flags_pseudoclass_modes():

@@ -82,9 +82,9 @@ def test_full_cfg2_batch_past_4gb(pool_ctx, opts):
         ctx.free(dst)
 
 
-def test_full_cfg2_batch_vp_equals_vm(pool_ctx):
-    """k_rs_vp and k_rs_vm share tables and integer algebra: the whole 1024-image
-    resized batch is bitwise identical."""
+def test_full_cfg2_batch_vr_within_one_lsb_of_vm(pool_ctx):
+    """k_rs_vr (two-limb weights) and k_rs_vm (three limbs, 22 bits) on the
+    whole 1024-image resized batch: every byte within 1 LSB, >= 99 % identical."""
     ctx, pool, stride, img = pool_ctx
     op = ImageProcessor(OptionsBag("w_500"), W, H).to_op()
     rc, arr, dst, cap = _run(ctx, pool, stride, img, op)
@@ -96,7 +96,8 @@ def test_full_cfg2_batch_vp_equals_vm(pool_ctx):
             assert rc2 == 0 and vm.stats("path_vr")[1] == 0
             a = ctx.d2h(dst, cap * N)
             b = vm.d2h(dst2, cap * N)
-            assert np.array_equal(a, b), int((a != b).sum())
+            d = np.abs(a.astype(np.int16) - b.astype(np.int16))
+            assert d.max() <= 1 and (d == 0).mean() >= 0.99, (int(d.max()), float((d == 0).mean()))
         finally:
             vm.free(dst2)
     finally:

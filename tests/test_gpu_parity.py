@@ -1013,6 +1013,21 @@ def test_face_blur_pixelate_bit_exact(ctx, case):
     _ = rng
 
 
+def test_face_fb_fixture_blocks(ctx):
+    """fi_pixelate_regions on the reference's faces.jpg (Pillow decode) with the
+    detector boxes recovered from face_fb.png: every block within 1 LSB of the
+    reference's output (FaceDetectProcessorTest.php:31-41) and equal to the
+    oracle, outside the footprints untouched."""
+    from flyimg_amd.processor import FaceDetectProcessor
+    from tests.test_face_fb_cpu import DETECTOR, faces_rgb, fixture_block_diff
+
+    src = faces_rgb()
+    got = np.ascontiguousarray(src.copy())
+    FaceDetectProcessor.blur_faces(ctx, got, ["%d %d %d %d" % d for d in DETECTOR])
+    assert fixture_block_diff(got) <= 1
+    assert np.array_equal(got, orc.im_pixelate_regions(src, DETECTOR))
+
+
 def test_face_blur_rejects_empty_scale(ctx):
     from flyimg_amd.processor import ExecFailedException, FaceDetectProcessor
 

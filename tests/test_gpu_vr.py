@@ -1,0 +1,107 @@
+"""k_rs_vr (the persistent block-major resample, fi_vr.hip) on every geometry
+class it takes: the path actually ran (its image counter rose by the batch),
+the output is within +-1 LSB of k_rs_vm's 22-bit three-limb path and >= 99 %
+identical to it, and within +-1 LSB / >= 98 % exact of the oracle
+(ImageProcessor.php:86 -thumbnail / -resize, IM's VerticalFilter then
+HorizontalFilter).  k_rs_vr quantises the weights to two
+signed-byte limbs (fi_plan.h VrV), k_rs_vm to three, so the two are not
+bit-identical; the tolerance here is the north_star's."""
+import numpy as np
+import pytest
+
+from flyimg_amd import _lib as L
+from flyimg_amd.processor import ImageProcessor, OptionsBag
+from flyimg_amd.synth import synth_rgb
+from oracle import oracle as orc
+from tests.test_gpu_parity import _context_with, _oracle_flags
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (W, H, options, images)
+    (1920, 1080, "w_500", 3),
+    (1920, 1080, "w_500", 40),
+    (3840, 2160, "w_512,h_512,c_1", 2),
+    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", 2),
+    (1024, 768, "w_200,h_200,c_1,r_180", 2),
+    (1200, 900, "w_300,r_270", 2),
+    (800, 600, "w_250,clsp_Gray", 2),
+    (333, 517, "w_97", 4),
+    (4000, 3000, "w_150", 2),  # sampled rows 5.33 apart: uneven, k_rs_vm (as cfg1)
+    (3840, 2160, "w_512,h_512,c_1", 300),
+    (1920, 1080, "w_500", 300),
+    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", 24),
+    (640, 480, "w_320", 7),  # 1/2: 85 output px per 512-B strip, more than k_rs_vr's 3 16-px blocks
+]
+
+
+# k_rs_vm's classes: ThumbnailImage sampled rows at uneven gaps (k_rs_vr takes
+# evenly spaced rows only) and strips wider than three 16-px output blocks
+NOT_VR = {(4000, 3000, "w_150"), (640, 480, "w_320")}
+
+
+@pytest.fixture(scope="module")
+def pair():
+    vr = _context_with({"FI_VR_RS": "1", "FI_FORCE_GENERIC": "0"})
+    vm = _context_with({"FI_VR_RS": "0", "FI_FORCE_GENERIC": "0"})
+    yield vr, vm
+    vr.close()
+    vm.close()
+
+
+def _close(a, b, name, min_same):
+    assert a is not None and b is not None and a.shape == b.shape, name
+    d = np.abs(a.astype(np.int16) - b.astype(np.int16))
+    same = float((d == 0).mean())
+    assert d.max() <= 1, f"{name}: max |diff| {d.max()}"
+    assert same >= min_same, f"{name}: identical fraction {same:.5f}"
+    return same
+
+
+def _oracle(src, op):
+    return orc.im_convert(src, op.target_w, op.target_h, _oracle_flags(op.flags), gravity=op.gravity, rotate=op.rotate)
+
+
+@pytest.mark.parametrize("W,H,opts,n", CASES, ids=[f"{c[0]}x{c[1]}-{c[2]}-x{c[3]}" for c in CASES])
+def test_vr_takes_the_class_and_matches(pair, W, H, opts, n):
+    vr, vm = pair
+    op = ImageProcessor(OptionsBag(opts), W, H).to_op()
+    base = [synth_rgb(W, H, 77 + k) for k in range(min(n, 4))]
+    srcs = [base[k % len(base)] for k in range(n)]
+    path = "path_vr" if (W, H, opts) not in NOT_VR else "path_vm"
+    before = vr.stats(path)[1]
+    ob, rb, rcb = vr.process(srcs, [op] * n)
+    assert rcb == 0 and all(r.status == 0 for r in rb), L.lib().fi_last_error()
+    assert vr.stats(path)[1] == before + n  # no silent fallback to another kernel
+    oa, ra, rca = vm.process(srcs[:len(base)], [op] * len(base))
+    assert rca == 0
+    for k in range(len(base)):
+        _close(ob[k], oa[k], f"{opts} image {k} vs k_rs_vm", 0.99)
+        for j in range(k, n, len(base)):  # repeated sources give identical outputs
+            assert np.array_equal(ob[j], ob[k])
+    if W * H <= 4_000_000:
+        _close(ob[0], _oracle(base[0], op), f"{opts} vs oracle", 0.98)
+
+
+def test_vr_mixed_batch(pair):
+    """one launch with several vertical tables: 8-bit and Q16 (gray / rotated)
+    output tiles, unequal tile costs (1080p, 4K, small images), checked image
+    by image against the oracle and against k_rs_vm"""
+    vr, vm = pair
+    geo = [(1920, 1080, "w_500"), (3840, 2160, "w_512,h_512,c_1"), (800, 600, "w_250,clsp_Gray"),
+           (1200, 900, "w_300,r_270"), (333, 517, "w_97"), (1024, 768, "w_200,h_200,c_1,r_180")]
+    srcs, ops = [], []
+    for k in range(12):
+        W, H, opts = geo[k % len(geo)]
+        srcs.append(synth_rgb(W, H, 300 + k))
+        ops.append(ImageProcessor(OptionsBag(opts), W, H).to_op())
+    before = vr.stats("path_vr")[1]
+    ob, rb, rcb = vr.process(srcs, ops)
+    assert rcb == 0 and all(r.status == 0 for r in rb)
+    assert vr.stats("path_vr")[1] == before + len(srcs)
+    oa, _, rca = vm.process(srcs, ops)
+    assert rca == 0
+    for k in range(len(srcs)):
+        _close(ob[k], oa[k], f"mixed {k} vs k_rs_vm", 0.99)
+        if srcs[k].shape[0] * srcs[k].shape[1] <= 4_000_000:
+            _close(ob[k], _oracle(srcs[k], ops[k]), f"mixed {k} vs oracle", 0.98)

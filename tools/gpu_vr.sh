@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/vr
 mkdir -p $OUT
-timeout -k 10 200 python -u tools/vp_check.py > $OUT/check.log 2>&1
+timeout -k 10 200 python -u tools/vr_check.py > $OUT/check.log 2>&1
 rc=$?
 cat $OUT/check.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
@@ -24,5 +24,5 @@ for v in ${VR_RUNS:-vr2 vm2 vr3 vm3}; do
   summ $OUT/$v.json $v
 done
 if [ -n "${VR_TIMING:-}" ]; then
-  timeout -k 10 200 python -u tools/vp_timing.py > $OUT/timing.log 2>&1; rc=$?; cat $OUT/timing.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 200 python -u tools/vr_timing.py > $OUT/timing.log 2>&1; rc=$?; cat $OUT/timing.log; [ $rc -eq 0 ] || exit $rc
 fi

@@ -10,6 +10,12 @@ same pixels after a JPEG round trip (Pillow, quality 90 -- flyimg's default
 `q_90` -- with 4:4:4 sampling, ImageMagick's choice at quality >= 90, and also
 4:2:0), and counts the images whose box changes.
 
+It also checks the PHP shim's DEFAULT smc_1 path (HipSmartCropProcessor,
+reference order): resize -> JPEG q90 4:2:0 (MozJPEG cjpeg's default sampling;
+libjpeg-turbo through Pillow stands in for MozJPEG here) -> decode that file
+-> fi_smartcrop; its box must equal the oracle's (pinned bit-exact to
+smartcrop.py) on the same decoded bytes for every image ("ref_order_q90_420").
+
   python tools/sc_jpeg_roundtrip.py [--synthetic N] [--out file.json]
 
 Sources: the reference's three photographs kept as fixtures under
@@ -29,6 +35,7 @@ sys.path.insert(0, ROOT)
 from flyimg_amd.processor import ImageProcessor, OptionsBag  # noqa: E402
 from flyimg_amd.runtime import Context  # noqa: E402
 from flyimg_amd.synth import synth_rgb  # noqa: E402
+from oracle import oracle as orc  # noqa: E402  (the checker)
 
 
 def top_box(ctx, rgb):
@@ -75,6 +82,9 @@ def main():
                 Image.fromarray(resized).save(buf, "JPEG", quality=90, subsampling=sub)
                 dec = np.asarray(Image.open(io.BytesIO(buf.getvalue())).convert("RGB"))
                 row[tag] = top_box(ctx, dec)
+                if tag == "q90_420":
+                    t = orc.sc_crop(dec, 100, 100)["top_crop"]
+                    row["ref_order_q90_420"] = (t["x"], t["y"], t["width"], t["height"])
             per.append(row)
     for tag in ("q90_444", "q90_420"):
         for group in ("fixture", "synthetic"):
@@ -85,6 +95,12 @@ def main():
                 "images": len(rows), "same_box": same, "different_box": len(rows) - same,
                 "mean_iou": round(float(np.mean(ious)), 4) if ious else None,
                 "min_iou": round(float(np.min(ious)), 4) if ious else None}
+    for group in ("fixture", "synthetic"):
+        rows = [r for r in per if r["source"].startswith(group)]
+        same = sum(1 for r in rows if tuple(r["q90_420"]) == tuple(r["ref_order_q90_420"]))
+        res["variants"][f"ref_order_q90_420/{group}"] = {
+            "images": len(rows), "gpu_box_equals_oracle_on_decoded_file": same,
+            "encoder": "libjpeg-turbo (Pillow) q90 4:2:0 standing in for MozJPEG cjpeg -quality 90"}
     res["fixtures"] = [r for r in per if r["source"].startswith("fixture")]
     print(json.dumps(res, indent=1))
     if args.out:

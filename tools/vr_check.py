@@ -3,7 +3,7 @@
 bit-identical to the streaming kernel (same weights, same integer algebra) on
 every geometry class; cases k_rs_vr does not take print vr_images 0.
 
-  python tools/vp_check.py            (GPU)
+  python tools/vr_check.py            (GPU)
 """
 import os
 import sys
