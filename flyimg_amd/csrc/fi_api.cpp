@@ -1382,6 +1382,7 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     if (vp == c->vr_at.end()) {
       std::array<int32_t, 4> o;
       o[0] = put(V.rows);
+      E.ai.insert(E.ai.end(), 32, 0);  // k_rs_vr reads the list 16 entries at a time, one group ahead
       align4();
       o[1] = put(V.bmeta);
       o[2] = put(V.w128);

@@ -712,10 +712,8 @@ bool build_vr_v(const AxisTable &v, VrV *m) {
   m->rstep = nl > 1 ? m->rows[1] - m->rows[0] : 1;
   for (int k = 1; k < nl && m->rstep > 0; k++)
     if (m->rows[k] != m->row0 + m->rstep * k) m->rstep = 0;
-  // unevenly spaced rows (ThumbnailImage sampling, e.g. cfg1's 2000 -> 1250):
-  // k_rs_vm's pieces stream them faster than a table-driven row stream did
-  // (cfg1 4.95 vs 5.31 ms), so k_rs_vr takes evenly spaced rows only
-  if (m->rstep <= 0) return false;
+  // unevenly spaced rows (ThumbnailImage sampling, e.g. cfg1's 2000 -> 1250)
+  // stream from the touched-row list (fi_vr.hip issue_rows)
   for (int k = 1; k < nl; k++) m->maxgap = std::max(m->maxgap, m->rows[k] - m->rows[k - 1]);
   return true;
 }

@@ -526,6 +526,54 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
       }
     }
   };
+  // the same staging software-pipelined: when a block is one item per thread of
+  // an aligned RGB source, block k + 1's loads are issued into registers before
+  // block k's horizontal pass (and before a chunk's vertical pass and maps), so
+  // their latency hides behind that work instead of heading every block
+  const bool pf = sC == 3 && a4 && nitem <= kFzThreads;
+  const int pf_rr = fz_div(tid, ng, rcp_ng), pf_g = tid - pf_rr * ng;
+  u32x4a pq[3];
+  auto stage_issue = [&](int r0) {
+    if (tid >= nitem) return;
+    const uint8_t *s = src + (int64_t)(r0 + pf_rr + yoff) * sstride + 48 * pf_g;
+    const int remb = r0 + pf_rr < hrows ? 3 * (sW - 16 * pf_g) : 0;
+    if (remb >= 48) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) pq[k] = *reinterpret_cast<const u32x4a *>(s + 16 * k);
+    } else {
+      uint32_t d[12];
+#pragma unroll
+      for (int k = 0; k < 12; k++) {
+        if (4 * k + 4 <= remb) {
+          d[k] = *reinterpret_cast<const uint32_t *>(s + 4 * k);
+        } else {
+          uint32_t v = 0x80808080u;
+#pragma unroll
+          for (int j = 0; j < 3; j++)
+            if (4 * k + j < remb) v = (v & ~(0xFFu << (8 * j))) | ((uint32_t)s[4 * k + j] << (8 * j));
+          d[k] = v;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 3; k++) pq[k] = u32x4a{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
+    }
+  };
+  auto stage_commit = [&]() {
+    if (tid >= nitem) return;
+    const uint32_t d[12] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y,
+                            pq[1].z, pq[1].w, pq[2].x, pq[2].y, pq[2].z, pq[2].w};
+    u32x4s w0, w1, w2;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t a0 = d[3 * k], a1 = d[3 * k + 1], a2 = d[3 * k + 2];
+      w0[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00060300u), 0x05020100u) ^ 0x80808080u;
+      w1[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00070401u), 0x06020100u) ^ 0x80808080u;
+      w2[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00000502u), 0x07040100u) ^ 0x80808080u;
+    }
+    *reinterpret_cast<u32x4s *>(shared + (0 * 16 + pf_rr) * PP + 16 * pf_g) = w0;
+    *reinterpret_cast<u32x4s *>(shared + (1 * 16 + pf_rr) * PP + 16 * pf_g) = w1;
+    *reinterpret_cast<u32x4s *>(shared + (2 * 16 + pf_rr) * PP + 16 * pf_g) = w2;
+  };
   const int32_t *hmS0 = ai + D.hmS0, *hmC = ai + D.hmC;
   const i32x4 *hmB = reinterpret_cast<const i32x4 *>(ai + D.hmB);
   const int k0l = mfma_i8_k(lane, 0), k8l = mfma_i8_k(lane, 8);
@@ -603,13 +651,19 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
   // kFzThreads: start and step once, no integer division per item
   const int stepy = kFzThreads / aw, stepx = kFzThreads - stepy * aw;
   const int lm0 = tid / aw, lx0 = tid - lm0 * aw;
+  if (pf) stage_issue(0);
 #pragma unroll 1
   for (int c = 0; c < chunks; c++) {
     const int k0 = ai[D.vqK0 + c];
     const int need = min(k0 + 64, hrows);
     while (produced < need) {
       __syncthreads();  // the shared region's previous readers (vertical phase) are done
-      stage_block(produced);
+      if (pf) {
+        stage_commit();
+        if (produced + 16 < hrows) stage_issue(produced + 16);  // in flight over the work below
+      } else {
+        stage_block(produced);
+      }
       __syncthreads();
       hpass(produced);
       produced += 16;

@@ -76,16 +76,13 @@ EXPECTED_PATH = {"vr": "path_vr", "vm": "path_vm", "generic": "path_generic_v"}
 ])
 def test_baseline_geometries_take_the_path(rctx, W, H, opts, even_rows):
     """The BASELINE geometries run on the kernel the path names (no silent
-    fallback to another resample kernel); k_rs_vr takes evenly spaced touched
-    rows only, so cfg1's thumbnail-sampled rows run on k_rs_vm on every
-    vertical-first MFMA path."""
+    fallback to another resample kernel); k_rs_vr streams unevenly spaced
+    touched rows (cfg1's thumbnail sampling) from the row list."""
     from flyimg_amd.processor import ImageProcessor, OptionsBag
 
     op = ImageProcessor(OptionsBag(opts), W, H).to_op()
     src = synth_rgb(W, H, 7)
     want = EXPECTED_PATH[rctx.path_name]
-    if want == "path_vr" and not even_rows:
-        want = "path_vm"
     before = rctx.stats(want)[1]
     outs, recs, rc = rctx.process([src], [op])
     assert rc == 0 and recs[0].status == 0

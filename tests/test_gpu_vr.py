@@ -27,7 +27,8 @@ CASES = [
     (1200, 900, "w_300,r_270", 2),
     (800, 600, "w_250,clsp_Gray", 2),
     (333, 517, "w_97", 4),
-    (4000, 3000, "w_150", 2),  # sampled rows 5.33 apart: uneven, k_rs_vm (as cfg1)
+    (4000, 3000, "w_150", 2),  # sampled rows 5.33 apart: uneven, streamed from the row list
+    (3000, 2000, "w_300,h_250,c_1", 3),  # cfg1: 1250 of 2000 rows at gaps of 1 and 2
     (3840, 2160, "w_512,h_512,c_1", 300),
     (1920, 1080, "w_500", 300),
     (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", 24),
@@ -35,9 +36,8 @@ CASES = [
 ]
 
 
-# k_rs_vm's classes: ThumbnailImage sampled rows at uneven gaps (k_rs_vr takes
-# evenly spaced rows only) and strips wider than three 16-px output blocks
-NOT_VR = {(4000, 3000, "w_150"), (640, 480, "w_320")}
+# k_rs_vm's class: strips wider than three 16-px output blocks
+NOT_VR = {(640, 480, "w_320")}
 
 
 @pytest.fixture(scope="module")

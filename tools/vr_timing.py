@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Per-phase cycle sums of k_rs_vr (FI_VP_VARIANT=9 stamps, s_memtime ticks)
+"""Per-phase cycle sums of k_rs_vr (FI_VR_VARIANT=9 stamps, s_memtime ticks)
 on a full cfg2 batch, averaged over the persistent workgroups.
 V waves 0-7: tile entry, vertical MFMA issue, block done (planes), barrier.
-H waves 8-12: -, record / fragment reload, horizontal pass, -, barrier.
-L waves 14-15: A-fragment DMA issue, row DMA issue, vmcnt wait, barrier."""
+H waves 8-12: -, tile entry (fragment reload), horizontal pass, phase records (wave 12), barrier.
+S wave 13: -, stores, barrier.
+L waves 14-15: barrier, row DMA issue, A-fragment / LUT DMA issue, vmcnt wait."""
 import ctypes
 import os
 import sys
@@ -46,10 +47,12 @@ with Context(0) as ctx:
     a = a[a[:, 0, 5] > 0]
     ph = a[:, 0, 5].mean()
     roles = {"V": (range(0, 8), ["tile entry", "V-MFMA issue", "planes", "barrier"]),
-             "H": (range(8, 13 if VR else 14), ["-", "rec+frags", "horizontal", "stores", "barrier"]),
-             "L": (range(14, 16), ["stores+A DMA", "piece DMA", "vmcnt wait", "barrier"])}
+             "H": (range(8, 13 if VR else 14), ["-", "tile entry", "horizontal", "records (w12)", "barrier"]),
+             "S": (range(13, 14), ["-", "stores", "barrier"]),
+             "L": (range(14, 16), ["barrier", "row DMA", "A+LUT DMA", "vmcnt wait"])}
     print(f"{len(a)} workgroups, phases/WG {ph:.0f}; per-phase ticks by wave (mean over workgroups)")
     for r, (waves, names) in roles.items():
         for w in waves:
             v = a[:, w, :len(names)].mean(axis=0) / ph
-            print(f"  {r} wave {w:2d}: work {v[:-1].sum():7.0f} | " + "  ".join(f"{n} {x:6.0f}" for n, x in zip(names, v)))
+            work = sum(x for n, x in zip(names, v) if n not in ("barrier", "-"))
+            print(f"  {r} wave {w:2d}: work {work:7.0f} | " + "  ".join(f"{n} {x:6.0f}" for n, x in zip(names, v)))
