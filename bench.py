@@ -173,6 +173,19 @@ def cfg4_cpu_baseline(items, n_sample=8, threads=None):
                       f"{cores} threads (one image per thread per class), {wall:.1f} s measured wall"}
 
 
+def source_hash():
+    """sha256 of the library's sources, as tools/pmc_to_json.py records it"""
+    import hashlib
+
+    d = os.path.join(REPO, "flyimg_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".cpp", ".h")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,6 +278,7 @@ def main():
                                       "host_plan_blob", "host_launch", "host_wait", "host_total")}
     # images per resample kernel over the timed steps (counts kept by the library)
     paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in KERNEL_OF_PATH}
+    ablation = ctx.stats("vr_ablation")[1]  # FI_VR_VARIANT profiling launches (wrong pixels)
     last = arrs[(args.warmup + args.steps - 1) % 2]
     allv = comm.allgather_obj({"elapsed": el, "stats": stats,
                                "ncand": sum(last[i].n_candidates for i in range(nimg)),
@@ -307,9 +321,11 @@ def main():
                 "parallelism": f"dp{world} (images sharded per GPU, {gather.backend} gather of 32-B result records)"
                                if world > 1 else "dp1",
                 "record_gather": gather.backend,
-                "arithmetic": "resample exact-integer i8 MFMA on u8 (weights rint(w*2^22) in three signed-byte "
-                              "limbs, int32 sums, Q16 intermediate as ImageMagick, +-1 LSB of IM's f64); smartcrop "
-                              "prescale int32 (Pillow fixed point), maps f32/f64, scores f64 (bit-exact)",
+                "arithmetic": "resample exact-integer i8 MFMA on u8 (k_rs_vr: weights rint(w*2^s) in two signed-byte "
+                              "limbs, s = 15-22 by the largest weight, each row's sum kept; k_rs_vm / k_rs_hv: "
+                              "three limbs at 2^22), int32 sums, Q16 intermediate as ImageMagick, +-1 LSB of IM's "
+                              "f64; smartcrop prescale int32 (Pillow fixed point), maps f32/f64, scores f64 "
+                              "(bit-exact)",
             },
             "roofline": {
                 "bound": "hbm",
@@ -330,6 +346,9 @@ def main():
                          "timed batch vs the oracle (pixels +-1 LSB, crop box bit-exact on the GPU pixels)")
                         if not args.no_verify else "skipped (--no-verify)",
         }
+        if ablation:
+            result["ablation"] = (f"FI_VR_VARIANT={os.environ.get('FI_VR_VARIANT')}: {ablation} profiling launches "
+                                  "with wrong pixels -- not a valid measurement")
         # HBM traffic of the dominant kernel from the committed rocprofv3 PMC
         # passes (tools/gpu_profile.sh -> profiles/traffic_<workload>_<kernel>.json)
         kern = [p for p, n in paths.items() if n]
@@ -339,9 +358,14 @@ def main():
             if os.path.exists(tf):
                 t = json.load(open(tf))
                 ipl = rs_n and (nimg * args.steps) // rs_n or nimg
-                result["roofline"]["traffic"] = round(t["hbm_bytes_per_image"] * ipl)
-                result["roofline"]["traffic_source"] = (f"profiles/traffic_{args.workload}_{kname}.json: "
-                                                        f"{t['correction']}, measured per image x {ipl} images")
+                src = f"profiles/traffic_{args.workload}_{kname}.json"
+                if t.get("source_sha256") == source_hash():
+                    result["roofline"]["traffic"] = round(t["hbm_bytes_per_image"] * ipl)
+                    result["roofline"]["traffic_source"] = (f"{src}: {t['correction']}, measured per image x {ipl} "
+                                                            "images on these kernel sources")
+                else:
+                    result["roofline"]["traffic_stale"] = (f"{src} was measured on other kernel sources "
+                                                           "(source_sha256 differs): not reported")
         if not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(W, H, options)

@@ -775,12 +775,16 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
 constexpr int kScoreThreads = 1024;
 constexpr int kScoreWaves = kScoreThreads / 64;
 
-template <bool LDS_MAPS>
+// MODE 0: maps read from global memory; 1: maps in LDS; 2: maps in LDS and
+// the grouped fast pass (kScoreGrouped below).
+template <int MODE>
 __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__restrict__ descs,
                                                              const DevCrop *__restrict__ crops,
                                                              const double *__restrict__ ad,
                                                              CropScore *__restrict__ scores,
-                                                             ScResult *__restrict__ results, const ScParamsDev P) {
+                                                             ScResult *__restrict__ results, const ScParamsDev P,
+                                                             const int32_t *__restrict__ ai) {
+  constexpr bool LDS_MAPS = MODE >= 1;
   extern __shared__ __attribute__((aligned(16))) uint32_t smaps[];
   __shared__ double lut[256];
   __shared__ double part[kScoreWaves][3];
@@ -840,8 +844,150 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
   const double aoi = fabs(oi);
   const double wd = P.detail_weight, ws = P.skin_weight, wt = P.saturation_weight;
 
+  if (MODE == 2) {
+    // ---- grouped fast pass (kScoreGrouped).  A group = crops of one size at one
+    // y0 whose x0 step by 8 (smartcrop.py crops(): range(0, W - cw, step)); its
+    // union of columns is cut into 64-column chunks.  Lane `col` of a chunk
+    // reads its map word and the three per-pixel terms ONCE per row and adds
+    // them, weighted by (importance - outside_importance) from the group's
+    // table, into the crops c = G - j (G = col / 8, j < J = ceil(nin_x / 8))
+    // whose window holds it: 3 FMAs per (crop, pixel) instead of a map word,
+    // three table reads and 10 f64 operations.  Slots j come 8 at a time; the
+    // 8 lanes of a column group share (c, j), so their sums meet in a 3-step
+    // butterfly and lane 8g stores gpart[c][j] -- every (crop, j < J) exactly
+    // once, added up per crop in j order below (deterministic).
+    // Fd = sum_in (imp - oi) d + oi T0: the outside pixels need no pass.
+    double *gpart = reinterpret_cast<double *>(smaps + ((npx + 3) & ~3));  // [ncrops][J][3]
+    const int ngrp = D.ngrp, GJ = D.gJ;
+    const int4 *grp = reinterpret_cast<const int4 *>(ai + D.grp);  // 2 x int4 per group
+    int ntask = 0;
+    for (int gi = 0; gi < ngrp; gi++) {
+      const int4 g0 = grp[2 * gi], g1 = grp[2 * gi + 1];  // {c0, n, xg0, y0}, {nin_x, nin_y, tab2, tab_w}
+      const int width = 8 * (g0.y - 1) + g1.x, J = (g1.x + 7) >> 3;
+      ntask += ((width + 63) >> 6) * ((J + 7) >> 3);
+    }
+    int gi = 0, tbase = 0, nck = 0, njb = 0;
+    int4 g0{0, 0, 0, 0}, g1{0, 0, 0, 0};
+    auto load_group = [&]() {
+      g0 = grp[2 * gi];
+      g1 = grp[2 * gi + 1];
+      nck = (8 * (g0.y - 1) + g1.x + 63) >> 6;
+      njb = (((g1.x + 7) >> 3) + 7) >> 3;
+    };
+    if (ngrp > 0) load_group();
+    for (int t = wave; t < ntask; t += kScoreWaves) {
+      while (t >= tbase + nck * njb) {
+        tbase += nck * njb;
+        gi++;
+        load_group();
+      }
+      const int tt = t - tbase, ck = tt / njb, jb = tt - ck * njb;
+      const int c0 = g0.x, n = g0.y, xg0 = g0.z, y0 = g0.w;
+      const int nin_x = g1.x, nin_y = g1.y, tw = g1.w, J = (nin_x + 7) >> 3;
+      const double *tab = ad + g1.z;
+      const int width = 8 * (n - 1) + nin_x;
+      const int col = 64 * ck + lane, G = col >> 3, r0 = col & 7;
+      const bool act = col < width;
+      const uint32_t *mcol = maps + (int64_t)y0 * W + xg0 + (act ? col : 0);
+      double acc[8][3];
+      int toff[8];
+      bool ok[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; jj++) {
+        const int j = 8 * jb + jj, c = G - j, rel = r0 + 8 * j;
+        ok[jj] = act && j < J && c >= 0 && c < n && rel < nin_x;
+        toff[jj] = ok[jj] ? rel : 0;
+        acc[jj][0] = acc[jj][1] = acc[jj][2] = 0.0;
+      }
+      // the table reads (L2) run two rows ahead of their use
+      double impA[8], impB[8], impC[8];
+      auto load_imp = [&](double (&o)[8], int dy) {
+        const double *trow = tab + (int64_t)min(dy, nin_y - 1) * tw;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) o[jj] = ok[jj] ? trow[toff[jj]] : 0.0;
+      };
+      load_imp(impA, 0);
+      load_imp(impB, 1);
+#pragma unroll 1
+      for (int dy = 0; dy < nin_y; dy++) {
+        load_imp(impC, dy + 2);
+        const uint32_t m = act ? mcol[dy * W] : 0u;
+        const double d = lut[(m >> 8) & 255];
+        const double a1 = lut[m & 255] * (d + sb);
+        const double a2 = lut[(m >> 16) & 255] * (d + tb);
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+          acc[jj][0] = fma(impA[jj], d, acc[jj][0]);
+          acc[jj][1] = fma(impA[jj], a1, acc[jj][1]);
+          acc[jj][2] = fma(impA[jj], a2, acc[jj][2]);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+          impA[jj] = impB[jj];
+          impB[jj] = impC[jj];
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 8; jj++)
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          double v = acc[jj][q];
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          v += __shfl_xor(v, 4, 64);
+          acc[jj][q] = v;
+        }
+      if ((lane & 7) == 0 && 8 * G < width) {
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+          const int j = 8 * jb + jj, c = G - j;
+          if (j < J && c >= 0 && c < n) {
+            double *o = gpart + ((size_t)(c0 + c) * GJ + j) * 3;
+            o[0] = acc[jj][0];
+            o[1] = acc[jj][1];
+            o[2] = acc[jj][2];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < ncrops; c += kScoreThreads) {
+      const DevCrop cr = crops[D.crop0 + c];
+      const int J = (cr.nin_x + 7) >> 3;
+      double Fd = 0, Fs = 0, Ft = 0;
+      for (int j = 0; j < J; j++) {
+        const double *o = gpart + ((size_t)c * GJ + j) * 3;
+        Fd += o[0];
+        Fs += o[1];
+        Ft += o[2];
+      }
+      Fd += oi * T[0];
+      Fs += oi * T[1];
+      Ft += oi * T[2];
+      // |python_sum - F| <= 6 gamma(n+4) (imax + imax2 + |oi|) total(a), a >= 0: python's
+      // sequential sum (5 gamma(n+1) sum |imp a|) plus this pass (fl(imp - oi), one FMA
+      // per term, <= nin_y + J + 5 additions deep)
+      const double g4 = (nn + 3.0) * u / (1.0 - (nn + 3.0) * u);
+      const double kb = 6.0 * g4 * (cr.imax + cr.imax2 + aoi) * 1.0000001;
+      const double Ed = kb * T[0], Es = kb * T[1], Et = kb * T[2];
+      const double area = cr.fw * cr.fh;
+      const double tot = (Fd * wd + Fs * ws + Ft * wt) / area;
+      const double mag = fabs(wd) * (fabs(Fd) + Ed) + fabs(ws) * (fabs(Fs) + Es) + fabs(wt) * (fabs(Ft) + Et);
+      const double B = ((fabs(wd) * Ed + fabs(ws) * Es + fabs(wt) * Et) * (1.0 + 16.0 * u) + 16.0 * u * mag) /
+                       area * 1.01;
+      s_tot[c] = tot;
+      s_bnd[c] = B;
+      CropScore &o = sco[c];
+      o.detail = Fd;
+      o.saturation = Ft;
+      o.skin = Fs;
+      o.total = tot;
+      o.bound = B;
+      o.exact = 0;
+    }
+  }
   // ---- fast pass: one wave per crop, lanes across the window's columns
-  for (int c = wave; c < ncrops; c += kScoreWaves) {
+  for (int c = wave; c < (MODE == 2 ? 0 : ncrops); c += kScoreWaves) {
     const DevCrop cr = crops[D.crop0 + c];
     const double *tab = ad + cr.table;
     double sd = 0, ss = 0, st = 0, id = 0, is = 0, it = 0;
@@ -1123,17 +1269,20 @@ int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, 
   hipLaunchKernelGGL(k_sc_vmaps, dim3(n, chunks), dim3(kPrepThreads), lds, s, descs, ai, P);
   return 0;
 }
-int launch_sc_score(hipStream_t s, bool lds_maps, const ScDesc *descs, int n, int max_px, const DevCrop *crops,
-                    const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P) {
+int launch_sc_score(hipStream_t s, int mode, const ScDesc *descs, int n, size_t lds, const DevCrop *crops,
+                    const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P, const int32_t *ai) {
   if (n <= 0) return 0;
-  if (lds_maps) {
-    const size_t lds = (size_t)max_px * 4;
+  if (mode == 2) {
+    if (lds > (size_t)kScoreLdsGrouped) return -1;
+    hipLaunchKernelGGL((k_sc_score2<2>), dim3(n), dim3(kScoreThreads), lds, s, descs, crops, ad, scores, results, P,
+                       ai);
+  } else if (mode == 1) {
     if (lds > (size_t)kScoreLdsMaps) return -1;
-    hipLaunchKernelGGL((k_sc_score2<true>), dim3(n), dim3(kScoreThreads), lds, s, descs, crops, ad, scores, results,
-                       P);
+    hipLaunchKernelGGL((k_sc_score2<1>), dim3(n), dim3(kScoreThreads), lds, s, descs, crops, ad, scores, results, P,
+                       ai);
   } else {
-    hipLaunchKernelGGL((k_sc_score2<false>), dim3(n), dim3(kScoreThreads), 0, s, descs, crops, ad, scores, results,
-                       P);
+    hipLaunchKernelGGL((k_sc_score2<0>), dim3(n), dim3(kScoreThreads), 0, s, descs, crops, ad, scores, results, P,
+                       ai);
   }
   return 0;
 }

@@ -73,6 +73,7 @@ def test_vr_takes_the_class_and_matches(pair, W, H, opts, n):
     ob, rb, rcb = vr.process(srcs, [op] * n)
     assert rcb == 0 and all(r.status == 0 for r in rb), L.lib().fi_last_error()
     assert vr.stats(path)[1] == before + n  # no silent fallback to another kernel
+    assert vr.stats("vr_ablation")[1] == 0  # production kernel (no FI_VR_VARIANT ablation)
     oa, ra, rca = vm.process(srcs[:len(base)], [op] * len(base))
     assert rca == 0
     for k in range(len(base)):

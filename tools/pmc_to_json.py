@@ -10,8 +10,23 @@ is doubled; WRITE_SIZE is taken as is (dword/byte stores: uncalibrated).
 import collections
 import csv
 import glob
+import hashlib
 import json
+import os
 import sys
+
+
+def source_hash():
+    """sha256 of the library's kernel and host sources (bench.py checks it: a
+    traffic figure measured on other sources is reported as stale)"""
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "flyimg_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".cpp", ".h")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()
+
 
 root, kname, ipd, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
 vals = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -20,7 +35,7 @@ for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         if kname not in r.get("Kernel_Name", ""):
             continue
         vals[r["Counter_Name"]][r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
-res = {"kernel": kname, "images_per_dispatch": ipd}
+res = {"kernel": kname, "images_per_dispatch": ipd, "source_sha256": source_hash()}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     d = vals.get(c, {})
     # bench.py re-runs a small verification batch after the timed loop: only

@@ -2,9 +2,8 @@
 """Per-phase cycle sums of k_rs_vr (FI_VR_VARIANT=9 stamps, s_memtime ticks)
 on a full cfg2 batch, averaged over the persistent workgroups.
 V waves 0-7: tile entry, vertical MFMA issue, block done (planes), barrier.
-H waves 8-12: -, tile entry (fragment reload), horizontal pass, phase records (wave 12), barrier.
-S wave 13: -, stores, barrier.
-L waves 14-15: barrier, row DMA issue, A-fragment / LUT DMA issue, vmcnt wait."""
+H waves 8-12: -, tile entry (fragment reload), horizontal pass, -, barrier.
+L waves 14-15: A-fragment DMA issue, phase records + row DMA issue, vmcnt wait, barrier."""
 import ctypes
 import os
 import sys
@@ -47,9 +46,8 @@ with Context(0) as ctx:
     a = a[a[:, 0, 5] > 0]
     ph = a[:, 0, 5].mean()
     roles = {"V": (range(0, 8), ["tile entry", "V-MFMA issue", "planes", "barrier"]),
-             "H": (range(8, 13 if VR else 14), ["-", "tile entry", "horizontal", "records (w12)", "barrier"]),
-             "S": (range(13, 14), ["-", "stores", "barrier"]),
-             "L": (range(14, 16), ["barrier", "row DMA", "A+LUT DMA", "vmcnt wait"])}
+             "H": (range(8, 13 if VR else 14), ["-", "tile entry", "horizontal", "-", "barrier"]),
+             "L": (range(14, 16), ["A DMA", "records + row DMA", "vmcnt wait", "barrier"])}
     print(f"{len(a)} workgroups, phases/WG {ph:.0f}; per-phase ticks by wave (mean over workgroups)")
     for r, (waves, names) in roles.items():
         for w in waves:
