@@ -225,7 +225,6 @@ struct fi_ctx {
   std::map<const AxisTable *, HvV> hvv_cache;  // ok iff nblk > 0
   std::map<const AxisTable *, HvH> hvh_cache;  // ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
-  bool sc_grouped = true;  // FI_SC_GROUPED=0: the per-crop fast pass of k_sc_score2 instead of the grouped one
   // Device-resident table heaps: every per-geometry table (tap tables, MFMA
   // fragments, Pillow coefficients, importance tables) is uploaded once and
   // stays at a fixed offset; a batch uploads only the tables it adds.  The
@@ -246,8 +245,6 @@ struct fi_ctx {
   std::map<const AxisTable *, int32_t> axis_wd_at;  // f64 weights (RGBA path) in heap_d
   std::map<const ScPlan *, ScTabs> sc_at;
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_at;
-  std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp2_at;  // importance - oi
-  std::map<const ScPlan *, std::array<int32_t, 3>> grp_at;  // crop groups: ai offset, count, max J
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
   std::map<const VrV *, std::array<int32_t, 4>> vr_at;    // rows, bmeta, w128, frag
   std::map<const MfmaH *, std::array<int32_t, 6>> mh_at;  // wsum, frag, s0, lut, frag2, wsum2
@@ -447,8 +444,6 @@ static void heap_reset(fi_ctx *c) {
   c->axis_wd_at.clear();
   c->sc_at.clear();
   c->imp_at.clear();
-  c->imp2_at.clear();
-  c->grp_at.clear();
   c->vv_at.clear();
   c->vr_at.clear();
   c->mh_at.clear();
@@ -660,7 +655,6 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
         e.second = std::max(e.second, ch.nin_y);
       }
       std::map<std::pair<uint64_t, uint64_t>, std::tuple<int32_t, int32_t, double>> tab_of;
-      std::map<std::pair<uint64_t, uint64_t>, std::pair<int32_t, double>> tab2_of;  // importance - oi
       for (auto &sz : sizes) {
         double fw, fh;
         memcpy(&fw, &sz.first.first, 8);
@@ -683,19 +677,6 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
           ip = c->imp_at.emplace(pk, std::make_pair(off, imax)).first;
         }
         tab_of[sz.first] = std::make_tuple(ip->second.first, nx, ip->second.second);
-        // the grouped fast pass weighs inside pixels by fl(importance - oi)
-        auto i2 = c->imp2_at.find(pk);
-        if (i2 == c->imp2_at.end()) {
-          double imax2 = 0;
-          const int32_t off = E.od();
-          for (double v : iit->second) {
-            const double w = v - E.params.outside_importance;
-            imax2 = std::max(imax2, std::fabs(w));
-            E.ad.push_back(w);
-          }
-          i2 = c->imp2_at.emplace(pk, std::make_pair(off, imax2)).first;
-        }
-        tab2_of[sz.first] = i2->second;
       }
       q.crop0 = (int32_t)L->crops.size();
       q.ncrops = (int32_t)P.crops.size();
@@ -713,36 +694,11 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
         dc.table = std::get<0>(t);
         dc.table_w = std::get<1>(t);
         dc.imax = std::get<2>(t);
-        dc.imax2 = tab2_of[{dbits(ch.fw), dbits(ch.fh)}].second;
         dc.rx = ch.rx;
         dc.ry = ch.ry;
         dc.rw = ch.rw;
         dc.rh = ch.rh;
         L->crops.push_back(dc);
-      }
-      // crop groups of the grouped fast pass: consecutive crops of one size at
-      // one y0 whose x0 step by 8 -- {c0, n, xg0, y0}, {nin_x, nin_y, table - oi, pitch}
-      if (c->grp_at.find(&P) == c->grp_at.end()) {
-        std::vector<int32_t> g;
-        int32_t ng = 0, gJ = 0;
-        for (size_t k = 0; k < P.crops.size();) {
-          const CropHost &a = P.crops[k];
-          size_t e = k + 1;
-          while (e < P.crops.size() && dbits(P.crops[e].fw) == dbits(a.fw) && dbits(P.crops[e].fh) == dbits(a.fh) &&
-                 P.crops[e].nin_x == a.nin_x && P.crops[e].nin_y == a.nin_y && P.crops[e].y0 == a.y0 &&
-                 P.crops[e].x0 == P.crops[e - 1].x0 + 8)
-            e++;
-          const auto key = std::make_pair(dbits(a.fw), dbits(a.fh));
-          g.insert(g.end(), {(int32_t)k, (int32_t)(e - k), a.x0, a.y0, a.nin_x, a.nin_y, tab2_of[key].first,
-                             std::get<1>(tab_of[key])});
-          gJ = std::max(gJ, (a.nin_x + 7) / 8);
-          ng++;
-          k = e;
-        }
-        while (E.ai.size() % 4) E.ai.push_back(0);  // int4 reads
-        const int32_t off = E.oi();
-        E.ai.insert(E.ai.end(), g.begin(), g.end());
-        c->grp_at.emplace(&P, std::array<int32_t, 3>{off, ng, gJ});
       }
       pp = placed.emplace(&P, q).first;
     }
@@ -789,12 +745,6 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.vqK0 = T.vqK0;
     d.prescale = P.prescale;
     d.exact_all = o.exact_all || !fast_ok;
-    if (c->sc_grouped) {
-      const auto &gq = c->grp_at.at(&P);
-      d.grp = gq[0];
-      d.ngrp = gq[1];
-      d.gJ = gq[2];
-    }
     // workspace (offsets; converted to pointers after allocation)
     auto take = [&](size_t n) { return (uint8_t *)(uintptr_t)(E.work.take(n) + 1); };
     if (P.fx > 1 || P.fy > 1) d.red = take((size_t)P.rw * P.rh * 3);
@@ -849,15 +799,14 @@ struct ScLaunches {
   size_t fz_off = 0;  // k_sc_fz
   int nfz = 0, fz_lds = 0;
   int nvq = 0, vq_chunks = 0, vq_lds = 0;
-  size_t sl_off = 0, sg_off = 0, s3_off = 0;   // k_sc_score2 with maps in LDS / global / grouped fast pass
-  int nsl = 0, nsg = 0, sl_px = 0, ns3 = 0;
-  size_t s3_lds = 0;
+  size_t sl_off = 0, sg_off = 0;   // k_sc_score2 with maps in LDS / global
+  int nsl = 0, nsg = 0, sl_px = 0;
   size_t crops_off = 0;
 };
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> hm, sl, sg, s3, vq, vm, fz;
+  std::vector<ScDesc> hm, sl, sg, vq, vm, fz;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
     const ScDesc &d = SL.descs[k];
@@ -884,11 +833,7 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
       if (d.pre) svp.push_back((int)k);
       smaps.push_back((int)k);
     }
-    const size_t lds3 = (size_t)((d.aw * d.ah + 3) & ~3) * 4 + (size_t)d.ncrops * d.gJ * 24;
-    if (d.ngrp > 0 && d.ncrops <= kScoreMaxCrops && lds3 <= (size_t)kScoreLdsGrouped) {
-      s3.push_back(d);
-      X->s3_lds = std::max(X->s3_lds, lds3);
-    } else if ((int64_t)d.aw * d.ah * 4 <= kScoreLdsMaps) {
+    if ((int64_t)d.aw * d.ah * 4 <= kScoreLdsMaps) {
       sl.push_back(d);
       X->sl_px = std::max(X->sl_px, d.aw * d.ah);
     } else {
@@ -911,8 +856,6 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->nsl = (int)sl.size();
   X->sg_off = B.addv(sg);
   X->nsg = (int)sg.size();
-  X->s3_off = B.addv(s3);
-  X->ns3 = (int)s3.size();
   X->crops_off = B.addv(SL.crops);
 }
 static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &X, const int32_t *ai,
@@ -953,9 +896,6 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
   {
     Timer t(c, "sc_score", 0, st, st);
     const DevCrop *crops = (const DevCrop *)(ab + X.crops_off);
-    if (launch_sc_score(st, 2, (const ScDesc *)(ab + X.s3_off), X.ns3, X.s3_lds, crops, ad, scores, results, PD,
-                        ai) != 0)
-      return set_err(FI_EDEVICE, "k_sc_score2 (grouped) launch rejected (%zu B)", X.s3_lds);
     if (launch_sc_score(st, 1, (const ScDesc *)(ab + X.sl_off), X.nsl, (size_t)X.sl_px * 4, crops, ad, scores,
                         results, PD, ai) != 0)
       return set_err(FI_EDEVICE, "k_sc_score2 launch rejected (%d px)", X.sl_px);
@@ -1881,7 +1821,7 @@ static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
   B.b.reserve(B.b.size() + bytes(Bp.rd) + bytes(Bp.vdescs) + bytes(Bp.vstrips) + bytes(Bp.vtiles) +
               bytes(Bp.vrtiles) + bytes(Bp.vr_info) + bytes(Bp.hdescs) + bytes(Bp.hstrips) + bytes(Bp.htiles) +
               bytes(Bp.apply) + bytes(E.ai) + bytes(E.af) + bytes(E.ad) + 32 * sizeof(int32_t) * Bp.rd.size() +
-              (size_t)1 << 20);
+              ((size_t)1 << 20));
   std::vector<int> m0, m1, m2, q0, q1, q2;  // q*: RGBA (matte) images of modes 0 / 1 / 2
   for (size_t k = 0; k < Bp.rd.size(); k++) {
     if (Bp.rd[k].mode >= 3) continue;
@@ -2017,7 +1957,7 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
   if (!S.rs_done) HIP_TRY(hipEventCreateWithFlags(&S.rs_done, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(S.rs_done, c->stream));
   HIP_TRY(hipStreamWaitEvent(c->sc_stream, S.rs_done, 0));
-  if (K.SX.nsl + K.SX.nsg + K.SX.ns3 > 0) {
+  if (K.SX.nsl + K.SX.nsg > 0) {
     const int rc = enqueue_sc(c, c->sc_stream, ab, K.SX, ai, ad, (CropScore *)(wb + Bp.scores_off),
                               (ScResult *)(wb + Bp.results_off), PD);
     if (rc) return rc;
@@ -2685,7 +2625,6 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_FORCE_GENERIC")) c->fast_rs = c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
-  if (const char *e = getenv("FI_SC_GROUPED")) c->sc_grouped = !(e[0] == '0');
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   // (the smartcrop stage on a stream of its own beside the next batch's
   // resample was measured in round 2: the resample fills every CU, so the

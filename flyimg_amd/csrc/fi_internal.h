@@ -82,7 +82,6 @@ struct DevCrop {
   int32_t table_w;        // row pitch of the table
   int32_t rx, ry, rw, rh; // rescaled ints (crop() :184-190)
   double imax;            // max |importance| over the table (fast-pass error bound)
-  double imax2;           // max |importance - outside_importance| (the grouped fast pass's table)
 };
 
 struct ScDesc {
@@ -114,7 +113,6 @@ struct ScDesc {
   double T[3];         // unused on host; device scratch
   int32_t result;      // index into result array
   int32_t exact_all;
-  int32_t grp, ngrp, gJ;  // k_sc_score2<2>: crop groups (ai offset, 2 x int4 each), count, max J
 };
 
 // smartcrop prescale planning (fi_plan.cpp plan_sc_prep): kPrepRows rows per
@@ -130,7 +128,6 @@ constexpr int kFzMaxLds = 80 * 1024;
 // k_sc_score2: maps resident in LDS when aw*ah*4 <= this; crops whose totals /
 // bounds / candidate list stay in LDS (more: the image's CropScore slots).
 constexpr int kScoreLdsMaps = 112 * 1024;
-constexpr int kScoreLdsGrouped = 128 * 1024;  // maps + the grouped fast pass's per-(crop, j) partials
 constexpr int kScoreMaxCrops = 1024;
 
 // v_mfma_i32_16x16x64_i8 operand map (pinned by tools/mfma_probe.hip): lane l

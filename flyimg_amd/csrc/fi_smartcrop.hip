@@ -526,54 +526,6 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
       }
     }
   };
-  // the same staging software-pipelined: when a block is one item per thread of
-  // an aligned RGB source, block k + 1's loads are issued into registers before
-  // block k's horizontal pass (and before a chunk's vertical pass and maps), so
-  // their latency hides behind that work instead of heading every block
-  const bool pf = sC == 3 && a4 && nitem <= kFzThreads;
-  const int pf_rr = fz_div(tid, ng, rcp_ng), pf_g = tid - pf_rr * ng;
-  u32x4a pq[3];
-  auto stage_issue = [&](int r0) {
-    if (tid >= nitem) return;
-    const uint8_t *s = src + (int64_t)(r0 + pf_rr + yoff) * sstride + 48 * pf_g;
-    const int remb = r0 + pf_rr < hrows ? 3 * (sW - 16 * pf_g) : 0;
-    if (remb >= 48) {
-#pragma unroll
-      for (int k = 0; k < 3; k++) pq[k] = *reinterpret_cast<const u32x4a *>(s + 16 * k);
-    } else {
-      uint32_t d[12];
-#pragma unroll
-      for (int k = 0; k < 12; k++) {
-        if (4 * k + 4 <= remb) {
-          d[k] = *reinterpret_cast<const uint32_t *>(s + 4 * k);
-        } else {
-          uint32_t v = 0x80808080u;
-#pragma unroll
-          for (int j = 0; j < 3; j++)
-            if (4 * k + j < remb) v = (v & ~(0xFFu << (8 * j))) | ((uint32_t)s[4 * k + j] << (8 * j));
-          d[k] = v;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 3; k++) pq[k] = u32x4a{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
-    }
-  };
-  auto stage_commit = [&]() {
-    if (tid >= nitem) return;
-    const uint32_t d[12] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y,
-                            pq[1].z, pq[1].w, pq[2].x, pq[2].y, pq[2].z, pq[2].w};
-    u32x4s w0, w1, w2;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t a0 = d[3 * k], a1 = d[3 * k + 1], a2 = d[3 * k + 2];
-      w0[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00060300u), 0x05020100u) ^ 0x80808080u;
-      w1[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00070401u), 0x06020100u) ^ 0x80808080u;
-      w2[k] = __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, 0x00000502u), 0x07040100u) ^ 0x80808080u;
-    }
-    *reinterpret_cast<u32x4s *>(shared + (0 * 16 + pf_rr) * PP + 16 * pf_g) = w0;
-    *reinterpret_cast<u32x4s *>(shared + (1 * 16 + pf_rr) * PP + 16 * pf_g) = w1;
-    *reinterpret_cast<u32x4s *>(shared + (2 * 16 + pf_rr) * PP + 16 * pf_g) = w2;
-  };
   const int32_t *hmS0 = ai + D.hmS0, *hmC = ai + D.hmC;
   const i32x4 *hmB = reinterpret_cast<const i32x4 *>(ai + D.hmB);
   const int k0l = mfma_i8_k(lane, 0), k8l = mfma_i8_k(lane, 8);
@@ -651,19 +603,13 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
   // kFzThreads: start and step once, no integer division per item
   const int stepy = kFzThreads / aw, stepx = kFzThreads - stepy * aw;
   const int lm0 = tid / aw, lx0 = tid - lm0 * aw;
-  if (pf) stage_issue(0);
 #pragma unroll 1
   for (int c = 0; c < chunks; c++) {
     const int k0 = ai[D.vqK0 + c];
     const int need = min(k0 + 64, hrows);
     while (produced < need) {
       __syncthreads();  // the shared region's previous readers (vertical phase) are done
-      if (pf) {
-        stage_commit();
-        if (produced + 16 < hrows) stage_issue(produced + 16);  // in flight over the work below
-      } else {
-        stage_block(produced);
-      }
+      stage_block(produced);
       __syncthreads();
       hpass(produced);
       produced += 16;
@@ -775,8 +721,7 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
 constexpr int kScoreThreads = 1024;
 constexpr int kScoreWaves = kScoreThreads / 64;
 
-// MODE 0: maps read from global memory; 1: maps in LDS; 2: maps in LDS and
-// the grouped fast pass (kScoreGrouped below).
+// MODE 0: maps read from global memory; 1: maps in LDS.
 template <int MODE>
 __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__restrict__ descs,
                                                              const DevCrop *__restrict__ crops,
@@ -844,150 +789,8 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
   const double aoi = fabs(oi);
   const double wd = P.detail_weight, ws = P.skin_weight, wt = P.saturation_weight;
 
-  if (MODE == 2) {
-    // ---- grouped fast pass (kScoreGrouped).  A group = crops of one size at one
-    // y0 whose x0 step by 8 (smartcrop.py crops(): range(0, W - cw, step)); its
-    // union of columns is cut into 64-column chunks.  Lane `col` of a chunk
-    // reads its map word and the three per-pixel terms ONCE per row and adds
-    // them, weighted by (importance - outside_importance) from the group's
-    // table, into the crops c = G - j (G = col / 8, j < J = ceil(nin_x / 8))
-    // whose window holds it: 3 FMAs per (crop, pixel) instead of a map word,
-    // three table reads and 10 f64 operations.  Slots j come 8 at a time; the
-    // 8 lanes of a column group share (c, j), so their sums meet in a 3-step
-    // butterfly and lane 8g stores gpart[c][j] -- every (crop, j < J) exactly
-    // once, added up per crop in j order below (deterministic).
-    // Fd = sum_in (imp - oi) d + oi T0: the outside pixels need no pass.
-    double *gpart = reinterpret_cast<double *>(smaps + ((npx + 3) & ~3));  // [ncrops][J][3]
-    const int ngrp = D.ngrp, GJ = D.gJ;
-    const int4 *grp = reinterpret_cast<const int4 *>(ai + D.grp);  // 2 x int4 per group
-    int ntask = 0;
-    for (int gi = 0; gi < ngrp; gi++) {
-      const int4 g0 = grp[2 * gi], g1 = grp[2 * gi + 1];  // {c0, n, xg0, y0}, {nin_x, nin_y, tab2, tab_w}
-      const int width = 8 * (g0.y - 1) + g1.x, J = (g1.x + 7) >> 3;
-      ntask += ((width + 63) >> 6) * ((J + 7) >> 3);
-    }
-    int gi = 0, tbase = 0, nck = 0, njb = 0;
-    int4 g0{0, 0, 0, 0}, g1{0, 0, 0, 0};
-    auto load_group = [&]() {
-      g0 = grp[2 * gi];
-      g1 = grp[2 * gi + 1];
-      nck = (8 * (g0.y - 1) + g1.x + 63) >> 6;
-      njb = (((g1.x + 7) >> 3) + 7) >> 3;
-    };
-    if (ngrp > 0) load_group();
-    for (int t = wave; t < ntask; t += kScoreWaves) {
-      while (t >= tbase + nck * njb) {
-        tbase += nck * njb;
-        gi++;
-        load_group();
-      }
-      const int tt = t - tbase, ck = tt / njb, jb = tt - ck * njb;
-      const int c0 = g0.x, n = g0.y, xg0 = g0.z, y0 = g0.w;
-      const int nin_x = g1.x, nin_y = g1.y, tw = g1.w, J = (nin_x + 7) >> 3;
-      const double *tab = ad + g1.z;
-      const int width = 8 * (n - 1) + nin_x;
-      const int col = 64 * ck + lane, G = col >> 3, r0 = col & 7;
-      const bool act = col < width;
-      const uint32_t *mcol = maps + (int64_t)y0 * W + xg0 + (act ? col : 0);
-      double acc[8][3];
-      int toff[8];
-      bool ok[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; jj++) {
-        const int j = 8 * jb + jj, c = G - j, rel = r0 + 8 * j;
-        ok[jj] = act && j < J && c >= 0 && c < n && rel < nin_x;
-        toff[jj] = ok[jj] ? rel : 0;
-        acc[jj][0] = acc[jj][1] = acc[jj][2] = 0.0;
-      }
-      // the table reads (L2) run two rows ahead of their use
-      double impA[8], impB[8], impC[8];
-      auto load_imp = [&](double (&o)[8], int dy) {
-        const double *trow = tab + (int64_t)min(dy, nin_y - 1) * tw;
-#pragma unroll
-        for (int jj = 0; jj < 8; jj++) o[jj] = ok[jj] ? trow[toff[jj]] : 0.0;
-      };
-      load_imp(impA, 0);
-      load_imp(impB, 1);
-#pragma unroll 1
-      for (int dy = 0; dy < nin_y; dy++) {
-        load_imp(impC, dy + 2);
-        const uint32_t m = act ? mcol[dy * W] : 0u;
-        const double d = lut[(m >> 8) & 255];
-        const double a1 = lut[m & 255] * (d + sb);
-        const double a2 = lut[(m >> 16) & 255] * (d + tb);
-#pragma unroll
-        for (int jj = 0; jj < 8; jj++) {
-          acc[jj][0] = fma(impA[jj], d, acc[jj][0]);
-          acc[jj][1] = fma(impA[jj], a1, acc[jj][1]);
-          acc[jj][2] = fma(impA[jj], a2, acc[jj][2]);
-        }
-#pragma unroll
-        for (int jj = 0; jj < 8; jj++) {
-          impA[jj] = impB[jj];
-          impB[jj] = impC[jj];
-        }
-      }
-#pragma unroll
-      for (int jj = 0; jj < 8; jj++)
-#pragma unroll
-        for (int q = 0; q < 3; q++) {
-          double v = acc[jj][q];
-          v += __shfl_xor(v, 1, 64);
-          v += __shfl_xor(v, 2, 64);
-          v += __shfl_xor(v, 4, 64);
-          acc[jj][q] = v;
-        }
-      if ((lane & 7) == 0 && 8 * G < width) {
-#pragma unroll
-        for (int jj = 0; jj < 8; jj++) {
-          const int j = 8 * jb + jj, c = G - j;
-          if (j < J && c >= 0 && c < n) {
-            double *o = gpart + ((size_t)(c0 + c) * GJ + j) * 3;
-            o[0] = acc[jj][0];
-            o[1] = acc[jj][1];
-            o[2] = acc[jj][2];
-          }
-        }
-      }
-    }
-    __syncthreads();
-    for (int c = tid; c < ncrops; c += kScoreThreads) {
-      const DevCrop cr = crops[D.crop0 + c];
-      const int J = (cr.nin_x + 7) >> 3;
-      double Fd = 0, Fs = 0, Ft = 0;
-      for (int j = 0; j < J; j++) {
-        const double *o = gpart + ((size_t)c * GJ + j) * 3;
-        Fd += o[0];
-        Fs += o[1];
-        Ft += o[2];
-      }
-      Fd += oi * T[0];
-      Fs += oi * T[1];
-      Ft += oi * T[2];
-      // |python_sum - F| <= 6 gamma(n+4) (imax + imax2 + |oi|) total(a), a >= 0: python's
-      // sequential sum (5 gamma(n+1) sum |imp a|) plus this pass (fl(imp - oi), one FMA
-      // per term, <= nin_y + J + 5 additions deep)
-      const double g4 = (nn + 3.0) * u / (1.0 - (nn + 3.0) * u);
-      const double kb = 6.0 * g4 * (cr.imax + cr.imax2 + aoi) * 1.0000001;
-      const double Ed = kb * T[0], Es = kb * T[1], Et = kb * T[2];
-      const double area = cr.fw * cr.fh;
-      const double tot = (Fd * wd + Fs * ws + Ft * wt) / area;
-      const double mag = fabs(wd) * (fabs(Fd) + Ed) + fabs(ws) * (fabs(Fs) + Es) + fabs(wt) * (fabs(Ft) + Et);
-      const double B = ((fabs(wd) * Ed + fabs(ws) * Es + fabs(wt) * Et) * (1.0 + 16.0 * u) + 16.0 * u * mag) /
-                       area * 1.01;
-      s_tot[c] = tot;
-      s_bnd[c] = B;
-      CropScore &o = sco[c];
-      o.detail = Fd;
-      o.saturation = Ft;
-      o.skin = Fs;
-      o.total = tot;
-      o.bound = B;
-      o.exact = 0;
-    }
-  }
   // ---- fast pass: one wave per crop, lanes across the window's columns
-  for (int c = wave; c < (MODE == 2 ? 0 : ncrops); c += kScoreWaves) {
+  for (int c = wave; c < ncrops; c += kScoreWaves) {
     const DevCrop cr = crops[D.crop0 + c];
     const double *tab = ad + cr.table;
     double sd = 0, ss = 0, st = 0, id = 0, is = 0, it = 0;
@@ -1272,11 +1075,7 @@ int launch_sc_v(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, 
 int launch_sc_score(hipStream_t s, int mode, const ScDesc *descs, int n, size_t lds, const DevCrop *crops,
                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P, const int32_t *ai) {
   if (n <= 0) return 0;
-  if (mode == 2) {
-    if (lds > (size_t)kScoreLdsGrouped) return -1;
-    hipLaunchKernelGGL((k_sc_score2<2>), dim3(n), dim3(kScoreThreads), lds, s, descs, crops, ad, scores, results, P,
-                       ai);
-  } else if (mode == 1) {
+  if (mode == 1) {
     if (lds > (size_t)kScoreLdsMaps) return -1;
     hipLaunchKernelGGL((k_sc_score2<1>), dim3(n), dim3(kScoreThreads), lds, s, descs, crops, ad, scores, results, P,
                        ai);

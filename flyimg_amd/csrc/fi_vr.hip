@@ -293,10 +293,21 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       cb = CT.b0;
     };
     if (ct < t1) ptile_load();
+    // the cursor block's table reads (meta; the bias row on L wave 0) are issued
+    // when the cursor moves there, a phase before next_phase uses them: their
+    // latency is spent at the barrier's lgkmcnt(0) wait instead of ahead of the
+    // row DMAs
+    int4 m{0, 0, 0, 0};  // {K0, ks, Rend, 0}
+    W16 wc{};
+    auto pref = [&]() {
+      if (ct >= t1) return;
+      m = ldc(reinterpret_cast<const int4 *>(ai + c_bmeta + 4 * cb));
+      if (li == 0) wc = ldc(reinterpret_cast<const W16 *>(ai + c_w128 + 16 * cb));
+    };
+    pref();
     // the phase at the cursor; writes its record (slot s) and stages its tile's
     // LUT (first block of a tile) -- L wave 0 only; advances the cursor
     auto next_phase = [&](int s) -> PI {
-      const int4 m = ldc(reinterpret_cast<const int4 *>(ai + c_bmeta + 4 * cb));  // {K0, ks, Rend, 0}
       PI r;
       r.t = ct;
       r.blk = cb;
@@ -308,9 +319,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       r.flags = (cb == CT.b0 ? kFirst : 0) | ((s & 1) ? kSlot : 0) | ((ck & (kLutSlots - 1)) << kTslotShift) |
                 (c_vsh << kVshShift);
       if (li == 0) {
-        // the bias row rides in the record (scalar loads two phases ahead) instead
-        // of a 64-byte DMA in the loader's stream
-        const W16 wc = ldc(reinterpret_cast<const W16 *>(ai + r.w128));
+        // the bias row rides in the record (scalar loads) instead of a 64-byte DMA
+        // in the loader's stream
         if (lane == 0) {
           Rec rr{r.t, r.blk, r.flags, r.gk0 % R, r.ks, r.grend, r.frag, r.w128, {}};
 #pragma unroll
@@ -327,6 +337,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         ct++;
         if (ct < t1) ptile_load();
       }
+      pref();
       return r;
     };
     // A fragments (ks k-steps x 2 limbs x 1 KB) into A slot `slot`

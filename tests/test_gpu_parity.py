@@ -44,15 +44,13 @@ def _context_with(env):
                 os.environ[k] = v
 
 
-_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_SC_GROUPED": "1"}
+_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0"}
 PATHS = {
     # default kernels: k_rs_vr (block-major persistent MFMA resample; k_rs_vm
     # where its tables do not fit) / k_rs_hv; k_sc_fz fused prescale + maps; k_sc_score2
-    # with the grouped fast pass
     "vr": dict(_ENV),
-    # the fallbacks: k_rs_vm streaming resample; k_sc_hmfma + k_sc_vq (H-stage rows through HBM);
-    # k_sc_score2's per-crop fast pass (FI_SC_GROUPED=0) in place of the grouped one
-    "vm": dict(_ENV, FI_VR_RS="0", FI_DISABLE_SC_FZ="1", FI_SC_GROUPED="0"),
+    # the fallbacks: k_rs_vm streaming resample; k_sc_hmfma + k_sc_vq (H-stage rows through HBM)
+    "vm": dict(_ENV, FI_VR_RS="0", FI_DISABLE_SC_FZ="1"),
     # generic kernels: two-pass resample; per-row prescale/maps kernels
     "generic": dict(_ENV, FI_FORCE_GENERIC="1"),
 }

@@ -24,3 +24,30 @@ def test_mfma_tables_exact():
         r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stdout + r.stderr
         assert "OK (0 failures)" in r.stdout
+
+
+@pytest.mark.parametrize("src,kernels", [
+    ("fi_vr.hip", ["_ZN2fi7k_rs_vrILi0EE"]),
+    ("fi_smartcrop.hip", ["_ZN2fi11k_sc_score2ILi1EE"]),
+])
+def test_hot_kernels_do_not_spill(src, kernels):
+    """The production kernels of the hot path keep every value in registers: a
+    VGPR spill (scratch) cost a 1.6x slowdown of k_rs_vr once (round 4)."""
+    import re
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    with tempfile.TemporaryDirectory() as d:
+        r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+                            "-I", os.path.join(ROOT, "include"), "-c", os.path.join(ROOT, "flyimg_amd/csrc", src),
+                            "-o", os.path.join(d, "k.o"), "-Rpass-analysis=kernel-resource-usage"],
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+    text = r.stderr
+    for k in kernels:
+        i = text.find("Function Name: " + k)
+        assert i >= 0, k
+        block = text[i:i + 2000]
+        scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", block).group(1))
+        assert scratch == 0, (k, scratch)
