@@ -395,7 +395,7 @@ static void put_frag2(std::vector<int32_t> &frag, size_t base, int lane, int j, 
 }
 // W = rint(w * 2^shift) per tap, then per output the |d| taps whose rounding
 // residual points furthest the needed way move by one so that sum(W) =
-// rint(sum(w) * 2^shift): IM's weights are normalised to sum 1, and a
+// 2^shift: IM's weights are normalised to sum 1, and a
 // quantised row that keeps its sum reproduces a flat region exactly (rounding
 // each tap alone leaves a bias that repeats on every output at integral
 // factors: 98.5 % exact at 1/10 against 99.98 % with the sum kept)
@@ -413,7 +413,10 @@ static void quant_axis(const AxisTable &t, int shift, std::vector<int32_t> *wq) 
       (*wq)[w0 + j] = (int32_t)lrint(x);
       sq += (*wq)[w0 + j];
     }
-    int64_t d = (int64_t)llrint(sx) - sq;
+    // IM normalises every row to sum 1 (resize.c density): the target is 2^shift,
+    // not the float-rounded sum of the float weights
+    int64_t d = (n > 0 ? ((int64_t)1 << shift) : 0) - sq;
+    (void)sx;
     if (d == 0) continue;
     const int dir = d > 0 ? 1 : -1;
     ord.clear();
@@ -708,6 +711,9 @@ bool build_vr_v(const AxisTable &v, VrV *m) {
   }
   for (int y = 0; y < ny; y++)
     for (int j = 0; j < v.count[y]; j++) m->w128[y] += 128 * wq[v.woff[y] + j];
+  // k_rs_vr's MFMA bias is the constant 128 * 2^shift: every row must sum to 2^shift
+  for (int y = 0; y < ny; y++)
+    if (m->w128[y] != (128 << m->shift)) return false;
   m->row0 = m->rows[0];
   m->rstep = nl > 1 ? m->rows[1] - m->rows[0] : 1;
   for (int k = 1; k < nl && m->rstep > 0; k++)

@@ -57,7 +57,7 @@ constexpr int kSW = 1;                   // S wave 13: the stores of the output 
 constexpr int kLW = 2;                   // L waves 14-15
 static_assert(kVW + kHW + kSW + kLW == 16, "16 waves");
 constexpr int kABytes = 4096;            // [t][limb][64 lanes][16 B]: two limbs, <= 2 k-steps
-constexpr int kRecBytes = 96;
+constexpr int kRecBytes = 32;
 constexpr int kLutSlots = 4;
 constexpr int kPlanePad = 176;           // 44 (mod 64) dwords: see fi_vm.hip kVmPlanePad
 constexpr int kOt8Pitch = 200;           // 8-bit output tile row (<= 64 px x 3 + the row shift)
@@ -196,12 +196,14 @@ __device__ __forceinline__ void wait_vm_le(int n) {
   }
 }
 
-struct Rec {  // 96 B in LDS (kRecBytes)
+struct Rec {  // 32 B in LDS (kRecBytes)
   int32_t t, blk, flags, slot0, ks, grend, frag, w128;  // frag / w128: int32 offsets into ai
-  int32_t corr[16];  // 128 * weight sums of the block's 16 output rows (the MFMA bias)
 };
 struct W16 {
   int32_t v[16];
+};
+struct W8 {
+  int32_t v[8];
 };
 struct Lds {  // offsets of the launch's LDS regions
   int ring, a, rec, cnt, lut, planes, otile;
@@ -293,21 +295,10 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       cb = CT.b0;
     };
     if (ct < t1) ptile_load();
-    // the cursor block's table reads (meta; the bias row on L wave 0) are issued
-    // when the cursor moves there, a phase before next_phase uses them: their
-    // latency is spent at the barrier's lgkmcnt(0) wait instead of ahead of the
-    // row DMAs
-    int4 m{0, 0, 0, 0};  // {K0, ks, Rend, 0}
-    W16 wc{};
-    auto pref = [&]() {
-      if (ct >= t1) return;
-      m = ldc(reinterpret_cast<const int4 *>(ai + c_bmeta + 4 * cb));
-      if (li == 0) wc = ldc(reinterpret_cast<const W16 *>(ai + c_w128 + 16 * cb));
-    };
-    pref();
     // the phase at the cursor; writes its record (slot s) and stages its tile's
     // LUT (first block of a tile) -- L wave 0 only; advances the cursor
     auto next_phase = [&](int s) -> PI {
+      const int4 m = ldc(reinterpret_cast<const int4 *>(ai + c_bmeta + 4 * cb));  // {K0, ks, Rend, 0}
       PI r;
       r.t = ct;
       r.blk = cb;
@@ -319,14 +310,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       r.flags = (cb == CT.b0 ? kFirst : 0) | ((s & 1) ? kSlot : 0) | ((ck & (kLutSlots - 1)) << kTslotShift) |
                 (c_vsh << kVshShift);
       if (li == 0) {
-        // the bias row rides in the record (scalar loads) instead of a 64-byte DMA
-        // in the loader's stream
-        if (lane == 0) {
-          Rec rr{r.t, r.blk, r.flags, r.gk0 % R, r.ks, r.grend, r.frag, r.w128, {}};
-#pragma unroll
-          for (int k = 0; k < 16; k++) rr.corr[k] = wc.v[k];
-          recs[s & 7] = rr;
-        }
+        if (lane == 0) recs[s & 7] = Rec{r.t, r.blk, r.flags, r.gk0 % R, r.ks, r.grend, r.frag, r.w128};
         if ((r.flags & kFirst) && lane < (c_lut_n + 3) / 4)
           dma16(lds_addr(lds) + (uint32_t)(O.lut + (ck & (kLutSlots - 1)) * 1024),
                 reinterpret_cast<const uint8_t *>(ai + c_lut), 16u * lane);
@@ -337,7 +321,6 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         ct++;
         if (ct < t1) ptile_load();
       }
-      pref();
       return r;
     };
     // A fragments (ks k-steps x 2 limbs x 1 KB) into A slot `slot`
@@ -374,7 +357,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     // Evenly spaced touched rows (rstep > 0): a loop with no loads, bases linear
     // in the pair index, the chunk swizzle from the ring slot.  Uneven ones
     // (ThumbnailImage sampling at a non-integral step, cfg1's 2000 -> 1250): the
-    // rows come from the touched-row list, 16 entries (four own pairs) per
+    // rows come from the touched-row list, 8 entries (two own pairs) per
     // scalar load, the next group's load in flight while this one is issued.
     auto issue_rows = [&](int limit) -> int {
       int n = 0;
@@ -388,12 +371,12 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         int k0 = RT.kbase + (rG - RT.g0);
         if (r_rstep == 0 && k0 + 1 < r_nrows) {
           const int cnt = min((seg - rG + 3) >> 2, (r_nrows - 1 - k0 + 3) >> 2);
-          const W16 *lst = reinterpret_cast<const W16 *>(ai + r_rows + k0);  // the host pads the list by 32
-          W16 cur = ldc(lst), nxt{};
-          for (int j0 = 0; j0 < cnt; j0 += 4) {
-            if (j0 + 4 < cnt) nxt = ldc(lst + (j0 / 4 + 1));
+          const W8 *lst = reinterpret_cast<const W8 *>(ai + r_rows + k0);  // the host pads the list by 32
+          W8 cur = ldc(lst), nxt{};
+          for (int j0 = 0; j0 < cnt; j0 += 2) {
+            if (j0 + 2 < cnt) nxt = ldc(lst + (j0 / 2 + 1));
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < 2; j++) {
               if (j0 + j >= cnt) break;
               const int r0 = cur.v[4 * j], r1 = cur.v[4 * j + 1];
               const uint32_t f = (uint32_t)((rslot & 7) | (((rslot >> 4) & 1) << 3));
@@ -599,8 +582,10 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         }
         stamp(0);
         const i32x4 *al = reinterpret_cast<const i32x4 *>(lds + O.a + (p & 1) * kABytes);
-        // 128 * weight sums of this lane's 4 output rows, from block p's record
-        const i32x4 corr = *reinterpret_cast<const i32x4 *>(&recs[p & 7].corr[4 * (lane >> 4)]);
+        // the MFMA bias, 128 * the weight sum of every output row (pixels enter as
+        // p - 128): the quantised rows sum to exactly 2^shift (fi_plan.h VrV)
+        const int32_t cb = 128 << ((C.flags >> kVshShift) & 31);
+        const i32x4 corr = {cb, cb, cb, cb};
         i32x4 acc[2][kT];
         const uint32_t RB = (uint32_t)R * 512u;
         // both k-steps' ring and A reads in flight before the first MFMA

@@ -50,4 +50,5 @@ def test_hot_kernels_do_not_spill(src, kernels):
         assert i >= 0, k
         block = text[i:i + 2000]
         scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", block).group(1))
-        assert scratch == 0, (k, scratch)
+        sspill = int(re.search(r"SGPRs Spill: (\d+)", block).group(1))
+        assert scratch == 0 and sspill == 0, (k, scratch, sspill)
