@@ -506,7 +506,32 @@ def run_cfg4(args, rank, world, local_rank, comm):
              "host_total")
     stats = {k: ctx.stats(k) for k in names}
     paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in KERNEL_OF_PATH}
-    allv = comm.allgather_obj({"elapsed": t1 - t0, "stats": stats, "bad": bad[0], "n": len(shard)})
+    ablation = ctx.stats("vr_ablation")[1]
+    # correctness of the timed work itself (untimed): 16 images of this rank's
+    # last batch, spread over it, against the oracle (each image its own size
+    # class and op; smart-crop boxes bit-exact on the GPU pixels)
+    vok, vtot, verr = 0, 0, None
+    if batches and not args.no_verify:
+        from oracle.verify import verify_mixed_batch  # the checker (test infrastructure)
+
+        lb, la = batches[-1], arrs[(len(batches) - 1) % 2]
+        slot = (len(batches) - 1) % 2
+        views, vops, seeds, offs, o = [], [], [], [], 0
+        for i in lb:
+            W, H, k = items[i]
+            op, (ow, oh, oc) = ops[(W, H, k)]
+            wh = (W, H)
+            views.append((pool + off_of[wh] + copy_of[i] * stride_of[wh] * H, W, H, stride_of[wh]))
+            vops.append(op)
+            seeds.append(0x5EED + 7919 * sizes.index(wh) + 104729 * copy_of[i])
+            offs.append(o)
+            o += ow * oh * oc
+        idxs = sorted({int(v) for v in np.linspace(0, len(lb) - 1, 16)})
+        vok, vtot, verr = verify_mixed_batch(ctx, la, views, vops, idxs, seeds, lambda j: dst[slot] + offs[j])
+        if verr:
+            log(f"rank {rank}: VERIFY FAILED {vok}/{vtot}: {verr}")
+    allv = comm.allgather_obj({"elapsed": t1 - t0, "stats": stats, "bad": bad[0], "n": len(shard),
+                               "vok": vok, "vtot": vtot, "verr": verr})
     if rank == 0:
         T = max(v["elapsed"] for v in allv)
         mpix = sum(W * H for W, H, _ in items) * args.steps / 1e6
@@ -550,15 +575,34 @@ def run_cfg4(args, rank, world, local_rank, comm):
             "stages_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4) for k, v in stats.items()},
             "shard_images": [v["n"] for v in allv],
             "failed_images": sum(v["bad"] for v in allv),
+            "verified": (f"{sum(v['vok'] for v in allv)}/{sum(v['vtot'] for v in allv)} images of each rank's last "
+                         "batch vs the oracle (pixels +-1 LSB, crop box bit-exact on the GPU pixels)")
+                        if not args.no_verify else "skipped (--no-verify)",
         }
+        if ablation:
+            result["ablation"] = (f"FI_VR_VARIANT={os.environ.get('FI_VR_VARIANT')}: {ablation} profiling launches "
+                                  "with wrong pixels -- not a valid measurement")
+        tf = os.path.join(REPO, "profiles", "traffic_cfg4_resize.json")
+        if os.path.exists(tf):
+            t = json.load(open(tf))
+            if t.get("source_sha256") == source_hash():
+                ipl = len(shard) * args.steps / max(rs_n, 1)  # images per resize launch
+                result["roofline"]["traffic"] = round(t["hbm_bytes_per_image"] * ipl)
+                result["roofline"]["traffic_source"] = (f"profiles/traffic_cfg4_resize.json: {t['correction']}, "
+                                                        "the resize launches of the sampled batches, per image")
+            else:
+                result["roofline"]["traffic_stale"] = "profiles/traffic_cfg4_resize.json measured on other sources"
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cfg4_cpu_baseline(items)
         print(json.dumps(result), flush=True)
+    verify_failed = any(v["verr"] for v in allv)
     ctx.free(pool)
     for d in dst:
         ctx.free(d)
     comm.close()
     ctx.close()
+    if verify_failed:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -212,6 +212,7 @@ struct fi_ctx {
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
   bool fast_rs = true;  // FI_FORCE_GENERIC=1: the generic two-pass resample (and smartcrop) kernels only
   bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
+  int vr_max_classes = 8;  // batches with more vertical tables stay on k_rs_vm (FI_VR_MAX_CLASSES)
   int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
@@ -1682,10 +1683,9 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     // (uneven tiles, per-tile table changes): measured on cfg4's mix (384 size
     // classes x five ops) k_rs_vm took 385 ms against 432 with k_rs_vr, so a
     // batch with more than kVrMaxClasses vertical tables stays on k_rs_vm
-    constexpr size_t kVrMaxClasses = 8;
     std::set<const VrV *> classes;
     for (const VrWork &w : vr) classes.insert(w.V);
-    if (!vr.empty() && classes.size() <= kVrMaxClasses && build_vr_tiles(c, E, Bp, vr)) work.swap(rest);
+    if (!vr.empty() && (int)classes.size() <= c->vr_max_classes && build_vr_tiles(c, E, Bp, vr)) work.swap(rest);
   }
   // bands of blocks only when the batch is too small to fill the chip
   int64_t nst = 0;
@@ -2625,6 +2625,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_FORCE_GENERIC")) c->fast_rs = c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
+  if (const char *e = getenv("FI_VR_MAX_CLASSES")) c->vr_max_classes = atoi(e);
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   // (the smartcrop stage on a stream of its own beside the next batch's
   // resample was measured in round 2: the resample fills every CU, so the

@@ -227,8 +227,9 @@ constexpr int kVrStampN = 16 * 6;
 __device__ uint64_t g_vr_stamps[kVrStampSlots * kVrStampN];
 
 // MODE (profiling ablations, FI_VR_VARIANT; wrong pixels): 0 production,
-// 1 DMA stream only, 2 no H role and no stores, 3 no stores, 9 production +
-// per-phase s_memtime sums; 10 + k: ablation k with the stamps.
+// 1 DMA stream only, 2 no H role and no stores, 3 no stores, 5 / 6 loader
+// priority 1 / 0 (production pixels), 9 production + per-phase s_memtime sums;
+// 10 + k: ablation k with the stamps.
 template <int MODE>
 __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ descs, const MStrip *__restrict__ strips,
                                                    const VrTile *__restrict__ tiles, int ntiles,
@@ -494,8 +495,11 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     // own pairs (starts 4 m + 2 li) below stream row x
     auto own_below = [&](int x) -> int { return x > 2 * li ? (x - 2 * li + 3) >> 2 : 0; };
 
-    // the loader's few instructions go first on its SIMD
-    __builtin_amdgcn_s_setprio(2);
+    // the loader's few instructions go first on its SIMD (MODE 5 / 6: priority 1 / 0)
+    if (M == 5)
+      __builtin_amdgcn_s_setprio(1);
+    else if (M != 6)
+      __builtin_amdgcn_s_setprio(2);
     if (li == 0 && lane == 0) hcnt[0] = 0;
     PI P0{}, P1{};
     if (N > 0) {
@@ -951,6 +955,8 @@ int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrT
     case 1: FI_VR_LAUNCH(1); break;
     case 2: FI_VR_LAUNCH(2); break;
     case 3: FI_VR_LAUNCH(3); break;
+    case 5: FI_VR_LAUNCH(5); break;
+    case 6: FI_VR_LAUNCH(6); break;
     case 9: FI_VR_LAUNCH(9); break;
     case 11: FI_VR_LAUNCH(11); break;
     case 12: FI_VR_LAUNCH(12); break;

@@ -89,3 +89,57 @@ def verify_batch(ctx, arr, idxs, src_ptr, seed_of, W, H, src_stride, op, dst_of,
         except AssertionError as e:
             err = err or f"image {i}: {e}"
     return ok, len(idxs), err
+
+
+def verify_mixed_batch(ctx, arr, views, ops, idxs, seeds, dst_of):
+    """verify_batch for a batch of mixed geometries (cfg4).  The untimed re-run
+    without the crop apply covers the WHOLE batch (views / ops of every image),
+    so the library makes the same per-batch kernel choices as in the timed run
+    (k_rs_vr takes a batch of <= FI_VR_MAX_CLASSES vertical tables; a single
+    image would always take it) and the re-run pixels are the timed run's.
+    Checked for images idxs: resampled pixels within +-1 LSB of the oracle;
+    with smart-crop, the record's box bit-exact with the oracle's smartcrop on
+    those pixels and the applied output equal to that box of them.  seeds[i]:
+    the synth_rgb seed of image i.  Returns (ok, total, first error)."""
+    import numpy as np
+
+    from flyimg_amd import _lib as L
+    from flyimg_amd.runtime import Op
+    from flyimg_amd.synth import synth_rgb
+    from oracle import oracle as orc
+
+    no_apply = [Op(op.target_w, op.target_h, op.flags & ~L.FI_OP_SMARTCROP_APPLY, op.gravity, op.rotate,
+                   op.smartcrop_w, op.smartcrop_h) for op in ops]
+    outs, recs, rc = ctx.process_device_views(views, no_apply)
+    ok, err = 0, None
+    for i in idxs:
+        a, op = arr[i], ops[i]
+        try:
+            assert rc == 0 and recs[i].status == 0 and outs[i] is not None, f"re-run status {rc}/{recs[i].status}"
+            assert a.status == 0, f"status {a.status}"
+            p, W, H, _ = views[i]
+            src = synth_rgb(W, H, seeds[i])
+            ref = orc.im_convert(src, op.target_w, op.target_h, oracle_flags(op), rotate=op.rotate)
+            rz = outs[i]
+            assert rz.shape == ref.shape, (rz.shape, ref.shape)
+            d = int(np.abs(rz.astype(np.int16) - ref.astype(np.int16)).max())
+            assert d <= 1, f"max |gpu - oracle| = {d}"
+            out = ctx.d2h(dst_of(i), a.out_h * a.out_stride).reshape(a.out_h, a.out_stride)
+            out = out[:, : a.out_w * a.out_channels].reshape(a.out_h, a.out_w, a.out_channels)
+            out = out[:, :, 0] if a.out_channels == 1 else out
+            if op.flags & L.FI_OP_SMARTCROP:
+                rgb = rz if rz.ndim == 3 else np.repeat(rz[:, :, None], 3, axis=2)
+                t = orc.sc_crop(np.ascontiguousarray(rgb), op.smartcrop_w or 100, op.smartcrop_h or 100)["top_crop"]
+                want = (t["x"], t["y"], t["width"], t["height"])
+                got = (a.crop_x, a.crop_y, a.crop_w, a.crop_h)
+                assert got == want, (got, want)
+                if op.flags & L.FI_OP_SMARTCROP_APPLY:
+                    x, y, w, h = got
+                    ow, oh = min(w + x, rz.shape[1] - x), min(h + y, rz.shape[0] - y)
+                    assert np.array_equal(out, rz[y:y + oh, x:x + ow]), "applied crop differs"
+            else:
+                assert np.array_equal(out, rz), "timed output differs from the re-run"
+            ok += 1
+        except AssertionError as e:
+            err = err or f"image {i}: {e}"
+    return ok, len(idxs), err
