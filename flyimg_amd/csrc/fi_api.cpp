@@ -246,6 +246,7 @@ struct fi_ctx {
   std::map<const AxisTable *, int32_t> axis_wd_at;  // f64 weights (RGBA path) in heap_d
   std::map<const ScPlan *, ScTabs> sc_at;
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_at;
+  std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp2_at;  // importance - oi
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
   std::map<const VrV *, std::array<int32_t, 4>> vr_at;    // rows, bmeta, w128, frag
   std::map<const MfmaH *, std::array<int32_t, 6>> mh_at;  // wsum, frag, s0, lut, frag2, wsum2
@@ -445,6 +446,7 @@ static void heap_reset(fi_ctx *c) {
   c->axis_wd_at.clear();
   c->sc_at.clear();
   c->imp_at.clear();
+  c->imp2_at.clear();
   c->vv_at.clear();
   c->vr_at.clear();
   c->mh_at.clear();
@@ -656,6 +658,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
         e.second = std::max(e.second, ch.nin_y);
       }
       std::map<std::pair<uint64_t, uint64_t>, std::tuple<int32_t, int32_t, double>> tab_of;
+      std::map<std::pair<uint64_t, uint64_t>, std::pair<int32_t, double>> tab2_of;  // importance - oi
       for (auto &sz : sizes) {
         double fw, fh;
         memcpy(&fw, &sz.first.first, 8);
@@ -678,6 +681,20 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
           ip = c->imp_at.emplace(pk, std::make_pair(off, imax)).first;
         }
         tab_of[sz.first] = std::make_tuple(ip->second.first, nx, ip->second.second);
+        // the fast pass weighs inside pixels by fl(importance - oi): the outside
+        // ones then need no pass (k_sc_score2)
+        auto i2 = c->imp2_at.find(pk);
+        if (i2 == c->imp2_at.end()) {
+          double imax2 = 0;
+          const int32_t off = E.od();
+          for (double v : iit->second) {
+            const double w = v - E.params.outside_importance;
+            imax2 = std::max(imax2, std::fabs(w));
+            E.ad.push_back(w);
+          }
+          i2 = c->imp2_at.emplace(pk, std::make_pair(off, imax2)).first;
+        }
+        tab2_of[sz.first] = i2->second;
       }
       q.crop0 = (int32_t)L->crops.size();
       q.ncrops = (int32_t)P.crops.size();
@@ -695,6 +712,8 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
         dc.table = std::get<0>(t);
         dc.table_w = std::get<1>(t);
         dc.imax = std::get<2>(t);
+        dc.table2 = tab2_of[{dbits(ch.fw), dbits(ch.fh)}].first;
+        dc.imax2 = tab2_of[{dbits(ch.fw), dbits(ch.fh)}].second;
         dc.rx = ch.rx;
         dc.ry = ch.ry;
         dc.rw = ch.rw;

@@ -82,6 +82,9 @@ struct DevCrop {
   int32_t table_w;        // row pitch of the table
   int32_t rx, ry, rw, rh; // rescaled ints (crop() :184-190)
   double imax;            // max |importance| over the table (fast-pass error bound)
+  double imax2;           // max |importance - outside_importance| over the table2
+  int32_t table2;         // arena offset (double units): fl(importance - outside_importance), same layout
+  int32_t pad2;
 };
 
 struct ScDesc {
