@@ -213,6 +213,7 @@ struct fi_ctx {
   bool fast_rs = true;  // FI_FORCE_GENERIC=1: the generic two-pass resample (and smartcrop) kernels only
   bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
   int vr_max_classes = 8;  // batches with more vertical tables stay on k_rs_vm (FI_VR_MAX_CLASSES)
+  int res_align = 16;      // row pitch alignment of the resized image kept for smartcrop apply (FI_RES_ALIGN)
   int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
@@ -975,6 +976,7 @@ struct BatchPlan {
   int h_tile_pitch = 0;  // k_rs_h_tile: max staged row bytes over the mode-2 images
   int h_tile_taps = 0;   // k_rs_h_tile: max horizontal window over the mode-2 images
   std::vector<size_t> res_off;    // per image: resized buffer in the workspace (smartcrop apply)
+  std::vector<int64_t> res_stride;  // per image: the row pitch of out_of (out_stride, or padded in the workspace)
   std::vector<uint8_t *> out_of;  // per image: the final 8-bit output (dst, or the workspace +1-tagged)
   std::vector<MonoItem> mono;
   std::vector<ConvItem> conv_items;
@@ -1184,8 +1186,16 @@ static void plan_image(fi_ctx *c, Exec &E, BatchPlan &Bp, int i) {
   d.out_h = P.out_h;
   d.out_c = P.out_c;
   d.dst_stride = im.out_stride;
+  Bp.res_stride[i] = im.out_stride;
   if (apply) {
-    Bp.res_off[i] = E.work.take((size_t)need);
+    // the resized image stays in the workspace for smartcrop and the crop
+    // apply: rows padded to res_align bytes, so the readers' 16-byte loads
+    // are aligned (the -monochrome and convolution outputs keep out_stride)
+    if (!P.mono && !P.conv) {
+      const int64_t a = c->res_align;
+      Bp.res_stride[i] = d.dst_stride = (im.out_stride + a - 1) / a * a;
+    }
+    Bp.res_off[i] = E.work.take((size_t)(Bp.res_stride[i] * im.out_h));
     d.dst = (uint8_t *)(uintptr_t)(Bp.res_off[i] + 1);  // workspace, resolved later
   } else {
     d.dst = im.dst;
@@ -1233,7 +1243,7 @@ static void plan_image(fi_ctx *c, Exec &E, BatchPlan &Bp, int i) {
   if (smc) {
     ScItem it{};
     it.img = nullptr;  // the resized image: resolved with the workspace
-    it.stride = im.out_stride;
+    it.stride = Bp.res_stride[i];
     it.W = P.out_w;
     it.H = P.out_h;
     it.C = P.out_c;
@@ -1350,7 +1360,7 @@ static void resolve_workspace(Exec &E, BatchPlan &Bp, uint8_t *wb) {
     const ResizeDesc &d = Bp.rd[Bp.rd_of[i]];
     ApplyDesc a{};
     a.src = Bp.out_of[i];
-    a.src_stride = imgs[i].out_stride;
+    a.src_stride = Bp.res_stride[i];
     a.W = d.out_w;
     a.H = d.out_h;
     a.C = d.out_c;
@@ -2064,6 +2074,7 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async, std::shar
   Bp.rd_of.assign(n, -1);
   Bp.sc_of.assign(n, -1);
   Bp.res_off.assign(n, 0);
+  Bp.res_stride.assign(n, 0);
   Bp.out_of.assign(n, nullptr);
   for (int i = 0; i < n; i++) plan_image(c, E, Bp, i);
   const double t_images = now_ms();
@@ -2645,6 +2656,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_VR_MAX_CLASSES")) c->vr_max_classes = atoi(e);
+  if (const char *e = getenv("FI_RES_ALIGN")) c->res_align = std::max(1, atoi(e));
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   // (the smartcrop stage on a stream of its own beside the next batch's
   // resample was measured in round 2: the resample fills every CU, so the

@@ -386,6 +386,16 @@ constexpr int kFzRing = 80;  // a 64-row window at any 16-row block alignment
 #define FI_FZ_THREADS 512
 #endif
 constexpr int kFzThreads = FI_FZ_THREADS;  // 8 waves; two workgroups per CU (LDS)
+#ifndef FI_FZ_ABL
+#define FI_FZ_ABL 0
+#endif
+// profiling ablations (wrong maps): 1 no source loads, 2 no horizontal pass,
+// 4 no vertical pass, 8 no luma loop, 16 no maps loop
+constexpr int kFzAbl = FI_FZ_ABL;
+#ifndef FI_FZ_REV
+#define FI_FZ_REV 0
+#endif
+constexpr bool kFzRev = FI_FZ_REV;
 constexpr int kFzGather = 4;                // skin/saturation table reads in flight per thread
 // skin | saturation << 8 of every 24-bit colour (sc_skin_sat of the colour and
 // its luma): built once per parameter set, a gather replaces ~200 f64 VALU
@@ -412,7 +422,7 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
                                                         const int32_t *__restrict__ ai, const ScParamsDev P,
                                                         const uint16_t *__restrict__ skinsat) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  const ScDesc &D = descs[blockIdx.x];
+  const ScDesc &D = descs[kFzRev ? gridDim.x - 1 - blockIdx.x : blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int aw = D.aw, ah = D.ah, hrows = D.hrows, yoff = D.ybox_first;
   const int apitch = (aw * 3 + 15) & ~15, lpitch = (aw + 3) & ~3;
@@ -450,7 +460,10 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
         if (fast[u]) {
           const uint8_t *s = src + (int64_t)(r0 + rr + yoff) * sstride + 48 * g;
           const int remb = r0 + rr < hrows ? 3 * (sW - 16 * g) : 0;  // the group's bytes inside the row
-          if (remb >= 48) {
+          if (kFzAbl & 1) {  // profiling ablation: no source loads
+#pragma unroll
+            for (int k = 0; k < 3; k++) q[u][k] = u32x4a{(uint32_t)it, (uint32_t)r0, (uint32_t)k, (uint32_t)g};
+          } else if (remb >= 48) {
 #pragma unroll
             for (int k = 0; k < 3; k++) q[u][k] = *reinterpret_cast<const u32x4a *>(s + 16 * k);
           } else {
@@ -534,6 +547,7 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
     // fragments are loaded before the first block's MFMAs, so the second
     // block's load latency hides behind the first block's work
     constexpr int kW = kFzThreads / 64;
+    if (kFzAbl & 2) return;
 #pragma unroll 1
     for (int bp = wave; bp < nb; bp += 2 * kW) {
       i32x4 Bfs[2][2][3];
@@ -625,7 +639,7 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
     const uint8_t *pA = ring + ((k0 + rA) % kFzRing) * apitch + 8 * (lane & 1);
     const uint8_t *pB = ring + ((k0 + rA + 8) % kFzRing) * apitch + 8 * (lane & 1);
 #pragma unroll 1
-    for (int t = wave; t < nq; t += kFzThreads / 64) {
+    for (int t = wave; t < ((kFzAbl & 4) ? 0 : nq); t += kFzThreads / 64) {
       const i32x2 lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pA + 16 * t));
       const i32x2 hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pB + 16 * t));
       const i32x4 B = {lo.x, lo.y, hi.x, hi.y};
@@ -644,7 +658,7 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
     const int nr = pe - pa;
     int m = lm0, x = lx0;  // (m, x) of it, stepped by (stepy, stepx) without a division
 #pragma unroll 1
-    for (int it = tid; it < nr * aw; it += kFzThreads, m += stepy, x += stepx) {
+    for (int it = tid; it < ((kFzAbl & 8) ? 0 : nr * aw); it += kFzThreads, m += stepy, x += stepx) {
       if (x >= aw) {
         x -= aw;
         m++;
@@ -667,7 +681,7 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
     constexpr int kG = LUT ? kFzGather : 1;
     int yr_n = lm0, x_n = lx0;  // (row, column) of the next item
 #pragma unroll 1
-    for (int base = tid; base < nit; base += kG * kFzThreads) {
+    for (int base = tid; base < ((kFzAbl & 16) ? 0 : nit); base += kG * kFzThreads) {
       uint32_t sv[kG];
       int yrs[kG], xs[kG];
 #pragma unroll
