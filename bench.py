@@ -73,6 +73,11 @@ KERNEL_OF_PATH = {
     "path_generic_h": "k_rs_h_u8 + k_rs_v_final (two-pass)",
     "path_copy": "k_rs_copy",
 }
+# smartcrop prescale + maps kernel per image (counts kept by the library)
+SC_KERNEL_OF_PATH = {
+    "sc_path_fd": "k_sc_fd (prescale + maps, source rows by LDS-DMA)",
+    "sc_path_fz": "k_sc_fz (prescale + maps, register-staged source rows)",
+}
 
 
 def log(*a):
@@ -278,6 +283,7 @@ def main():
                                       "host_plan_blob", "host_launch", "host_wait", "host_total")}
     # images per resample kernel over the timed steps (counts kept by the library)
     paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in KERNEL_OF_PATH}
+    sc_paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in SC_KERNEL_OF_PATH}
     ablation = ctx.stats("vr_ablation")[1]  # FI_VR_VARIANT profiling launches (wrong pixels)
     last = arrs[(args.warmup + args.steps - 1) % 2]
     allv = comm.allgather_obj({"elapsed": el, "stats": stats,
@@ -340,6 +346,7 @@ def main():
                 "avg_launch_ms": round(rs_ms / max(rs_n, 1), 4),
             },
             "stages_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()},
+            "smartcrop_kernels": " + ".join(f"{SC_KERNEL_OF_PATH[p]} ({n} images)" for p, n in sc_paths.items() if n),
             "exact_rescored_crops_per_step": allv[0]["ncand"],
             "failed_images": sum(v["bad"] for v in allv),
             "verified": (f"{sum(v['ok'] for v in allv_v)}/{sum(v['tot'] for v in allv_v)} images of the last "

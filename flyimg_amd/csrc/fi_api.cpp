@@ -51,6 +51,8 @@ int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds,
                  const ScParamsDev &P);
 int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
                  const uint16_t *skinsat);
+int launch_sc_fd(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
+                 const uint16_t *skinsat);
 int launch_sc_skinsat(hipStream_t s, uint16_t *table, const ScParamsDev &P);
 int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c);
 int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *len, int n, uint8_t *const *dst,
@@ -216,6 +218,7 @@ struct fi_ctx {
   int res_align = 16;      // row pitch alignment of the resized image kept for smartcrop apply (FI_RES_ALIGN)
   int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
+  bool sc_fd = true;        // FI_SC_FD=0: k_sc_fz instead of its LDS-DMA form k_sc_fd
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
   DevBuf jpeg[3];           // GPU JPEG decode: upload (compressed data + tables), -, coefficients + planes
   void *jpeg_host = nullptr;  // its pinned staging
@@ -417,6 +420,7 @@ struct ScItem {       // one smartcrop job
   int tw, th;
   int result;          // index into results
   fi_smartcrop_options opt;
+  bool padded = false; // every row readable to fd_rp(W) bytes (library-owned buffers)
 };
 
 struct Exec {
@@ -761,6 +765,11 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.hmS0 = T.hmS0;
     d.vq = prep && P.vq_ok ? 1 : 0;
     d.fz = d.vq && P.fz_ok && c->sc_fz ? 1 : 0;
+    d.fd = d.fz && c->sc_fd && it.C == 3 && it.stride % 16 == 0 && (it.padded || (it.W * 3) % 16 == 0) &&
+                   P.hm_nb <= kFdCWaves &&
+                   fd_lds(it.W, P.hm_pitch, P.aw, P.ah) <= kFdMaxLds
+               ? 1
+               : 0;
     d.vqA = T.vqA;
     d.vqC = T.vqC;
     d.vqK0 = T.vqK0;
@@ -817,8 +826,8 @@ struct ScLaunches {
   Launch red, hp, vp, maps;        // generic (fi_kernels.hip)
   size_t hm_off = 0, vq_off = 0, vm_off = 0;   // k_sc_hmfma / k_sc_vq / k_sc_vmaps
   int nhm = 0, hm_chunks = 0, hm_lds = 0, nvm = 0, v_chunks = 0, v_lds = 0;
-  size_t fz_off = 0;  // k_sc_fz
-  int nfz = 0, fz_lds = 0;
+  size_t fz_off = 0, fd_off = 0;  // k_sc_fz, k_sc_fd
+  int nfz = 0, fz_lds = 0, nfd = 0, fd_lds = 0;
   int nvq = 0, vq_chunks = 0, vq_lds = 0;
   size_t sl_off = 0, sg_off = 0;   // k_sc_score2 with maps in LDS / global
   int nsl = 0, nsg = 0, sl_px = 0;
@@ -827,13 +836,16 @@ struct ScLaunches {
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> hm, sl, sg, vq, vm, fz;
+  std::vector<ScDesc> hm, sl, sg, vq, vm, fz, fd;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
     const ScDesc &d = SL.descs[k];
     const ScPlan &P = *SL.plans[k];
     if (d.red) sred.push_back((int)k);
-    if (d.fz) {
+    if (d.fz && d.fd && ((uintptr_t)d.img & 15) == 0) {
+      fd.push_back(d);
+      X->fd_lds = std::max(X->fd_lds, fd_lds(d.W, d.hm_pitch, d.aw, d.ah));
+    } else if (d.fz) {
       fz.push_back(d);
       X->fz_lds = std::max(X->fz_lds, P.fz_lds);
     } else if (d.prep) {
@@ -873,6 +885,10 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->nvq = (int)vq.size();
   X->fz_off = B.addv(fz);
   X->nfz = (int)fz.size();
+  X->fd_off = B.addv(fd);
+  X->nfd = (int)fd.size();
+  c->stats["sc_path_fd"].launches += X->nfd;  // images per smartcrop prescale kernel (fi_kernel_stats)
+  c->stats["sc_path_fz"].launches += X->nfz;
   X->sl_off = B.addv(sl);
   X->nsl = (int)sl.size();
   X->sg_off = B.addv(sg);
@@ -887,7 +903,7 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
   // on the stream that reads it, so batches queued before a parameter change
   // have read the old table first
   const uint16_t *skinsat = nullptr;
-  if (X.nfz > 0) {
+  if (X.nfz > 0 || X.nfd > 0) {
     const std::string key(reinterpret_cast<const char *>(&PD), offsetof(ScParamsDev, pad));
     if (!c->skinsat.p || c->skinsat_key != key) {
       const int rc = ensure(c, &c->skinsat, (size_t)2 << 24);
@@ -904,8 +920,10 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
     if (launch_sc_h(st, (const ScDesc *)(ab + X.hm_off), X.nhm, X.hm_chunks, X.hm_lds, ai) != 0 ||
         launch_sc_vq(st, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0 ||
         launch_sc_v(st, (const ScDesc *)(ab + X.vm_off), X.nvm, X.v_chunks, X.v_lds, ai, PD) != 0 ||
-        launch_sc_fz(st, (const ScDesc *)(ab + X.fz_off), X.nfz, X.fz_lds, ai, PD, skinsat) != 0)
-      return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d)", X.hm_lds, X.vq_lds, X.fz_lds);
+        launch_sc_fz(st, (const ScDesc *)(ab + X.fz_off), X.nfz, X.fz_lds, ai, PD, skinsat) != 0 ||
+        launch_sc_fd(st, (const ScDesc *)(ab + X.fd_off), X.nfd, X.fd_lds, ai, PD, skinsat) != 0)
+      return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d/%d)", X.hm_lds, X.vq_lds, X.fz_lds,
+                     X.fd_lds);
     if (X.hp.tiles)
       hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, st, desc(X.hp), pre(X.hp), X.hp.n, ai);
     if (X.vp.tiles)
@@ -1250,6 +1268,7 @@ static void plan_image(fi_ctx *c, Exec &E, BatchPlan &Bp, int i) {
     it.tw = im.smartcrop_w > 0 ? im.smartcrop_w : 100;
     it.th = im.smartcrop_h > 0 ? im.smartcrop_h : 100;
     it.result = (int)Bp.sitems.size();
+    it.padded = apply && Bp.res_stride[i] % 16 == 0;  // workspace rows at a 16-B rounded pitch
     fi_smartcrop_default_options(&it.opt);
     Bp.sc_of[i] = (int)Bp.sitems.size();
     Bp.sitems.push_back(it);
@@ -2251,6 +2270,7 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   items[0].th = th;
   items[0].result = 0;
   items[0].opt = opt;
+  items[0].padded = true;  // the caller (fi_smartcrop_ex) staged it at a 16-B rounded pitch, + 256 B
   ScLaunchData SL;
   std::vector<int> st(1, FI_OK);
   std::vector<std::string> errs(1);
@@ -2471,7 +2491,8 @@ int fi_jpeg_decode_device(fi_ctx *c, const uint8_t *const *data, const size_t *l
                      status[i] == FI_EUNSUPPORTED ? "JPEG stream the GPU decoder does not handle" : "malformed JPEG");
   return FI_OK;
 }
-// Test hook: the skin / saturation table of k_sc_fz<true> for `params`
+// Test hook: the skin / saturation table of k_sc_fz<true> / k_sc_fd for `params`,
+// returned in r-major colour order (the device table is in sc_colour_key order)
 int fi_debug_skinsat(fi_ctx *c, const fi_smartcrop_params *params, uint16_t *out) {
   if (!c || !out) return set_err(FI_EINVAL, "bad arguments");
   fi_smartcrop_params p;
@@ -2487,8 +2508,10 @@ int fi_debug_skinsat(fi_ctx *c, const fi_smartcrop_params *params, uint16_t *out
   launch_sc_skinsat(c->stream, (uint16_t *)c->skinsat.p, PD);
   c->skinsat_key.clear();  // built on c->stream, not the smartcrop stream: rebuilt before the next use
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out, c->skinsat.p, (size_t)2 << 24, hipMemcpyDeviceToHost, c->stream));
+  std::vector<uint16_t> z((size_t)1 << 24);
+  HIP_TRY(hipMemcpyAsync(z.data(), c->skinsat.p, (size_t)2 << 24, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  for (uint32_t k = 0; k < (1u << 24); k++) out[k] = z[sc_colour_key(k >> 16, (k >> 8) & 255, k & 255)];  // r-major
   return FI_OK;
 }
 // Test hook: the -monochrome kernels (fi_mono.hip) on a caller-supplied Q16
@@ -2655,6 +2678,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_FORCE_GENERIC")) c->fast_rs = c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
+  if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';
   if (const char *e = getenv("FI_VR_MAX_CLASSES")) c->vr_max_classes = atoi(e);
   if (const char *e = getenv("FI_RES_ALIGN")) c->res_align = std::max(1, atoi(e));
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;

@@ -105,6 +105,7 @@ struct ScDesc {
   int32_t hmB, hmC, hmS0;  // arena offsets (int32 units; hmB 16-B aligned)
   int32_t vq;              // 1: vertical pass + maps by k_sc_vq (tables below)
   int32_t fz;              // 1: both passes + maps by k_sc_fz (hm + vq tables, one workgroup per image)
+  int32_t fd;              // 1 (with fz): rows readable to fd_rp(W) bytes, so k_sc_fd may take it
   int32_t vqA, vqC, vqK0;  // arena offsets (int32 units; vqA 16-B aligned)
   uint8_t *red;        // reduce scratch rw*rh*3
   uint8_t *hbuf;       // H-pass scratch aw*hrows*3
@@ -128,6 +129,42 @@ constexpr int kPrepMaxLds = 64 * 1024;
 // kFzRing (80) H-stage rows + max(3 source planes of 16 rows, 16 prescaled rows
 // + luma); <= 80 KB keeps two workgroups per CU
 constexpr int kFzMaxLds = 80 * 1024;
+// k_sc_fd (fi_smartcrop.hip): k_sc_fz's passes with the source rows streamed
+// by LDS-DMA, one 16-wave workgroup per CU.  LDS: kFdSlots raw blocks of 16
+// source rows (row pitch fd_rp = 16-B rounded W * 3; a slot rounded up to the
+// DMA's 1 KB steps), a tail that the horizontal pass's last window may read
+// past the last slot (zero weights there), then the kFzRing H-stage rows, 16
+// prescaled rows and their luma.
+// k_sc_skinsat's table of all 2^24 colours is laid out in Z-order of the
+// channel bits (r2 g2 b2 r1 g1 b1 ...): a 128-byte line holds a 4x4x4 colour
+// cube, so the maps pass's gathers for a noisy or smooth neighbourhood of
+// colours touch ~1/4 of the lines an r-major table does
+__host__ __device__ inline uint32_t sc_spread3(uint32_t x) {  // bit i -> bit 3 i (8 bits)
+  x = (x | (x << 8)) & 0x0000F00Fu;
+  x = (x | (x << 4)) & 0x000C30C3u;
+  return (x | (x << 2)) & 0x00249249u;
+}
+__host__ __device__ inline uint32_t sc_colour_key(uint32_t r, uint32_t g, uint32_t b) {
+  return (sc_spread3(r) << 2) | (sc_spread3(g) << 1) | sc_spread3(b);
+}
+constexpr int kFdSlots = 3;
+constexpr int kFdCWaves = 14;  // compute waves (one 16-px column block each: aw <= 224); 14, 15 load
+constexpr int kFdMaxLds = 160 * 1024;
+__host__ __device__ inline int fd_rp(int W) { return (W * 3 + 15) & ~15; }
+__host__ __device__ inline int fd_slot_bytes(int W) { return (16 * fd_rp(W) + 1023) & ~1023; }
+__host__ __device__ inline int fd_ring_off(int W, int PP) {
+  const int tail = 3 * PP - fd_rp(W);
+  return kFdSlots * fd_slot_bytes(W) + (tail > 0 ? (tail + 15) & ~15 : 0);
+}
+// then the vertical pass's A fragments of every analysed-row chunk (3 limbs x
+// 64 lanes x 16 B each) and its per-row bias (int32)
+__host__ __device__ inline int fd_tab_off(int W, int PP, int aw) {
+  const int apitch = (aw * 3 + 15) & ~15, lpitch = (aw + 3) & ~3;
+  return fd_ring_off(W, PP) + 80 * apitch + 16 * apitch + 16 * lpitch;
+}
+__host__ __device__ inline int fd_lds(int W, int PP, int aw, int ah) {
+  return fd_tab_off(W, PP, aw) + (ah + kVqRows - 1) / kVqRows * 3072 + 4 * ah;
+}
 // k_sc_score2: maps resident in LDS when aw*ah*4 <= this; crops whose totals /
 // bounds / candidate list stay in LDS (more: the image's CropScore slots).
 constexpr int kScoreLdsMaps = 112 * 1024;

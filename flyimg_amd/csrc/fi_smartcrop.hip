@@ -398,13 +398,15 @@ constexpr int kFzAbl = FI_FZ_ABL;
 constexpr bool kFzRev = FI_FZ_REV;
 constexpr int kFzGather = 4;                // skin/saturation table reads in flight per thread
 // skin | saturation << 8 of every 24-bit colour (sc_skin_sat of the colour and
-// its luma): built once per parameter set, a gather replaces ~200 f64 VALU
+// its luma) at sc_colour_key(r, g, b): built once per parameter set, a gather replaces ~200 f64 VALU
 // instructions per analysed pixel in k_sc_fz<true>; bit-identical by construction.
 __global__ __launch_bounds__(256) void k_sc_skinsat(uint16_t *__restrict__ t, const ScParamsDev P) {
   const uint32_t c = blockIdx.x * 256u + threadIdx.x;  // (r << 16) | (g << 8) | b
   const uint32_t r = c >> 16, g = (c >> 8) & 255u, b = c & 255u;
-  const uint32_t v = sc_skin_sat(r, g, b, sc_luma(r, g, b), P);
-  t[c] = (uint16_t)((v & 255u) | ((v >> 16) << 8));
+  const uint32_t L = sc_luma(r, g, b);
+  uint32_t v;
+  if (!sc_skin_sat_est(sc_fast_params(P), r, g, b, L, v)) v = sc_skin_sat(r, g, b, L, P);
+  t[sc_colour_key(r, g, b)] = (uint16_t)((v & 255u) | ((v >> 16) << 8));
 }
 
 // n / d for 0 <= n < 2^22, 0 < d < 2^12 from a float reciprocal and one
@@ -702,7 +704,7 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
           sv[u] = 0;
           if (it < nit) {
             const uint8_t *qq = prer + (y0 + yrs[u] - pa) * apitch + 3 * xs[u];
-            sv[u] = skinsat[((uint32_t)qq[0] << 16) | ((uint32_t)qq[1] << 8) | qq[2]];
+            sv[u] = skinsat[sc_colour_key(qq[0], qq[1], qq[2])];
           }
         }
       }
@@ -731,9 +733,410 @@ __global__ __launch_bounds__(kFzThreads, 4) void k_sc_fz(const ScDesc *__restric
   }
 }
 
+// ---- k_sc_fd: k_sc_fz's passes (same tables, same arithmetic, bit-identical
+// maps) with the source stream decoupled from the compute.  One 16-wave
+// workgroup per CU: waves 0-13 run the horizontal pass, the vertical pass,
+// luma and maps; waves 14-15 copy 16-row source blocks by LDS-DMA
+// (global_load_lds_dwordx4, no VGPRs, no VALU) into kFdSlots raw slots, two
+// blocks ahead of the horizontal pass, and wait for each with an exact vmcnt.
+// k_sc_fz has one block of loads in flight per workgroup only while it stages
+// (ablation: 0.24 of its 0.55 ms per cfg2 step are that load latency); here
+// they stay in flight through the MFMA and maps phases.  The horizontal pass
+// reads its A fragments straight from the raw interleaved rows (three 8-byte
+// LDS reads per 8 pixels, v_perm into the three channels), so there is no
+// staging pass and no plane buffer.  One barrier per source block, plus three
+// per analysed-row chunk.  Needs 3-channel sources with 16-B aligned rows
+// readable to fd_rp(W) bytes (the host's ScDesc.fd).
+constexpr int kFdThreads = 1024;
+constexpr int kFdC = kFdCWaves * 64;
+#ifndef FI_FD_ABL
+#define FI_FD_ABL 0
+#endif
+// profiling ablations (wrong maps): 1 no source DMA, 2 no horizontal pass,
+// 4 no vertical pass, 8 no luma loop, 16 no maps loop, 32 no table reads,
+// 64 no map stores
+constexpr int kFdAbl = FI_FD_ABL;
+// skin / saturation: 1 = every pixel from k_sc_skinsat's table (k_sc_fz's
+// way), 0 = sc_skin_sat_est per pixel and the table only for what it leaves
+// open: one workgroup per CU has no second workgroup to cover the gathers'
+// latency, and the L2 serves divergent gathers one line per request
+#ifndef FI_FD_LUT
+#define FI_FD_LUT 0
+#endif
+constexpr bool kFdLut = FI_FD_LUT;
+__device__ __forceinline__ void fd_dma16(uint32_t m0, const uint8_t *sbase, uint32_t voff) {
+  // lane i's 16 bytes at sbase + voff land at LDS m0 + 16 i (m0, sbase uniform)
+  unsigned keep;
+  const uint64_t sb = (uint64_t)(uintptr_t)sbase;
+  sbase = reinterpret_cast<const uint8_t *>((uintptr_t)(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sb >> 32)) << 32) |
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sb)));
+  m0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)m0);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(m0)
+      : "memory");
+}
+// s_waitcnt vmcnt(n) for n <= 15 (larger n wait for 15: conservative)
+__device__ __forceinline__ void fd_wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+}
+__device__ __forceinline__ uint32_t fd_ch(int c, uint32_t a0, uint32_t a1, uint32_t a2) {
+  // channel c of 4 interleaved RGB pixels (12 bytes a0 a1 a2), as p - 128
+  const uint32_t s1 = c == 0 ? 0x00060300u : c == 1 ? 0x00070401u : 0x00000502u;
+  const uint32_t s2 = c == 0 ? 0x05020100u : c == 1 ? 0x06020100u : 0x07040100u;
+  return __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, s1), s2) ^ 0x80808080u;
+}
+
+// workgroup barrier without the vmcnt(0) that __syncthreads' fence adds: the
+// loader waves' DMAs for the next blocks stay in flight across it (LDS
+// accesses are complete at lgkmcnt(0); nothing here reads a global store of
+// this kernel)
+__device__ __forceinline__ void fd_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__global__ __launch_bounds__(kFdThreads) void k_sc_fd(const ScDesc *__restrict__ descs,
+                                                      const int32_t *__restrict__ ai, const ScParamsDev P,
+                                                      const uint16_t *__restrict__ skinsat) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+  const ScDesc &D = descs[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool loader = wave >= kFdCWaves;
+  const int aw = D.aw, ah = D.ah, hrows = D.hrows, yoff = D.ybox_first;
+  const int apitch = (aw * 3 + 15) & ~15, lpitch = (aw + 3) & ~3;
+  const int PP = D.hm_pitch, KS = D.hm_ks, nb = D.hm_nb;
+  const int RP = fd_rp(D.W), slotB = fd_slot_bytes(D.W);
+  const int64_t sstride = D.stride;
+  uint8_t *raw = lds8;                                         // [kFdSlots][16][RP] source rows
+  uint8_t *ring = lds8 + fd_ring_off(D.W, PP);                 // [kFzRing][apitch] H-stage rows, p - 128
+  uint8_t *prer = ring + kFzRing * apitch, *lum = prer + 16 * apitch;  // [16][apitch], [16][lpitch]
+  uint8_t *abuf = lds8 + fd_tab_off(D.W, PP, aw);             // [chunks][3][64] i32x4 vertical A fragments
+  const int chunks = (ah + kVqRows - 1) / kVqRows;
+  int32_t *cbuf = reinterpret_cast<int32_t *>(abuf + chunks * 3072);  // [ah] vertical bias
+  const int nblk = (min(ai[D.vqK0 + chunks - 1] + 64, hrows) + 15) >> 4;  // blocks the last chunk needs
+  // ---- loader side: block blk -> slot blk % kFdSlots, DMA steps i = lw, lw + 2, ...
+  const int ninstr = slotB >> 10, lw = wave - kFdCWaves;
+  const int cnt = (ninstr - lw + 1) >> 1;  // this loader wave's DMAs per block
+  const int rpc = RP >> 4;                 // 16-byte chunks per row
+  const float rcp_rpc = 1.0f / (float)rpc;
+  const uint32_t raw_m0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)raw;
+  const uint32_t ab_m0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)abuf;
+  auto issue = [&](int blk) {
+    if (blk >= nblk || (kFdAbl & 1)) return;
+    const int r0 = blk << 4;
+    const uint8_t *sb = D.img + (int64_t)(r0 + yoff) * sstride;
+    const int last = hrows - 1 - r0;  // rows past the analysed rows repeat the last one (never used)
+#pragma unroll 1
+    for (int i = lw; i < ninstr; i += 2) {
+      const int j = 64 * i + lane;
+      int row = fz_div(j, rpc, rcp_rpc);
+      const int col = j - row * rpc;
+      row = min(row, min(15, last));  // lanes past the block's 16 rows land in the slot's padding
+      fd_dma16(raw_m0 + (uint32_t)((blk % kFdSlots) * slotB + 1024 * i), sb,
+               (uint32_t)(row * sstride + 16 * col));
+    }
+  };
+  // ---- compute side: wave w owns column block w (the host admits images of
+  // <= kFdCWaves blocks: aw <= 224; cfg2: 13); its B fragments stay in
+  // registers for the whole image
+  const int32_t *hmS0 = ai + D.hmS0, *hmC = ai + D.hmC;
+  const i32x4 *hmB = reinterpret_cast<const i32x4 *>(ai + D.hmB);
+  const int k0l = mfma_i8_k(lane, 0), k8l = mfma_i8_k(lane, 8);
+  auto load_b = [&](int b, i32x4 (&Bf)[2][3], int &s0, int32_t &cx) {
+    s0 = hmS0[b];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+      for (int q = 0; q < 3; q++) Bf[t][q] = t < KS ? hmB[((b * KS + t) * 3 + q) * 64 + lane] : i32x4{0, 0, 0, 0};
+    const int x = 16 * b + (lane & 15);
+    cx = x < aw ? hmC[x] : 0;
+  };
+  i32x4 Bh[2][3];
+  int s0h = 0;
+  int32_t cxh = 0;
+  if (!loader && wave < nb) load_b(wave, Bh, s0h, cxh);
+  // the slot's 16 rows x column block b -> H-stage rows r0 .. r0 + 15
+  auto hpass_block = [&](int r0, const uint8_t *slot, int b, const i32x4 (&Bf)[2][3], int s0, int32_t cx) {
+    const int x = 16 * b + (lane & 15);
+    i32x4 acc[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+      for (int q = 0; q < 3; q++) acc[c][q] = i32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      if (t < KS) {
+        const uint8_t *rp = slot + (lane & 15) * RP + 3 * (s0 + 64 * t);
+        const i32x2 *p0 = reinterpret_cast<const i32x2 *>(rp + 3 * k0l);
+        const i32x2 *p1 = reinterpret_cast<const i32x2 *>(rp + 3 * k8l);
+        const i32x2 u0 = p0[0], u1 = p0[1], u2 = p0[2], v0 = p1[0], v1 = p1[1], v2 = p1[2];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+          const i32x4 a = {(int32_t)fd_ch(c, u0.x, u0.y, u1.x), (int32_t)fd_ch(c, u1.y, u2.x, u2.y),
+                           (int32_t)fd_ch(c, v0.x, v0.y, v1.x), (int32_t)fd_ch(c, v1.y, v2.x, v2.y)};
+#pragma unroll
+          for (int q = 0; q < 3; q++) acc[c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, Bf[t][q], acc[c][q], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int row = r0 + 4 * (lane >> 4) + i;
+      if (x < aw && row < hrows) {
+        uint8_t *dst = ring + (row % kFzRing) * apitch + 3 * x;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+          const uint32_t v = (uint32_t)acc[c][0][i] + ((uint32_t)acc[c][1][i] << 8) + ((uint32_t)acc[c][2][i] << 16) +
+                             (uint32_t)cx;
+          dst[c] = (uint8_t)(pil_clip8((int32_t)v) ^ 0x80u);
+        }
+      }
+    }
+  };
+  auto hpass = [&](int r0, const uint8_t *slot) {
+    if (wave < nb) hpass_block(r0, slot, wave, Bh, s0h, cxh);
+  };
+  const int rA = 16 * (lane >> 4) + ((lane & 15) >> 1);
+  const int nq = apitch >> 4, nbytes = 3 * aw;
+  const int stepy = kFdC / aw, stepx = kFdC - stepy * aw;
+  const int lm0 = tid / aw, lx0 = tid - lm0 * aw;
+  const ScFast F = sc_fast_params(P);
+  const int ng4 = (aw + 3) >> 2;  // luma: 4-pixel groups per row
+  const float rcp_ng4 = 1.0f / (float)ng4;
+  // ---- prologue: every chunk's vertical A fragments, source blocks 0 and 1
+  // in flight; the vertical bias into LDS; block 0 and the fragments landed
+  if (loader) {
+    const uint8_t *afrag = reinterpret_cast<const uint8_t *>(ai + D.vqA);
+#pragma unroll 1
+    for (int k = lw; k < 3 * chunks; k += 2) fd_dma16(ab_m0 + 1024 * k, afrag, (uint32_t)(1024 * k + 16 * lane));
+    issue(0);
+    issue(1);
+    fd_wait_vm(1 < nblk ? cnt : 0);
+  } else {
+#pragma unroll 1
+    for (int i = tid; i < ah; i += kFdC) cbuf[i] = ai[D.vqC + i];
+  }
+  fd_barrier();
+  int blk = 0;  // next block for the horizontal pass (in slot blk % kFdSlots)
+#pragma unroll 1
+  for (int c = 0; c < chunks; c++) {
+    const int k0 = ai[D.vqK0 + c];
+    const int need = min(k0 + 64, hrows);
+#pragma unroll 1
+    while (16 * blk < need) {
+      if (loader) {
+        issue(blk + 2);                        // into the slot block blk - 1 left
+        fd_wait_vm(blk + 2 < nblk ? cnt : 0);  // block blk + 1 landed
+      } else if (!(kFdAbl & 2)) {
+        hpass(16 * blk, raw + (blk % kFdSlots) * slotB);
+      }
+      fd_barrier();
+      blk++;
+    }
+    // the chunk's window is in the ring (and the last chunk's maps are done
+    // with prer / lum: a barrier of their own when no block ran in between)
+    fd_barrier();
+    const int y0 = kVqRows * c, y1 = min(y0 + kVqRows, ah), pa = max(0, y0 - 1), pe = min(ah, pa + 16);
+    if (!loader) {
+      const i32x4 *af = reinterpret_cast<const i32x4 *>(abuf + c * 3072);
+      const i32x4 A0 = af[lane], A1 = af[64 + lane], A2 = af[128 + lane];
+      int32_t cy[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) cy[i] = cbuf[min(pa + 4 * (lane >> 4) + i, ah - 1)];
+      const uint8_t *pA = ring + ((k0 + rA) % kFzRing) * apitch + 8 * (lane & 1);
+      const uint8_t *pB = ring + ((k0 + rA + 8) % kFzRing) * apitch + 8 * (lane & 1);
+#pragma unroll 1
+      for (int t = wave; t < ((kFdAbl & 4) ? 0 : nq); t += kFdCWaves) {
+        const i32x2 lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pA + 16 * t));
+        const i32x2 hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pB + 16 * t));
+        const i32x4 B = {lo.x, lo.y, hi.x, hi.y};
+        const i32x4 d2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const i32x4 d1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, B, d2 << 8, 0, 0, 0);
+        const i32x4 d0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const int col = 16 * t + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int m = 4 * (lane >> 4) + i;
+          const int32_t sv = (int32_t)((uint32_t)d0[i] + ((uint32_t)d1[i] << 8) + (uint32_t)cy[i]);
+          if (col < nbytes && pa + m < pe) prer[m * apitch + col] = pil_clip8(sv);
+        }
+      }
+    }
+    fd_barrier();
+    // maps items (analysed rows y0 .. y1 - 1): the first kFzGather skin /
+    // saturation table reads per thread go out before the luma pass, so their
+    // latency overlaps it and its barrier
+    const int nit = (y1 - y0) * aw;
+    int yr_n = lm0, x_n = lx0;  // (row, column) of the thread's next item
+    uint32_t sv[kFzGather];
+    // the kFzGather items of a step: (row, column) from the walk; walk() is
+    // run twice per step (for the table reads, then for the maps) so only the
+    // reads' results stay live across the luma pass
+    auto walk = [&](int (&yrs)[kFzGather], int (&xs)[kFzGather]) {
+#pragma unroll
+      for (int u = 0; u < kFzGather; u++) {
+        if (x_n >= aw) {
+          x_n -= aw;
+          yr_n++;
+        }
+        yrs[u] = yr_n;
+        xs[u] = x_n;
+        yr_n += stepy;
+        x_n += stepx;
+      }
+    };
+    auto gather = [&](int base) {
+      int yrs[kFzGather], xs[kFzGather];
+      walk(yrs, xs);
+#pragma unroll
+      for (int u = 0; u < kFzGather; u++) {
+        const int it = base + u * kFdC;
+        sv[u] = 0;
+        if (it < nit) {
+          const uint8_t *qq = prer + (y0 + yrs[u] - pa) * apitch + 3 * xs[u];
+          sv[u] = (kFdAbl & 32) ? qq[0] * 0x101u : skinsat[sc_colour_key(qq[0], qq[1], qq[2])];
+        }
+      }
+    };
+    const int nr = pe - pa;
+    if (!loader) {
+      if (kFdLut && !(kFdAbl & 16)) gather(tid);
+      // luma of the prescaled rows pa .. pe - 1, four pixels per item
+#pragma unroll 1
+      for (int it = tid; it < ((kFdAbl & 8) ? 0 : nr * ng4); it += kFdC) {
+        const int m = fz_div(it, ng4, rcp_ng4), g = it - m * ng4;
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(prer + m * apitch + 12 * g);
+        const uint32_t a0 = q[0], a1 = q[1], a2 = q[2];
+        const uint32_t R = fd_ch(0, a0, a1, a2) ^ 0x80808080u, G = fd_ch(1, a0, a1, a2) ^ 0x80808080u,
+                       B = fd_ch(2, a0, a1, a2) ^ 0x80808080u;
+        uint32_t l4 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          l4 |= sc_luma((R >> (8 * j)) & 255u, (G >> (8 * j)) & 255u, (B >> (8 * j)) & 255u) << (8 * j);
+        *reinterpret_cast<uint32_t *>(lum + m * lpitch + 4 * g) = l4;
+        const int y = pa + m;
+        if (D.pre && y >= y0 && y < y1) {
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int x = 4 * g + j;
+            if (x < aw) {
+              uint8_t *o = D.pre + ((int64_t)y * aw + x) * 3;
+              o[0] = (uint8_t)(R >> (8 * j));
+              o[1] = (uint8_t)(G >> (8 * j));
+              o[2] = (uint8_t)(B >> (8 * j));
+            }
+          }
+        }
+      }
+    }
+    fd_barrier();
+    if (!loader && !kFdLut) {
+      // kFzGather items per step: skin / saturation by sc_skin_sat_est, the
+      // table read only for the items it leaves open (skin candidates,
+      // saturation bytes at an integer boundary), all in flight together
+      int yr_w = lm0, x_w = lx0;
+#pragma unroll 1
+      for (int base = tid; base < ((kFdAbl & 16) ? 0 : nit); base += kFzGather * kFdC) {
+        uint32_t stv[kFzGather];
+        int yrs[kFzGather], xs[kFzGather];
+#pragma unroll
+        for (int u = 0; u < kFzGather; u++) {
+          if (x_w >= aw) {
+            x_w -= aw;
+            yr_w++;
+          }
+          yrs[u] = yr_w;
+          xs[u] = x_w;
+          yr_w += stepy;
+          x_w += stepx;
+          stv[u] = 0;
+          if (base + u * kFdC < nit) {
+            const int m = y0 + yrs[u] - pa;
+            const uint8_t *qq = prer + m * apitch + 3 * xs[u];
+            const uint32_t r = qq[0], g = qq[1], b = qq[2];
+            if (!sc_skin_sat_est(F, r, g, b, lum[m * lpitch + xs[u]], stv[u])) {
+              const uint32_t t = skinsat[sc_colour_key(r, g, b)];
+              stv[u] = (t & 255u) | ((t >> 8) << 16);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kFzGather; u++) {
+          const int it = base + u * kFdC;
+          if (it >= nit) break;
+          const int yr = yrs[u], x = xs[u], y = y0 + yr, m = y - pa;
+          const uint8_t *lrow = lum + m * lpitch;
+          const uint32_t L = lrow[x];
+          uint32_t E = L;
+          if (aw >= 3 && ah >= 3 && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
+            const int v = 4 * (int)L - (int)lrow[x - lpitch] - (int)lrow[x + lpitch] - (int)lrow[x - 1] - (int)lrow[x + 1] + 1;
+            E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
+          }
+          if (!(kFdAbl & 64)) D.maps[(int64_t)y * aw + x] = stv[u] | (E << 8);
+        }
+      }
+    }
+    if (!loader && kFdLut) {
+      yr_n = lm0;
+      x_n = lx0;
+#pragma unroll 1
+      for (int base = tid; base < ((kFdAbl & 16) ? 0 : nit); base += kFzGather * kFdC) {
+        if (base != tid) {
+          const int ys = yr_n, xs0 = x_n;
+          gather(base);
+          yr_n = ys;
+          x_n = xs0;
+        }
+        int yrs[kFzGather], xs[kFzGather];
+        walk(yrs, xs);
+#pragma unroll
+        for (int u = 0; u < kFzGather; u++) {
+          const int it = base + u * kFdC;
+          if (it >= nit) break;
+          const int yr = yrs[u], x = xs[u], y = y0 + yr, m = y - pa;
+          const uint8_t *lrow = lum + m * lpitch;
+          const uint32_t L = lrow[x];
+          uint32_t E = L;
+          if (aw >= 3 && ah >= 3 && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
+            const int v = 4 * (int)L - (int)lrow[x - lpitch] - (int)lrow[x + lpitch] - (int)lrow[x - 1] - (int)lrow[x + 1] + 1;
+            E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
+          }
+          if (!(kFdAbl & 64)) D.maps[(int64_t)y * aw + x] = ((sv[u] & 255u) | ((sv[u] >> 8) << 16)) | (E << 8);
+        }
+      }
+    }
+  }
+  if (loader) fd_wait_vm(0);  // every DMA landed before the workgroup retires
+}
+
 // ---------------------------------------------------------------------------
 constexpr int kScoreThreads = 1024;
 constexpr int kScoreWaves = kScoreThreads / 64;
+#ifndef FI_SC_BANDS
+#define FI_SC_BANDS 0
+#endif
+constexpr bool kScoreBands = FI_SC_BANDS;
 
 // MODE 0: maps read from global memory; 1: maps in LDS.
 template <int MODE>
@@ -751,6 +1154,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
   __shared__ double s_tot[kScoreMaxCrops];
   __shared__ double s_bnd[kScoreMaxCrops];
   __shared__ int32_t cand[kScoreMaxCrops];
+  __shared__ double s_part[kScoreMaxCrops][3];  // band partial sums (crop-major)
   __shared__ int32_t ncand_s, first_cand_s;
   const ScDesc &D = descs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -802,12 +1206,48 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
   const double aoi = fabs(oi);
   const double wd = P.detail_weight, ws = P.skin_weight, wt = P.saturation_weight;
 
-  // ---- fast pass: one wave per crop, lanes across the window's columns.
+  // ---- fast pass: one wave per (crop, band of the window's rows), lanes
+  // across the window's columns.  Bands (FI_SC_BANDS=1) balance the waves
+  // when the crops are few (cfg2: 37 crops -> 74 items on 16 waves, not 3
+  // rounds of 16 / 16 / 5) but measured slower (0.40 vs 0.37 ms per cfg2
+  // step: per-item reductions), so the default is one band per crop.
   // F = sum_in (imp - oi) a + oi * total(a): the outside pixels need no pass,
   // the inside ones weigh by the table of fl(importance - oi) -- 7 f64
   // operations per (crop, pixel) instead of 10
-  for (int c = wave; c < ncrops; c += kScoreWaves) {
+  auto finalize = [&](int c, double sd, double ss, double st) {
+    const DevCrop &cr = crops[D.crop0 + c];
+    const double Fd = sd + oi * T[0], Fs = ss + oi * T[1], Ft = st + oi * T[2];
+    // |python_sum - F| <= 6 gamma(n+4) (imax + imax2 + |oi|) total(a), a >= 0 (biases
+    // >= 0, host-checked): python's sequential sum (5 gamma(n+1) sum |imp a|) plus
+    // this pass (fl(imp - oi), one FMA per term, <= nin_y + 16 additions deep
+    // with the band and wave reductions)
+    const double g4 = (nn + 3.0) * u / (1.0 - (nn + 3.0) * u);
+    const double kb = 6.0 * g4 * (cr.imax + cr.imax2 + aoi) * 1.0000001;
+    const double Ed = kb * T[0], Es = kb * T[1], Et = kb * T[2];
+    const double area = cr.fw * cr.fh;
+    const double tot = (Fd * wd + Fs * ws + Ft * wt) / area;
+    const double mag = fabs(wd) * (fabs(Fd) + Ed) + fabs(ws) * (fabs(Fs) + Es) + fabs(wt) * (fabs(Ft) + Et);
+    const double B = ((fabs(wd) * Ed + fabs(ws) * Es + fabs(wt) * Et) * (1.0 + 16.0 * u) + 16.0 * u * mag) /
+                     area * 1.01;
+    if (!big) {
+      s_tot[c] = tot;
+      s_bnd[c] = B;
+    }
+    CropScore &o = sco[c];
+    o.detail = Fd;
+    o.saturation = Ft;
+    o.skin = Fs;
+    o.total = tot;
+    o.bound = B;
+    o.exact = 0;
+  };
+  const int nbands = big || !kScoreBands ? 1 : max(1, min(min(8, kScoreMaxCrops / ncrops), (4 * kScoreWaves + ncrops - 1) / ncrops));
+  const int nitems = ncrops * nbands;
+  for (int item = wave; item < nitems; item += kScoreWaves) {
+    const int c = item / nbands, band = item - c * nbands;
     const DevCrop cr = crops[D.crop0 + c];
+    const int bh = (cr.nin_y + nbands - 1) / nbands;
+    const int ya = min(cr.nin_y, band * bh), yb = min(cr.nin_y, ya + bh);
     const double *tab = ad + cr.table2;
     double sd = 0, ss = 0, st = 0;
     for (int dx0 = 0; dx0 < cr.nin_x; dx0 += 64) {
@@ -829,9 +1269,9 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
         ss = fma(imp, a1, ss);
         st = fma(imp, a2, st);
       };
-      int dy = 0;
+      int dy = ya;
 #pragma unroll 1
-      for (; dy + 4 <= cr.nin_y; dy += 4) {
+      for (; dy + 4 <= yb; dy += 4) {
         uint32_t m[4];
         double imp[4];
 #pragma unroll
@@ -842,7 +1282,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
         for (int u = 0; u < 4; u++) row_terms(act ? m[u] : 0u, imp[u]);  // m = 0: every term is 0
       }
 #pragma unroll 1
-      for (; dy < cr.nin_y; dy++) {
+      for (; dy < yb; dy++) {
         const uint32_t m = mcol[dy * W];
         row_terms(act ? m : 0u, tcol[(int64_t)dy * cr.table_w]);
       }
@@ -851,29 +1291,25 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
     ss = wave_sum(ss);
     st = wave_sum(st);
     if (lane == 0) {
-      const double Fd = sd + oi * T[0], Fs = ss + oi * T[1], Ft = st + oi * T[2];
-      // |python_sum - F| <= 6 gamma(n+4) (imax + imax2 + |oi|) total(a), a >= 0 (biases
-      // >= 0, host-checked): python's sequential sum (5 gamma(n+1) sum |imp a|) plus
-      // this pass (fl(imp - oi), one FMA per term, <= nin_y + 8 additions deep)
-      const double g4 = (nn + 3.0) * u / (1.0 - (nn + 3.0) * u);
-      const double kb = 6.0 * g4 * (cr.imax + cr.imax2 + aoi) * 1.0000001;
-      const double Ed = kb * T[0], Es = kb * T[1], Et = kb * T[2];
-      const double area = cr.fw * cr.fh;
-      const double tot = (Fd * wd + Fs * ws + Ft * wt) / area;
-      const double mag = fabs(wd) * (fabs(Fd) + Ed) + fabs(ws) * (fabs(Fs) + Es) + fabs(wt) * (fabs(Ft) + Et);
-      const double B = ((fabs(wd) * Ed + fabs(ws) * Es + fabs(wt) * Et) * (1.0 + 16.0 * u) + 16.0 * u * mag) /
-                       area * 1.01;
-      if (!big) {
-        s_tot[c] = tot;
-        s_bnd[c] = B;
+      if (nbands == 1) {
+        finalize(c, sd, ss, st);
+      } else {
+        s_part[item][0] = sd;
+        s_part[item][1] = ss;
+        s_part[item][2] = st;
       }
-      CropScore &o = sco[c];
-      o.detail = Fd;
-      o.saturation = Ft;
-      o.skin = Fs;
-      o.total = tot;
-      o.bound = B;
-      o.exact = 0;
+    }
+  }
+  if (nbands > 1) {
+    __syncthreads();
+    for (int c = tid; c < ncrops; c += kScoreThreads) {
+      double sd = 0, ss = 0, st = 0;  // bands in order: deterministic
+      for (int k = 0; k < nbands; k++) {
+        sd += s_part[c * nbands + k][0];
+        ss += s_part[c * nbands + k][1];
+        st += s_part[c * nbands + k][2];
+      }
+      finalize(c, sd, ss, st);
     }
   }
   __syncthreads();
@@ -1067,6 +1503,13 @@ int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32
   if (n <= 0) return 0;
   if (lds > kFzMaxLds || !skinsat) return -1;
   hipLaunchKernelGGL((k_sc_fz<true>), dim3(n), dim3(kFzThreads), lds, s, descs, ai, P, skinsat);
+  return 0;
+}
+int launch_sc_fd(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
+                 const uint16_t *skinsat) {
+  if (n <= 0) return 0;
+  if (lds > kFdMaxLds || !skinsat) return -1;
+  hipLaunchKernelGGL(k_sc_fd, dim3(n), dim3(kFdThreads), lds, s, descs, ai, P, skinsat);
   return 0;
 }
 int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,

@@ -44,11 +44,14 @@ def _context_with(env):
                 os.environ[k] = v
 
 
-_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0"}
+_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_SC_FD": "1"}
 PATHS = {
     # default kernels: k_rs_vr (block-major persistent MFMA resample; k_rs_vm
-    # where its tables do not fit) / k_rs_hv; k_sc_fz fused prescale + maps; k_sc_score2
+    # where its tables do not fit) / k_rs_hv; k_sc_fd fused prescale + maps
+    # (source rows by LDS-DMA); k_sc_score2
     "vr": dict(_ENV),
+    # the same with k_sc_fz (register-staged source rows, two workgroups per CU)
+    "fz": dict(_ENV, FI_SC_FD="0"),
     # the fallbacks: k_rs_vm streaming resample; k_sc_hmfma + k_sc_vq (H-stage rows through HBM)
     "vm": dict(_ENV, FI_VR_RS="0", FI_DISABLE_SC_FZ="1"),
     # generic kernels: two-pass resample; per-row prescale/maps kernels
@@ -65,7 +68,9 @@ def rctx(request):
     c.close()
 
 
-EXPECTED_PATH = {"vr": "path_vr", "vm": "path_vm", "generic": "path_generic_v"}
+EXPECTED_PATH = {"vr": "path_vr", "fz": "path_vr", "vm": "path_vm", "generic": "path_generic_v"}
+# smartcrop prescale kernel of each path (images counted by fi_kernel_stats)
+EXPECTED_SC = {"vr": "sc_path_fd", "fz": "sc_path_fz", "vm": None, "generic": None}
 
 
 @pytest.mark.parametrize("W,H,opts,even_rows", [
@@ -92,6 +97,7 @@ def test_baseline_geometries_take_the_path(rctx, W, H, opts, even_rows):
 @pytest.fixture(scope="module", params=sorted(PATHS))
 def sctx(request):
     c = _context_with(PATHS[request.param])
+    c.path_name = request.param
     yield c
     c.close()
 
@@ -167,6 +173,31 @@ def test_smartcrop_fast_bounds_contain_exact(sctx, case):
             assert c.total.hex() == g[7]
         else:
             assert abs(c.total - exact) <= 1e-9 * max(1.0, abs(exact)), (c.total, exact)
+
+
+@pytest.mark.parametrize("w,h", [(500, 281), (333, 500), (450, 300), (301, 201)])
+def test_smartcrop_prescale_kernel_of_path(sctx, w, h):
+    """fi_smartcrop runs its prescale + maps on the kernel the path names
+    (k_sc_fd on the default path for 3-channel images at the staged 16-B
+    rounded pitch, k_sc_fz with FI_SC_FD=0; no silent fallback), and the
+    result is the oracle's: every crop's scores bit-exact (exact_all).  The
+    sizes prescale by 1.8-3 (a 14-row chunk's window within 64 H-stage rows)."""
+    src = synth_rgb(w, h, 0x5C + w)
+    names = ("sc_path_fd", "sc_path_fz")
+    before = {k: sctx.stats(k)[1] for k in names}
+    r = sctx.smartcrop_ex(src, 100, 100, options=_opts(True), want_images=True)
+    ran = {k: sctx.stats(k)[1] - before[k] for k in names}
+    want = EXPECTED_SC[sctx.path_name]
+    if want is not None:
+        assert ran[want] == 1 and sum(ran.values()) == 1, ran
+    else:
+        assert sum(ran.values()) == 0, ran
+    ref = orc.sc_crop(src, 100, 100)
+    assert r["n"] == len(ref["crops"])
+    for c, g in zip(r["crops"], ref["crops"]):
+        assert [c.x, c.y, c.width, c.height] == [g["x"], g["y"], g["width"], g["height"]]
+        assert [c.detail.hex(), c.saturation.hex(), c.skin.hex(), c.total.hex()] == \
+            [g["score"][k].hex() for k in ("detail", "saturation", "skin", "total")]
 
 
 def test_smartcrop_reference_fixture(sctx):
