@@ -943,6 +943,7 @@ __global__ __launch_bounds__(kFdThreads) void k_sc_fd(const ScDesc *__restrict__
   for (int c = 0; c < chunks; c++) {
     const int k0 = ai[D.vqK0 + c];
     const int need = min(k0 + 64, hrows);
+    bool phased = false;
 #pragma unroll 1
     while (16 * blk < need) {
       if (loader) {
@@ -953,10 +954,11 @@ __global__ __launch_bounds__(kFdThreads) void k_sc_fd(const ScDesc *__restrict__
       }
       fd_barrier();
       blk++;
+      phased = true;
     }
-    // the chunk's window is in the ring (and the last chunk's maps are done
-    // with prer / lum: a barrier of their own when no block ran in between)
-    fd_barrier();
+    // the chunk's window is in the ring; the last chunk's maps are done with
+    // prer / lum (a barrier of their own when no block ran in between)
+    if (!phased) fd_barrier();
     const int y0 = kVqRows * c, y1 = min(y0 + kVqRows, ah), pa = max(0, y0 - 1), pe = min(ah, pa + 16);
     if (!loader) {
       const i32x4 *af = reinterpret_cast<const i32x4 *>(abuf + c * 3072);
