@@ -692,10 +692,14 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
         if (i2 == c->imp2_at.end()) {
           double imax2 = 0;
           const int32_t off = E.od();
-          for (double v : iit->second) {
-            const double w = v - E.params.outside_importance;
-            imax2 = std::max(imax2, std::fabs(w));
-            E.ad.push_back(w);
+          const int nx2 = (nx + 63) / 64 * 64;  // rows padded with zeros: k_sc_score2's idle lanes weigh 0
+          for (int y = 0; y < ny; y++) {
+            for (int x = 0; x < nx; x++) {
+              const double w = iit->second[(size_t)y * nx + x] - E.params.outside_importance;
+              imax2 = std::max(imax2, std::fabs(w));
+              E.ad.push_back(w);
+            }
+            E.ad.insert(E.ad.end(), (size_t)(nx2 - nx), 0.0);
           }
           i2 = c->imp2_at.emplace(pk, std::make_pair(off, imax2)).first;
         }
@@ -718,6 +722,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
         dc.table_w = std::get<1>(t);
         dc.imax = std::get<2>(t);
         dc.table2 = tab2_of[{dbits(ch.fw), dbits(ch.fh)}].first;
+        dc.table2_w = (dc.table_w + 63) / 64 * 64;
         dc.imax2 = tab2_of[{dbits(ch.fw), dbits(ch.fh)}].second;
         dc.rx = ch.rx;
         dc.ry = ch.ry;

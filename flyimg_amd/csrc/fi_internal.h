@@ -83,8 +83,8 @@ struct DevCrop {
   int32_t rx, ry, rw, rh; // rescaled ints (crop() :184-190)
   double imax;            // max |importance| over the table (fast-pass error bound)
   double imax2;           // max |importance - outside_importance| over the table2
-  int32_t table2;         // arena offset (double units): fl(importance - outside_importance), same layout
-  int32_t pad2;
+  int32_t table2;         // arena offset (double units): fl(importance - outside_importance), rows of
+  int32_t table2_w;       //   table2_w = table_w rounded up to 64 (zeros past table_w)
 };
 
 struct ScDesc {

@@ -1245,32 +1245,40 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
   };
   const int nbands = big || !kScoreBands ? 1 : max(1, min(min(8, kScoreMaxCrops / ncrops), (4 * kScoreWaves + ncrops - 1) / ncrops));
   const int nitems = ncrops * nbands;
-  for (int item = wave; item < nitems; item += kScoreWaves) {
+  for (int item = __builtin_amdgcn_readfirstlane(wave); item < nitems; item += kScoreWaves) {
     const int c = item / nbands, band = item - c * nbands;
     const DevCrop cr = crops[D.crop0 + c];
     const int bh = (cr.nin_y + nbands - 1) / nbands;
     const int ya = min(cr.nin_y, band * bh), yb = min(cr.nin_y, ya + bh);
-    const double *tab = ad + cr.table2;
+    const int t2w = cr.table2_w;
+    const __amdgpu_buffer_rsrc_t trs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(ad + cr.table2), (short)0, cr.nin_y * t2w * 8, 0x00020000);
     double sd = 0, ss = 0, st = 0;
+    auto row_terms = [&](uint32_t m, double imp) {
+      const double d = lut[(m >> 8) & 255];
+      const double a1 = lut[m & 255] * (d + sb);
+      const double a2 = lut[(m >> 16) & 255] * (d + tb);
+      sd = fma(imp, d, sd);
+      ss = fma(imp, a1, ss);
+      st = fma(imp, a2, st);
+    };
     for (int dx0 = 0; dx0 < cr.nin_x; dx0 += 64) {
       const int dx = dx0 + lane;
-      const bool act = dx < cr.nin_x;
+      // LDS maps: lanes past the window read whatever lies there (finite
+      // terms) and weigh it by the table's zero padding, so no lane test and
+      // the table rows load by scalar base + lane offset; global maps keep
+      // the column clamp (the read must stay inside the buffer)
+      const bool act = LDS_MAPS || dx < cr.nin_x;
       const int dxc = act ? dx : 0;
       const uint32_t *mcol = maps + (int64_t)cr.y0 * W + cr.x0 + dxc;
-      const double *tcol = tab + dxc;
-      // rows in groups of 4: the four map words are read unconditionally (the
-      // column is clamped) and zeroed for idle lanes after the read, so the
-      // group's map reads, then its 12 table reads, go out together (a
-      // conditional read put an exec-masked block and a full LDS wait
-      // between consecutive rows)
-      auto row_terms = [&](uint32_t m, double imp) {
-        const double d = lut[(m >> 8) & 255];
-        const double a1 = lut[m & 255] * (d + sb);
-        const double a2 = lut[(m >> 16) & 255] * (d + tb);
-        sd = fma(imp, d, sd);
-        ss = fma(imp, a1, ss);
-        st = fma(imp, a2, st);
+      // table row r, column dxc: buffer load, row offset in an SGPR
+      auto tload = [&](int r) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(trs, 8u * (uint32_t)dxc,
+                                                                               (uint32_t)(r * t2w * 8), 0));
       };
+      // rows in groups of 4: the four map words, then the four table values,
+      // go out together (a conditional read put an exec-masked block and a
+      // full LDS wait between consecutive rows)
       int dy = ya;
 #pragma unroll 1
       for (; dy + 4 <= yb; dy += 4) {
@@ -1279,14 +1287,14 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
 #pragma unroll
         for (int u = 0; u < 4; u++) m[u] = mcol[(dy + u) * W];
 #pragma unroll
-        for (int u = 0; u < 4; u++) imp[u] = tcol[(int64_t)(dy + u) * cr.table_w];
+        for (int u = 0; u < 4; u++) imp[u] = tload(dy + u);
 #pragma unroll
         for (int u = 0; u < 4; u++) row_terms(act ? m[u] : 0u, imp[u]);  // m = 0: every term is 0
       }
 #pragma unroll 1
       for (; dy < yb; dy++) {
         const uint32_t m = mcol[dy * W];
-        row_terms(act ? m : 0u, tcol[(int64_t)dy * cr.table_w]);
+        row_terms(act ? m : 0u, tload(dy));
       }
     }
     sd = wave_sum(sd);

@@ -227,7 +227,8 @@ constexpr int kVrStampN = 16 * 6;
 __device__ uint64_t g_vr_stamps[kVrStampSlots * kVrStampN];
 
 // MODE (profiling ablations, FI_VR_VARIANT; wrong pixels): 0 production,
-// 1 DMA stream only, 2 no H role and no stores, 3 no stores, 5 / 6 loader
+// 1 DMA stream only, 2 no H role and no stores, 3 no stores, 4 no A-fragment
+// DMAs after the first two blocks, 5 / 6 loader
 // priority 1 / 0 (production pixels), 9 production + per-phase s_memtime sums;
 // 10 + k: ablation k with the stamps.
 template <int MODE>
@@ -514,7 +515,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     if (kStamp) tprev = __builtin_amdgcn_s_memtime();
     for (int p = 0; p < N + 2; p++) {
       // A fragments of block p + 1 (its record was written last phase)
-      if (M != 1 && p + 1 < N) issue_a(P1, (p + 1) & 1);
+      if (M != 1 && M != 4 && p + 1 < N) issue_a(P1, (p + 1) & 1);
       stamp(0);
       PI P2{};
       if (p + 2 < N) P2 = next_phase(p + 2);
@@ -956,15 +957,17 @@ int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrT
     case 2: FI_VR_LAUNCH(2); break;
     case 3: FI_VR_LAUNCH(3); break;
     case 5: FI_VR_LAUNCH(5); break;
+    case 4: FI_VR_LAUNCH(4); break;
     case 6: FI_VR_LAUNCH(6); break;
     case 9: FI_VR_LAUNCH(9); break;
+    case 14: FI_VR_LAUNCH(14); break;
     case 11: FI_VR_LAUNCH(11); break;
     case 12: FI_VR_LAUNCH(12); break;
     case 13: FI_VR_LAUNCH(13); break;
     default: FI_VR_LAUNCH(0); break;
   }
 #undef FI_VR_LAUNCH
-  return (v == 1 || v == 2 || v == 3 || v == 11 || v == 12 || v == 13) ? 1 : 0;
+  return (v == 1 || v == 2 || v == 3 || v == 4 || v == 11 || v == 12 || v == 13 || v == 14) ? 1 : 0;
 }
 
 }  // namespace fi
