@@ -628,6 +628,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           const uint32_t want = (uint32_t)kHW * (uint32_t)(p + 1);
           while (hcnt[0] < want) __builtin_amdgcn_s_sleep(1);
         }
+        stamp(4);
         // block done: ClampToQuantum(257 acc / 2^shift) -> Q16 hi / lo signed-byte planes
         const float vscale = __builtin_amdgcn_ldexpf(257.0f, -((C.flags >> kVshShift) & 31));
 #pragma unroll
@@ -654,7 +655,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       phase_barrier();
       stamp(3);
     }
-    stamp_out(4);
+    stamp_out(5);
     return;
   }
 

@@ -45,12 +45,12 @@ with Context(0) as ctx:
     a = buf.reshape(256, 16, 6).astype(np.float64)
     a = a[a[:, 0, 5] > 0]
     ph = a[:, 0, 5].mean()
-    roles = {"V": (range(0, 8), ["tile entry", "V-MFMA issue", "planes", "barrier"]),
+    roles = {"V": (range(0, 8), ["tile entry", "V-MFMA issue", "planes", "barrier", "plane wait"]),
              "H": (range(8, 13 if VR else 14), ["-", "tile entry", "horizontal", "-", "barrier"]),
              "L": (range(14, 16), ["A DMA", "records + row DMA", "vmcnt wait", "barrier"])}
     print(f"{len(a)} workgroups, phases/WG {ph:.0f}; per-phase ticks by wave (mean over workgroups)")
     for r, (waves, names) in roles.items():
         for w in waves:
             v = a[:, w, :len(names)].mean(axis=0) / ph
-            work = sum(x for n, x in zip(names, v) if n not in ("barrier", "-"))
+            work = sum(x for n, x in zip(names, v) if n not in ("barrier", "-", "plane wait"))
             print(f"  {r} wave {w:2d}: work {work:7.0f} | " + "  ".join(f"{n} {x:6.0f}" for n, x in zip(names, v)))
