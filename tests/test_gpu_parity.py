@@ -372,7 +372,7 @@ def test_horizontal_first_within_one_lsb_of_oracle(rctx, case):
     before = {p: rctx.stats(p)[1] for p in ("path_hv", "path_generic_h")}
     outs, recs, rc = rctx.process([src], [Op(tw, th, flags, g, rot)])
     assert rc == 0 and recs[0].status == 0, L.lib().fi_last_error()
-    want = "path_hv" if hv and rctx.path_name in ("vr", "vm") else "path_generic_h"
+    want = "path_hv" if hv and rctx.path_name != "generic" else "path_generic_h"
     assert rctx.stats(want)[1] == before[want] + 1, (want, {p: rctx.stats(p)[1] - before[p] for p in before})
     ref = orc.im_convert(src, tw, th, _oracle_flags(flags), gravity=g, rotate=rot)
     _cmp(outs[0], ref, name)

@@ -25,7 +25,7 @@ if want prof; then
     python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/profile_bench.json" 2> "$OUT/prof.err"; rc=$?
   echo "rocprof cfg2 rc=$rc"; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof3" -o run -- \
-    python3 "$ROOT/bench.py" --workload cfg3 --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/profile_bench3.json" 2> "$OUT/prof3.err"; rc=$?
+    python3 "$ROOT/bench.py" --workload cfg3 --steps 6 --warmup 2 --no-cpu-baseline > "$OUT/profile_bench3.json" 2> "$OUT/prof3.err"; rc=$?
   echo "rocprof cfg3 rc=$rc"; [ $rc -eq 0 ] || exit $rc
   cd "$ROOT"
 fi
