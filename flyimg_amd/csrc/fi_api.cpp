@@ -216,6 +216,7 @@ struct fi_ctx {
   bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
   int vr_max_classes = 8;  // batches with more vertical tables stay on k_rs_vm (FI_VR_MAX_CLASSES)
   int res_align = 16;      // row pitch alignment of the resized image kept for smartcrop apply (FI_RES_ALIGN)
+  bool timing_resize_only = false;  // fi_set_timing(2): stage timing events around the resample only
   int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   bool sc_fd = true;        // FI_SC_FD=0: k_sc_fz instead of its LDS-DMA form k_sc_fd
@@ -322,7 +323,7 @@ struct Timer {  // HIP-event range: starts on stream sa, ends on stream sb
   hipStream_t sb;
   Timer(fi_ctx *c_, const char *name, double bytes) : Timer(c_, name, bytes, c_->stream, c_->stream) {}
   Timer(fi_ctx *c_, const char *name, double bytes, hipStream_t sa, hipStream_t sb_)
-      : c(c_), on(c_->timing), sb(sb_) {
+      : c(c_), on(c_->timing && (!c_->timing_resize_only || strcmp(name, "resize") == 0)), sb(sb_) {
     if (!on) return;
     r.name = name;
     r.bytes = bytes;
@@ -3125,6 +3126,7 @@ int fi_fill_synthetic(fi_ctx *c, uint8_t *dev, int32_t w, int32_t h, int32_t str
 int fi_set_timing(fi_ctx *c, int32_t enable) {
   if (!c) return set_err(FI_EINVAL, "ctx is NULL");
   c->timing = enable != 0;
+  c->timing_resize_only = enable == 2;
   return FI_OK;
 }
 int fi_reset_stats(fi_ctx *c) {

@@ -351,7 +351,8 @@ class Context:
         return self._lib.fi_wait(self.h, keep)
 
     # ---- timing ----------------------------------------------------------------
-    def set_timing(self, on: bool):
+    def set_timing(self, on):
+        """True / 1: every stage timed; 2: the resample stage only; False / 0: off."""
         L.check(self._lib.fi_set_timing(self.h, int(on)))
 
     def reset_stats(self):

@@ -240,9 +240,14 @@ int fi_memcpy_d2h(fi_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 int fi_fill_synthetic(fi_ctx *ctx, uint8_t *dev, int32_t w, int32_t h, int32_t stride,
                       uint32_t seed);
 
-/* Kernel timing (HIP events on the launch stream).  Names: "resize",
- * "resize_v", "resize_h", "sc_prescale", "sc_maps", "sc_score", "crop_apply",
- * "batch".  bytes = algorithmic bytes accounted to that kernel. */
+/* Stage timing (HIP event ranges on the launch streams).  enable: 0 off, 1
+ * every stage ("batch", "resize", "sc_prep", "sc_score", "crop_apply", "mono",
+ * "conv", "h2d_src", "d2h_out"), 2 the resample stage only (each event range
+ * adds a few microseconds between dependent kernels).  fi_kernel_stats also
+ * reports host timings ("host_*", "host_total") and per-path image counters
+ * ("path_vr", "path_vm", "path_hv", "path_generic_v", "path_generic_h",
+ * "path_copy", "sc_path_fd", "sc_path_fz").  bytes = algorithmic bytes
+ * accounted to that stage. */
 int fi_set_timing(fi_ctx *ctx, int32_t enable);
 int fi_reset_stats(fi_ctx *ctx);
 int fi_kernel_stats(fi_ctx *ctx, const char *name, double *total_ms, int64_t *launches,
