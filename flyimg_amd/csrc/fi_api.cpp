@@ -2008,9 +2008,11 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
     (void)launch_mono(c->stream, (const MonoDesc *)(ab + K.mono_off), (int)Bp.mono.size(), ad + K.mono_wts);
   }
   HIP_TRY(hipGetLastError());
-  if (!S.rs_done) HIP_TRY(hipEventCreateWithFlags(&S.rs_done, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(S.rs_done, c->stream));
-  HIP_TRY(hipStreamWaitEvent(c->sc_stream, S.rs_done, 0));
+  if (c->sc_stream != c->stream) {  // (one stream today: stream order is the dependency)
+    if (!S.rs_done) HIP_TRY(hipEventCreateWithFlags(&S.rs_done, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(S.rs_done, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->sc_stream, S.rs_done, 0));
+  }
   if (K.SX.nsl + K.SX.nsg > 0) {
     const int rc = enqueue_sc(c, c->sc_stream, ab, K.SX, ai, ad, (CropScore *)(wb + Bp.scores_off),
                               (ScResult *)(wb + Bp.results_off), PD);
