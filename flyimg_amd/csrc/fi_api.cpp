@@ -2298,7 +2298,7 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   Blob &B = E.blob;
   ScLaunches SX;
   add_sc_launches(c, B, SL, st, &SX);
-  const size_t ai_off = B.addv(E.ai), ad_off = B.addv(E.ad);
+  const size_t ai_off = B.addv(E.ai), af_off = B.addv(E.af), ad_off = B.addv(E.ad);
   if (!heap_fits(c, E)) return set_err(FI_ENOMEM, "smartcrop tables exceed the device table heap");
   rc = ensure(c, &c->arena, B.b.size() + 256);
   if (rc) return rc;
@@ -2307,7 +2307,7 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   memcpy(c->pinned, B.b.data(), B.b.size());
   HIP_TRY(hipMemcpyAsync(c->arena.p, c->pinned, B.b.size(), hipMemcpyHostToDevice, c->stream));
   uint8_t *ab = (uint8_t *)c->arena.p;
-  rc = heap_commit(c, E, ab, ai_off, ai_off, ad_off);
+  rc = heap_commit(c, E, ab, ai_off, af_off, ad_off);
   if (rc) return rc;
   rc = enqueue_sc(c, c->stream, ab, SX, (const int32_t *)c->heap_i.p, (const double *)c->heap_d.p,
                   (CropScore *)(wb + scores_off), (ScResult *)(wb + results_off), to_dev(params));
