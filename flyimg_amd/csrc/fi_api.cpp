@@ -215,6 +215,7 @@ struct fi_ctx {
   bool fast_rs = true;  // FI_FORCE_GENERIC=1: the generic two-pass resample (and smartcrop) kernels only
   bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
   int vr_max_classes = 8;  // batches with more vertical tables stay on k_rs_vm (FI_VR_MAX_CLASSES)
+  bool vm_lpt = true;      // k_rs_vm tiles: LPT images -> XCDs, longest tiles first (FI_VM_LPT=0: round robin)
   int res_align = 16;      // row pitch alignment of the resized image kept for smartcrop apply (FI_RES_ALIGN)
   bool timing_resize_only = false;  // fi_set_timing(2): stage timing events around the resample only
   int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
@@ -1746,7 +1747,12 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   for (const Work1 &w : work) nst += w.nstrips;
   // XCD-aware order: the strips of one image go to one XCD queue (blockIdx % 8 under
   // round-robin dispatch) back to back, so the halo columns they share hit that L2
+  // With c->vm_lpt (mixed batches: cfg4) the images go to the XCD queues by
+  // LPT on their pieces and each queue runs its longest tiles first, so the
+  // launch does not end on one 24 MP image's strips.
   std::vector<std::vector<VTile>> q8(8);
+  std::vector<std::vector<VTile>> img_tiles(work.size());
+  std::vector<int64_t> img_cost(work.size(), 0);
   for (size_t k = 0; k < work.size(); k++) {
     const Work1 &w = work[k];
     const VmV &V = *w.V;
@@ -1759,8 +1765,26 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
       if (b1 <= b0) continue;
       const int p0 = first_piece[b0 > 0 ? b0 - 1 : 0];
       const int p1 = first_piece[b1];
-      for (int st = 0; st < w.nstrips; st++) q8[k % 8].push_back(VTile{w.img, w.first_strip + st, p0, p1, b0, 0});
+      for (int st = 0; st < w.nstrips; st++) {
+        img_tiles[k].push_back(VTile{w.img, w.first_strip + st, p0, p1, b0, 0});
+        img_cost[k] += p1 - p0 + 1;
+      }
     }
+  }
+  if (c->vm_lpt && work.size() > 1) {
+    std::vector<int> order(work.size());
+    for (size_t k = 0; k < work.size(); k++) order[k] = (int)k;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return img_cost[x] > img_cost[y]; });
+    int64_t load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k : order) {
+      const int x = (int)(std::min_element(load, load + 8) - load);
+      load[x] += img_cost[k];
+      q8[x].insert(q8[x].end(), img_tiles[k].begin(), img_tiles[k].end());
+    }
+    for (auto &q : q8)
+      std::stable_sort(q.begin(), q.end(), [](const VTile &x, const VTile &y) { return x.p1 - x.p0 > y.p1 - y.p0; });
+  } else {
+    for (size_t k = 0; k < work.size(); k++) q8[k % 8].insert(q8[k % 8].end(), img_tiles[k].begin(), img_tiles[k].end());
   }
   size_t mx = 0;
   for (auto &q : q8) mx = std::max(mx, q.size());
@@ -2688,6 +2712,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';
   if (const char *e = getenv("FI_VR_MAX_CLASSES")) c->vr_max_classes = atoi(e);
+  if (const char *e = getenv("FI_VM_LPT")) c->vm_lpt = e[0] == '1';
   if (const char *e = getenv("FI_RES_ALIGN")) c->res_align = std::max(1, atoi(e));
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   // (the smartcrop stage on a stream of its own beside the next batch's
