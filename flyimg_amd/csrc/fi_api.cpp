@@ -1437,7 +1437,20 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     if (vp == c->vr_at.end()) {
       std::array<int32_t, 4> o;
       o[0] = put(V.rows);
-      E.ai.insert(E.ai.end(), 32, 0);  // k_rs_vr reads the list 16 entries at a time, one group ahead
+      E.ai.insert(E.ai.end(), 32, 0);
+      if (V.rstep == 0 && !V.rows.empty()) {
+        // the uneven list again, as each k_rs_vr loader wave walks it: class
+        // rho = k & 3, entry j = the pair (rows[4 j + rho], rows[4 j + rho + 1]),
+        // so a wave's own pairs (4 apart) are 16 consecutive ints per 8 pairs
+        const int n = (int)V.rows.size(), J = (n + 3) / 4 + 16;
+        std::vector<int32_t> p4(8 * (size_t)J);
+        for (int rho = 0; rho < 4; rho++)
+          for (int j = 0; j < J; j++) {
+            p4[(size_t)2 * (rho * J + j)] = V.rows[std::min(4 * j + rho, n - 1)];
+            p4[(size_t)2 * (rho * J + j) + 1] = V.rows[std::min(4 * j + rho + 1, n - 1)];
+          }
+        put(p4);
+      }
       align4();
       o[1] = put(V.bmeta);
       o[2] = put(V.w128);

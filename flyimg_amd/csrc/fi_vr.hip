@@ -199,11 +199,12 @@ __device__ __forceinline__ void wait_vm_le(int n) {
 struct Rec {  // 32 B in LDS (kRecBytes)
   int32_t t, blk, flags, slot0, ks, grend, frag, w128;  // frag / w128: int32 offsets into ai
 };
-struct W16 {
-  int32_t v[16];
-};
-struct W8 {
-  int32_t v[8];
+#ifndef FI_VR_PL
+#define FI_VR_PL 4
+#endif
+constexpr int PL = FI_VR_PL;  // k_rs_vr uneven row list: own pairs per scalar load
+struct WL {
+  int32_t v[2 * PL];
 };
 struct Lds {  // offsets of the launch's LDS regions
   int ring, a, rec, cnt, lut, planes, otile;
@@ -373,14 +374,19 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         int k0 = RT.kbase + (rG - RT.g0);
         if (r_rstep == 0 && k0 + 1 < r_nrows) {
           const int cnt = min((seg - rG + 3) >> 2, (r_nrows - 1 - k0 + 3) >> 2);
-          const W8 *lst = reinterpret_cast<const W8 *>(ai + r_rows + k0);  // the host pads the list by 32
-          W8 cur = ldc(lst), nxt{};
-          for (int j0 = 0; j0 < cnt; j0 += 2) {
-            if (j0 + 2 < cnt) nxt = ldc(lst + (j0 / 2 + 1));
+          // the host's pair list (after the row list and its 32-entry pad):
+          // class k0 & 3, own pair m at entry (k0 >> 2) + m, PL pairs per wait
+          // (scalar loads complete out of order: each wait is lgkmcnt(0))
+          const int J = ((r_nrows + 3) >> 2) + 16;
+          const WL *lst =
+              reinterpret_cast<const WL *>(ai + r_rows + r_nrows + 32 + 2 * ((k0 & 3) * J + (k0 >> 2)));
+          for (int j0 = 0; j0 < cnt; j0 += PL) {
+            const WL c0 = ldc(lst + j0 / PL);
+            const int jn = cnt - j0;
 #pragma unroll
-            for (int j = 0; j < 2; j++) {
-              if (j0 + j >= cnt) break;
-              const int r0 = cur.v[4 * j], r1 = cur.v[4 * j + 1];
+            for (int j = 0; j < PL; j++) {
+              if (j >= jn) continue;
+              const int r0 = c0.v[2 * j], r1 = c0.v[2 * j + 1];
               const uint32_t f = (uint32_t)((rslot & 7) | (((rslot >> 4) & 1) << 3));
               uint32_t lc = lane_c ^ f;
               if (16 * (int)lc >= r_nbytes) lc = 0;
@@ -389,7 +395,6 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
               rslot += 4;
               if (rslot >= R) rslot -= R;
             }
-            cur = nxt;
           }
           n += cnt;
           rG += 4 * cnt;
