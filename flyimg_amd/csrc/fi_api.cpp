@@ -1820,7 +1820,7 @@ static void build_hv_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   };
   std::map<const HvH *, int32_t> splaced;  // first strip in Bp.hstrips
   struct Work1 {
-    int32_t img, first_strip, nstrips, nblk;
+    int32_t img, first_strip, nstrips, nblk, nrows;
   };
   std::vector<Work1> work;
   for (size_t q = 0; q < Bp.hv_img.size(); q++) {
@@ -1879,12 +1879,17 @@ static void build_hv_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     m.vws = vp->second[2];
     m.hw128 = hp->second[0];
     m.W = Bp.hv_W[q];
-    work.push_back({(int32_t)Bp.hdescs.size(), sp->second, (int32_t)H.strips.size(), V.nblk});
+    work.push_back({(int32_t)Bp.hdescs.size(), sp->second, (int32_t)H.strips.size(), V.nblk, V.nrows});
     Bp.hdescs.push_back(m);
   }
   int64_t nst = 0;
   for (const Work1 &w : work) nst += w.nstrips;
-  std::vector<std::vector<HvTile>> q8(8);  // XCD-aware order, as build_vm_tiles
+  // XCD-aware order, as build_vm_tiles (with c->vm_lpt: images by LPT on their
+  // source rows x strips, each queue's tiles longest first)
+  std::vector<std::vector<HvTile>> q8(8);
+  std::vector<std::vector<HvTile>> img_tiles(work.size());
+  std::vector<int64_t> img_cost(work.size(), 0);
+  auto tile_cost = [&](const Work1 &w, const HvTile &t) { return (int64_t)(t.b1 - t.b0) * w.nrows / std::max(w.nblk, 1) + 16; };
   for (size_t k = 0; k < work.size(); k++) {
     const Work1 &w = work[k];
     constexpr int64_t target = 8192;  // workgroups the bands aim for
@@ -1893,8 +1898,29 @@ static void build_hv_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     for (int bnd = 0; bnd < bands; bnd++) {
       const int b0 = (int)((int64_t)w.nblk * bnd / bands), b1 = (int)((int64_t)w.nblk * (bnd + 1) / bands);
       if (b1 <= b0) continue;
-      for (int st = 0; st < w.nstrips; st++) q8[k % 8].push_back(HvTile{w.img, w.first_strip + st, b0, b1});
+      for (int st = 0; st < w.nstrips; st++) {
+        img_tiles[k].push_back(HvTile{w.img, w.first_strip + st, b0, b1});
+        img_cost[k] += tile_cost(w, img_tiles[k].back());
+      }
     }
+  }
+  if (c->vm_lpt && work.size() > 1) {
+    std::vector<int> order(work.size());
+    for (size_t k = 0; k < work.size(); k++) order[k] = (int)k;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return img_cost[x] > img_cost[y]; });
+    std::vector<std::vector<std::pair<int64_t, HvTile>>> qc(8);
+    int64_t load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k : order) {
+      const int x = (int)(std::min_element(load, load + 8) - load);
+      load[x] += img_cost[k];
+      for (const HvTile &t : img_tiles[k]) qc[x].push_back({tile_cost(work[k], t), t});
+    }
+    for (int x = 0; x < 8; x++) {
+      std::stable_sort(qc[x].begin(), qc[x].end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+      for (const auto &e : qc[x]) q8[x].push_back(e.second);
+    }
+  } else {
+    for (size_t k = 0; k < work.size(); k++) q8[k % 8].insert(q8[k % 8].end(), img_tiles[k].begin(), img_tiles[k].end());
   }
   size_t mx = 0;
   for (auto &q : q8) mx = std::max(mx, q.size());
