@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 final evidence, in two gpurun calls (each under the 1200 s limit):
+# Round-4 final evidence, in up to three gpurun calls (each under the 1200 s limit):
 #   PART=1: full GPU tests + smoke, then PMC traffic (FETCH_SIZE / WRITE_SIZE,
-#           separate passes) of k_rs_vr on cfg2 / cfg3 / cfg1 / cfg5 and of every
-#           resample kernel ("k_rs_") on cfg4 -> gpurun_out/final/traffic_*.json
-#           (copy them into profiles/ before PART=2, so the bench lines report them)
+#           separate passes) of k_rs_vr on cfg2 / cfg3 / cfg1 / cfg5
+#           -> gpurun_out/final/traffic_*.json (copy them into profiles/ before
+#           PART=2, so the bench lines report them)
 #   PART=3: the cfg4 PMC passes (every resample kernel) -> traffic_cfg4_resize.json
 #   PART=2: rocprofv3 kernel stats of cfg2 / cfg3 / cfg4, the default bench line,
 #           the cfg1 / cfg3 / cfg4 / cfg5 lines -> gpurun_out/final/
