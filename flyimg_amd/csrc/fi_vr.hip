@@ -200,7 +200,7 @@ struct Rec {  // 32 B in LDS (kRecBytes)
   int32_t t, blk, flags, slot0, ks, grend, frag, w128;  // frag / w128: int32 offsets into ai
 };
 #ifndef FI_VR_PL
-#define FI_VR_PL 4
+#define FI_VR_PL 5
 #endif
 constexpr int PL = FI_VR_PL;  // k_rs_vr uneven row list: own pairs per scalar load
 struct WL {
