@@ -3,6 +3,10 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2]
 
+Ranks: under torch.distributed.run (WORLD_SIZE set) each process is one rank
+and WORLD_SIZE must equal --gpus; without a launcher, --gpus N > 1 starts N
+rank processes itself (launch_ranks) and relays rank 0's line.
+
 One step = one batch (fi_submit_batch_device; batch k+1 is planned on the
 host while batch k runs, every batch is finalized inside the timed region) over the rank's device-resident
 batch of synthetic RGB8 images (inputs already in HBM when timing starts):
@@ -191,6 +195,65 @@ def source_hash():
     return h.hexdigest()
 
 
+def launch_ranks(n: int) -> int:
+    """``bench.py --gpus N`` without an external launcher: start N rank
+    processes of this same command (RANK / LOCAL_RANK / WORLD_SIZE, a private
+    rendezvous id, MASTER_ADDR 127.0.0.1), relay rank 0's JSON line, and fail
+    when any rank fails.  Runs before this process loads the library or
+    touches a GPU; the ranks are children, not an exec of this process."""
+    import subprocess
+    import uuid
+
+    rdzv = f"bench{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29500"), FI_RDZV_ID=rdzv)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    log(f"launched {n} ranks (rendezvous {rdzv})")
+    import threading
+
+    out0 = []
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()))
+    reader.start()
+    # a rank that fails leaves the others waiting in the rendezvous: stop them
+    while any(p.poll() is None for p in procs):
+        if any(p.poll() not in (None, 0) for p in procs):
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    reader.join()
+    rcs = [p.wait() for p in procs]
+    lines = [ln for ln in "".join(out0).splitlines() if ln.startswith("{")]
+    if any(rcs) or len(lines) != 1:
+        log(f"error: rank exit codes {rcs}, {len(lines)} JSON lines from rank 0")
+        return 1
+    print(lines[0], flush=True)
+    return 0
+
+
+def dry_run(args, rank, world, local_rank, comm):
+    """Control-plane rehearsal of a multi-rank run: no library, no GPU.
+    ``FI_DRY_RUN_FAIL_RANK=r`` makes rank r exit 3 after joining (launcher test)."""
+    if os.environ.get("FI_DRY_RUN_FAIL_RANK") == str(rank):
+        sys.exit(3)
+    joined = comm.allgather_obj({"rank": rank, "local_rank": local_rank, "pid": os.getpid()})
+    comm.barrier()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": [j["rank"] for j in joined],
+                          "local_ranks": [j["local_rank"] for j in joined],
+                          "distinct_pids": len({j["pid"] for j in joined}), "workload": args.workload}), flush=True)
+    comm.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,17 +266,34 @@ def main():
                     help="diagnostic: every stage's event range inside the timed region (adds gaps)")
     ap.add_argument("--no-verify", action="store_true", help="skip the oracle check of the last timed batch "
                     "(profiling ablations only)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="control plane only (no GPU, no library): every rank joins the rendezvous, rank 0 prints "
+                         "one JSON line naming the ranks that joined (tests the launcher)")
     args = ap.parse_args()
 
+    # ---- ranks: an external launcher (torch.distributed.run) sets WORLD_SIZE;
+    # without one, --gpus N > 1 starts its own N ranks before anything touches
+    # the GPU in this process.  A mismatch is an error, never a 1-rank line.
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        log(f"error: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}: launch one rank per GPU "
+            f"(torch.distributed.run --nproc-per-node {args.gpus}) or run without a launcher")
+        sys.exit(2)
+
+    from flyimg_amd.parallel import env_rank_world, make_comm
+
+    rank, world, local_rank = env_rank_world()
+    comm = make_comm()
+    if args.dry_run:
+        return dry_run(args, rank, world, local_rank, comm)
+
     from flyimg_amd import _lib as L
-    from flyimg_amd.parallel import RecordGather, env_rank_world, make_comm
+    from flyimg_amd.parallel import RecordGather
     from flyimg_amd.processor import ImageProcessor, OptionsBag
     from flyimg_amd.runtime import Context
 
-    rank, world, local_rank = env_rank_world()
-    if world != args.gpus and rank == 0:
-        log(f"note: WORLD_SIZE={world} vs --gpus {args.gpus}; using WORLD_SIZE")
-    comm = make_comm()
     if args.workload == "cfg4":
         return run_cfg4(args, rank, world, local_rank, comm)
     W, H, nimg, options, cfg_text = WORKLOADS[args.workload]

@@ -100,8 +100,11 @@ class FileComm:
 
 
 def make_comm():
+    """The control-plane comm of this rank.  ``FI_RDZV_ID`` (set by bench.py's
+    own launcher) names the rendezvous; under ``torch.distributed.run`` the
+    ranks share the agent's PID as parent and the master port."""
     rank, world, _ = env_rank_world()
-    return SoloComm() if world == 1 else FileComm(rank, world)
+    return SoloComm() if world == 1 else FileComm(rank, world, run_id=os.environ.get("FI_RDZV_ID") or None)
 
 
 def shard_lpt(costs: list[float], world: int) -> list[list[int]]:

@@ -64,3 +64,38 @@ def test_cfg4_cpu_baseline_leg_on_a_tiny_list():
 def test_cpu_baseline_max_images_bounds_the_sample():
     r = bench.cpu_baseline(64, 48, "w_32,h_24,c_1", budget_s=30.0, threads=3, max_images=5)
     assert r["images"] == 5 and r["cores"] == 3 and r["wall_s"] < 30.0
+
+
+def _bench(args, **env):
+    import subprocess
+
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "FI_RDZV_ID")}
+    e.update(env)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=e, capture_output=True,
+                          text=True, timeout=120)
+
+
+def test_bench_launches_its_own_ranks_dry_run():
+    """`bench.py --gpus N` without a launcher starts N rank
+    processes; both join the rendezvous and rank 0's one JSON line comes back."""
+    import json
+
+    r = _bench(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks"] == [0, 1] and d["local_ranks"] == [0, 1] and d["distinct_pids"] == 2
+
+
+def test_bench_refuses_world_size_mismatch():
+    r = _bench(["--gpus", "8", "--dry-run"], WORLD_SIZE="1", RANK="0")
+    assert r.returncode != 0 and r.stdout == ""
+    assert "WORLD_SIZE=1 but --gpus 8" in r.stderr
+
+
+def test_bench_launcher_fails_when_a_rank_fails():
+    """a failing rank ends the run non-zero (the others are stopped, not left
+    waiting in the rendezvous), and no JSON line is printed"""
+    r = _bench(["--gpus", "2", "--dry-run"], FI_DRY_RUN_FAIL_RANK="1")
+    assert r.returncode != 0 and r.stdout == ""
