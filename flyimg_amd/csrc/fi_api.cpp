@@ -60,6 +60,8 @@ int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *
                       void *(*alloc)(void *, int, size_t), void *actx, std::string *err);
 int launch_sc_score(hipStream_t s, int mode, const ScDesc *descs, int n, size_t lds, const DevCrop *crops,
                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P, const int32_t *ai);
+int launch_sc_score3(hipStream_t s, const ScDesc *descs, int n, size_t lds, const DevCrop *crops, const ScGroup *groups,
+                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P, const int32_t *ai);
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
 __global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
 // tiled horizontal-first pass 1 (fi_kernels.hip)
@@ -221,6 +223,7 @@ struct fi_ctx {
   int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   bool sc_fd = true;        // FI_SC_FD=0: k_sc_fz instead of its LDS-DMA form k_sc_fd
+  bool sc_mf = true;        // FI_SC_MFMA=0: k_sc_score2 (f64 VALU fast pass) instead of k_sc_score3
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
   DevBuf jpeg[3];           // GPU JPEG decode: upload (compressed data + tables), -, coefficients + planes
   void *jpeg_host = nullptr;  // its pinned staging
@@ -253,6 +256,8 @@ struct fi_ctx {
   std::map<const ScPlan *, ScTabs> sc_at;
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_at;
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp2_at;  // importance - oi
+  // k_sc_score3 B fragments: (table, nx, nslot, step) -> heap offset + the table's digit sums / q
+  std::map<std::tuple<const std::vector<double> *, int, int, int>, std::pair<int32_t, ScoreBTab>> sgb_at;
   std::map<const VmV *, std::array<int32_t, 8>> vv_at;
   std::map<const VrV *, std::array<int32_t, 4>> vr_at;    // rows, bmeta, w128, frag
   std::map<const MfmaH *, std::array<int32_t, 6>> mh_at;  // wsum, frag, s0, lut, frag2, wsum2
@@ -454,6 +459,7 @@ static void heap_reset(fi_ctx *c) {
   c->sc_at.clear();
   c->imp_at.clear();
   c->imp2_at.clear();
+  c->sgb_at.clear();
   c->vv_at.clear();
   c->vr_at.clear();
   c->mh_at.clear();
@@ -580,9 +586,111 @@ static void add_axis_f64(fi_ctx *c, Exec &E, const AxisTable *t, DevAxis *d) {
 struct ScLaunchData {
   std::vector<ScDesc> descs;
   std::vector<DevCrop> crops;  // one list per distinct plan, shared by its images
+  std::vector<ScGroup> groups; // k_sc_score3 groups, shared like the crops
   int nscores = 0;             // per-image CropScore slots
   std::vector<const ScPlan *> plans;
 };
+
+// k_sc_score3 groups of one plan's crops (fi_internal.h ScGroup): per
+// importance table, the distinct x origins in chunks of 16 (M rows) times the
+// y origins in chunks of kSgSlots (`step` apart: crops() walks a full grid per
+// scale).  The plan keeps k_sc_score2 when any condition fails: more than
+// kSgMax groups, x origins not 8-B aligned (two ds_read_b64 per fragment),
+// windows wider than kSgMaxKs k-steps or of more than 2^17 pixels (int32
+// sums of 2^14-bounded products), or planes beyond the LDS.
+template <class ImpOf, class Placed>
+static void plan_score_groups(fi_ctx *c, Exec &E, const ScPlan &P, int step, const ImpOf &imp_of, ScLaunchData *L,
+                              Placed *q) {
+  const size_t g0 = L->groups.size();
+  std::vector<ScGroup> gs;
+  std::vector<std::array<int, 3>> where(P.crops.size(), {-1, -1, -1});
+  std::vector<std::pair<uint64_t, uint64_t>> order;
+  for (const CropHost &ch : P.crops) {
+    const auto k = std::make_pair(dbits(ch.fw), dbits(ch.fh));
+    if (std::find(order.begin(), order.end(), k) == order.end()) order.push_back(k);
+  }
+  int tail = 0;
+  for (const auto &k : order) {
+    const auto &t = imp_of.at(k);
+    const std::vector<double> *tab = std::get<0>(t);
+    const int nx = std::get<1>(t), ny = std::get<2>(t);
+    if ((int64_t)nx * ny >= (1 << 17)) return;
+    std::vector<int> xs, ys;
+    for (const CropHost &ch : P.crops)
+      if (std::make_pair(dbits(ch.fw), dbits(ch.fh)) == k) {
+        xs.push_back(ch.x0);
+        ys.push_back(ch.y0);
+      }
+    std::sort(xs.begin(), xs.end());
+    xs.erase(std::unique(xs.begin(), xs.end()), xs.end());
+    std::sort(ys.begin(), ys.end());
+    ys.erase(std::unique(ys.begin(), ys.end()), ys.end());
+    for (size_t i = 1; i < ys.size(); i++)
+      if (ys[i] - ys[i - 1] != step) return;
+    for (int x : xs)
+      if (x % 8) return;
+    for (size_t xa = 0; xa < xs.size(); xa += 16)
+      for (size_t ya = 0; ya < ys.size(); ya += kSgSlots) {
+        const int nm = (int)std::min<size_t>(16, xs.size() - xa), nslot = (int)std::min<size_t>(kSgSlots, ys.size() - ya);
+        const auto bk = std::make_tuple(tab, nx, nslot, step);
+        auto bt = c->sgb_at.find(bk);
+        if (bt == c->sgb_at.end()) {
+          ScoreBTab b;
+          sc_score_btab(*tab, nx, ny, E.params.outside_importance, nslot, step, &b);
+          int32_t off = -1;
+          if (b.ok) {
+            while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
+            off = E.oi();
+            E.ai.insert(E.ai.end(), b.frag.begin(), b.frag.end());
+          }
+          b.frag.clear();
+          bt = c->sgb_at.emplace(bk, std::make_pair(off, std::move(b))).first;
+        }
+        const ScoreBTab &b = bt->second.second;
+        if (!b.ok) return;
+        ScGroup g{};
+        g.bfrag = bt->second.first;
+        g.nrows = b.nrows;
+        g.ks = b.ks;
+        g.ybase = ys[ya];
+        g.nm = nm;
+        g.nslot = nslot;
+        g.q = b.q;
+        g.step = step;
+        for (int m = 0; m < 16; m++) g.x0[m] = xs[xa + std::min(m, nm - 1)];
+        for (int i = 0; i < kSgDigits; i++) g.S[i] = b.S[i];
+        tail = std::max(tail, g.x0[nm - 1] + 64 * g.ks);
+        for (size_t ci = 0; ci < P.crops.size(); ci++) {
+          const CropHost &ch = P.crops[ci];
+          if (std::make_pair(dbits(ch.fw), dbits(ch.fh)) != k) continue;
+          const auto xi = std::find(xs.begin() + xa, xs.begin() + xa + nm, ch.x0);
+          const int yi = (ch.y0 - ys[ya]) / step;
+          if (xi == xs.begin() + xa + nm || ch.y0 < ys[ya] || yi >= nslot) continue;
+          where[ci] = {(int)gs.size(), (int)(xi - (xs.begin() + xa)), yi};
+        }
+        gs.push_back(g);
+      }
+  }
+  if (gs.empty() || (int)gs.size() > kSgMax) return;
+  // LDS: the seven planes (rows of sg_pitch(aw) bytes) and what the last row's
+  // widest fragment reads past them; the maps (exact re-score) and the
+  // cross-wave sums reuse the same space
+  const int pitch = sg_pitch(P.aw);
+  const int64_t lds = std::max<int64_t>({(int64_t)kSgPlanes * P.ah * pitch + std::max(0, tail - pitch) + 16,
+                                         (int64_t)P.aw * P.ah * 4, (int64_t)gs.size() * kSgPlanes * 1024});
+  if (lds > kScore3Lds) return;
+  for (size_t ci = 0; ci < P.crops.size(); ci++) {
+    if (where[ci][0] < 0) return;
+    DevCrop &dc = L->crops[q->crop0 + ci];
+    dc.sg = where[ci][0];
+    dc.sm = where[ci][1];
+    dc.sj = where[ci][2];
+  }
+  q->sg0 = (int32_t)g0;
+  q->nsg = (int32_t)gs.size();
+  q->sg_lds = (int32_t)((lds + 15) & ~15);
+  L->groups.insert(L->groups.end(), gs.begin(), gs.end());
+}
 
 // Plan the smartcrop stage of `items` into E (descriptors, crops, tables,
 // workspace).  Per-item status in status[].  Images sharing a plan (same
@@ -595,6 +703,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
   const bool fast_ok = E.params.skin_bias >= 0 && E.params.saturation_bias >= 0;
   struct Placed {  // per batch: the plan's crop list in this batch's crop array
     int32_t crop0 = 0, ncrops = 0;
+    int32_t sg0 = 0, nsg = 0, sg_lds = 0;  // k_sc_score3 groups (nsg = 0: k_sc_score2)
   };
   std::map<const ScPlan *, Placed> placed;
   for (size_t k = 0; k < items.size(); k++) {
@@ -666,6 +775,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
       }
       std::map<std::pair<uint64_t, uint64_t>, std::tuple<int32_t, int32_t, double>> tab_of;
       std::map<std::pair<uint64_t, uint64_t>, std::pair<int32_t, double>> tab2_of;  // importance - oi
+      std::map<std::pair<uint64_t, uint64_t>, std::tuple<const std::vector<double> *, int, int>> imp_of;
       for (auto &sz : sizes) {
         double fw, fh;
         memcpy(&fw, &sz.first.first, 8);
@@ -706,6 +816,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
           i2 = c->imp2_at.emplace(pk, std::make_pair(off, imax2)).first;
         }
         tab2_of[sz.first] = i2->second;
+        imp_of[sz.first] = std::make_tuple(&iit->second, nx, ny);
       }
       q.crop0 = (int32_t)L->crops.size();
       q.ncrops = (int32_t)P.crops.size();
@@ -730,8 +841,10 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
         dc.ry = ch.ry;
         dc.rw = ch.rw;
         dc.rh = ch.rh;
+        dc.sg = dc.sm = dc.sj = -1;
         L->crops.push_back(dc);
       }
+      if (fast_ok) plan_score_groups(c, E, P, o.step, imp_of, L, &q);
       pp = placed.emplace(&P, q).first;
     }
     const Placed &q = pp->second;
@@ -791,6 +904,9 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.maps = (uint32_t *)take((size_t)P.aw * P.ah * 4);
     d.crop0 = q.crop0;
     d.ncrops = q.ncrops;
+    d.sg0 = q.sg0;
+    d.ngrp = c->sc_mf ? q.nsg : 0;
+    d.sg_lds = q.sg_lds;
     d.score0 = L->nscores;
     L->nscores += q.ncrops;
     L->descs.push_back(d);
@@ -838,12 +954,14 @@ struct ScLaunches {
   int nvq = 0, vq_chunks = 0, vq_lds = 0;
   size_t sl_off = 0, sg_off = 0;   // k_sc_score2 with maps in LDS / global
   int nsl = 0, nsg = 0, sl_px = 0;
+  size_t s3_off = 0, groups_off = 0;  // k_sc_score3 (exact-integer MFMA fast pass)
+  int ns3 = 0, s3_lds = 0;
   size_t crops_off = 0;
 };
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> hm, sl, sg, vq, vm, fz, fd;
+  std::vector<ScDesc> hm, sl, sg, vq, vm, fz, fd, s3;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
     const ScDesc &d = SL.descs[k];
@@ -873,7 +991,10 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
       if (d.pre) svp.push_back((int)k);
       smaps.push_back((int)k);
     }
-    if ((int64_t)d.aw * d.ah * 4 <= kScoreLdsMaps) {
+    if (d.ngrp > 0) {
+      s3.push_back(d);
+      X->s3_lds = std::max(X->s3_lds, d.sg_lds);
+    } else if ((int64_t)d.aw * d.ah * 4 <= kScoreLdsMaps) {
       sl.push_back(d);
       X->sl_px = std::max(X->sl_px, d.aw * d.ah);
     } else {
@@ -900,6 +1021,11 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->nsl = (int)sl.size();
   X->sg_off = B.addv(sg);
   X->nsg = (int)sg.size();
+  X->s3_off = B.addv(s3);
+  X->ns3 = (int)s3.size();
+  c->stats["sc_score_mfma"].launches += X->ns3;  // images per score kernel (fi_kernel_stats)
+  c->stats["sc_score_valu"].launches += X->nsl + X->nsg;
+  X->groups_off = B.addv(SL.groups);
   X->crops_off = B.addv(SL.crops);
 }
 static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &X, const int32_t *ai,
@@ -946,6 +1072,9 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
                         results, PD, ai) != 0)
       return set_err(FI_EDEVICE, "k_sc_score2 launch rejected (%d px)", X.sl_px);
     (void)launch_sc_score(st, 0, (const ScDesc *)(ab + X.sg_off), X.nsg, 0, crops, ad, scores, results, PD, ai);
+    if (launch_sc_score3(st, (const ScDesc *)(ab + X.s3_off), X.ns3, (size_t)X.s3_lds, crops,
+                         (const ScGroup *)(ab + X.groups_off), ad, scores, results, PD, ai) != 0)
+      return set_err(FI_EDEVICE, "k_sc_score3 launch rejected (%d B LDS)", X.s3_lds);
   }
   HIP_TRY(hipGetLastError());
   return FI_OK;
@@ -2076,7 +2205,7 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
     HIP_TRY(hipEventRecord(S.rs_done, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->sc_stream, S.rs_done, 0));
   }
-  if (K.SX.nsl + K.SX.nsg > 0) {
+  if (K.SX.nsl + K.SX.nsg + K.SX.ns3 > 0) {
     const int rc = enqueue_sc(c, c->sc_stream, ab, K.SX, ai, ad, (CropScore *)(wb + Bp.scores_off),
                               (ScResult *)(wb + Bp.results_off), PD);
     if (rc) return rc;
@@ -2750,6 +2879,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';
+  if (const char *e = getenv("FI_SC_MFMA")) c->sc_mf = e[0] == '1';
   if (const char *e = getenv("FI_VR_MAX_CLASSES")) c->vr_max_classes = atoi(e);
   if (const char *e = getenv("FI_VM_LPT")) c->vm_lpt = e[0] == '1';
   if (const char *e = getenv("FI_RES_ALIGN")) c->res_align = std::max(1, atoi(e));

@@ -85,6 +85,8 @@ struct DevCrop {
   double imax2;           // max |importance - outside_importance| over the table2
   int32_t table2;         // arena offset (double units): fl(importance - outside_importance), rows of
   int32_t table2_w;       //   table2_w = table_w rounded up to 64 (zeros past table_w)
+  int32_t sg, sm, sj;     // k_sc_score3: group (within the image's), M row (x origin), y slot
+  int32_t pad;
 };
 
 struct ScDesc {
@@ -117,6 +119,8 @@ struct ScDesc {
   double T[3];         // unused on host; device scratch
   int32_t result;      // index into result array
   int32_t exact_all;
+  int32_t sg0, ngrp;   // k_sc_score3 groups (batch group array); ngrp = 0: k_sc_score2
+  int32_t sg_lds, sg_pad;  // its dynamic LDS
 };
 
 // smartcrop prescale planning (fi_plan.cpp plan_sc_prep): kPrepRows rows per
@@ -169,6 +173,31 @@ __host__ __device__ inline int fd_lds(int W, int PP, int aw, int ah) {
 // bounds / candidate list stay in LDS (more: the image's CropScore slots).
 constexpr int kScoreLdsMaps = 112 * 1024;
 constexpr int kScoreMaxCrops = 1024;
+// k_sc_score3: the fast pass as exact-integer MFMA (v_mfma_i32_16x16x64_i8).
+// Crops of one importance table form groups: up to 16 x origins (the M rows)
+// x up to kSgSlots y origins `step` apart (N columns = kSgDigits balanced
+// base-256 digits of Tq = rint((importance - oi) 2^q) per slot).  The image's
+// maps enter as seven signed-byte planes (value - 128) in LDS: edge, skin,
+// sat, and the low / high bytes of skin * edge and sat * edge; per row of the
+// group's rows and 64-column k-step, D[limb] += A(16 x origins x 64 px of
+// that plane) B(64 px x 16 (digit, slot)).  Every sum is an exact int32; the
+// host B fragments are [nrows][ks][64 lanes][16 B].
+constexpr int kSgSlots = 3;
+constexpr int kSgDigits = 5;
+constexpr int kSgPlanes = 7;
+constexpr int kSgMax = 2;          // groups per image (accumulators in registers)
+constexpr int kSgMaxKs = 3;        // 64-px k-steps per window row
+constexpr int kSgMaxCrops = kSgMax * 16 * kSgSlots;
+constexpr int kScore3Lds = 160 * 1024 - 4608;  // dynamic LDS cap (k_sc_score3 has 4384 B of static LDS)
+__host__ __device__ inline int sg_pitch(int aw) { return (aw + 7) & ~7; }
+struct ScGroup {
+  int32_t bfrag;                // ai offset (16-B aligned) of the B fragments
+  int32_t nrows, ks, ybase;     // analysed rows [ybase, ybase + nrows)
+  int32_t nm, nslot, q, step;   // x origins used, y slots, Tq = rint((imp - oi) 2^q), slot spacing
+  int32_t x0[16];               // x origin of M row m (rows >= nm repeat the last)
+  int32_t S[kSgDigits];         // sum of each digit over the window (the p - 128 bias)
+  int32_t pad[3];
+};
 
 // v_mfma_i32_16x16x64_i8 operand map (pinned by tools/mfma_probe.hip): lane l
 // holds A[l & 15][k] and B[k][l & 15] for its 16 fragment bytes j, with

@@ -1216,6 +1216,56 @@ void sc_importance_table(const fi_smartcrop_params &P, double fw, double fh, int
     }
 }
 
+// k_sc_score3's B fragments (fi_internal.h ScGroup, v_mfma_i32_16x16x64_i8:
+// lane l holds B[k = mfma_i8_k(l, j)][n = l & 15]).  Column n = digit n % 5 of
+// slot n / 5.  Tq is formed exactly: imp 2^q and oi 2^q are doubles scaled by
+// a power of two, their difference is exact in long double (|.| < 2^44 with
+// no bit below 2^-10), then rounded once, so |Tq 2^-q - (imp - oi)| <= 2^-q-1.
+void sc_score_btab(const std::vector<double> &imp, int nx, int ny, double oi, int nslot, int step, ScoreBTab *out) {
+  *out = ScoreBTab();
+  if (nx <= 0 || ny <= 0 || nslot < 1 || nslot > kSgSlots) return;
+  double m = 0;
+  for (double v : imp) m = std::max(m, std::fabs(v - oi));
+  int q = 38;
+  while (q > 0 && std::ldexp(m, q) * (1 + 1e-9) + 1 >= std::ldexp(1.0, 38) * 1.9) q--;
+  const int ks = (nx + 63) / 64;
+  if (ks > kSgMaxKs) return;
+  std::vector<std::array<int8_t, kSgDigits>> dg((size_t)nx * ny);
+  for (int v = 0; v < ny; v++)
+    for (int u = 0; u < nx; u++) {
+      const long double a = (long double)std::ldexp(imp[(size_t)v * nx + u], q);
+      const long double b = (long double)std::ldexp(oi, q);
+      int64_t x = (int64_t)std::llrintl(a - b);
+      auto &d = dg[(size_t)v * nx + u];
+      for (int i = 0; i < kSgDigits; i++) {
+        const int64_t r = ((x + 128) & 255) - 128;
+        d[i] = (int8_t)r;
+        out->S[i] += (int32_t)r;
+        x = (x - r) / 256;
+      }
+      if (x != 0) return;  // |Tq| beyond five digits (cannot happen with q above)
+    }
+  out->q = q;
+  out->ks = ks;
+  out->nrows = ny + step * (nslot - 1);
+  out->frag.assign((size_t)out->nrows * ks * 256, 0);
+  for (int r = 0; r < out->nrows; r++)
+    for (int t = 0; t < ks; t++) {
+      uint8_t *f = reinterpret_cast<uint8_t *>(&out->frag[((size_t)r * ks + t) * 256]);
+      for (int l = 0; l < 64; l++) {
+        const int n = l & 15, slot = n / kSgDigits, digit = n % kSgDigits;
+        if (slot >= nslot) continue;
+        const int v = r - step * slot;
+        if (v < 0 || v >= ny) continue;
+        for (int j = 0; j < 16; j++) {
+          const int u = 64 * t + mfma_i8_k(l, j);
+          if (u < nx) f[l * 16 + j] = (uint8_t)dg[(size_t)v * nx + u][digit];
+        }
+      }
+    }
+  out->ok = true;
+}
+
 // ---- ScaleImage contribution lists (resize.c ScaleImage; oracle
 // or_im_scale_q16 is the literal loop) ----------------------------------------
 void im_scale_rows(int H, int oh, ScaleList *L) {

@@ -218,6 +218,17 @@ void plan_sc_prep(ScPlan *p);
 int plan_sc(int W, int H, int target_w, int target_h, const fi_smartcrop_options &o, ScPlan *p);
 void sc_importance_table(const fi_smartcrop_params &P, double fw, double fh, int nx, int ny,
                          std::vector<double> *out);
+// k_sc_score3's B fragments of one importance table (fi_internal.h ScGroup):
+// Tq(u, v) = rint((imp(u, v) - oi) 2^q) as kSgDigits balanced signed base-256
+// digits, q the largest that keeps |Tq| < 2^38.9; rows r of a group with
+// `nslot` y origins `step` apart hold window row r - step j in slot j.
+struct ScoreBTab {
+  bool ok = false;
+  int q = 0, nrows = 0, ks = 0;
+  int32_t S[5] = {0, 0, 0, 0, 0};  // sum over the window of each digit
+  std::vector<int32_t> frag;       // [nrows][ks][64 lanes][16 B]
+};
+void sc_score_btab(const std::vector<double> &imp, int nx, int ny, double oi, int nslot, int step, ScoreBTab *out);
 // or_pil_coeffs equivalent (Resample.c precompute_coeffs + normalize_coeffs_8bpc)
 int pil_coeffs(int in_size, float in0, float in1, int out_size, std::vector<int32_t> *bounds,
                std::vector<int32_t> *kk);

@@ -1405,6 +1405,307 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
 }
 
 // ---------------------------------------------------------------------------
+// k_sc_score3: k_sc_score2's fast pass as exact-integer MFMA (fi_internal.h
+// ScGroup).  One 16-wave workgroup per image:
+//   1. the maps -> seven signed-byte planes in LDS (edge, skin, sat and the
+//      low / high bytes of skin * edge, sat * edge, each as value - 128) and
+//      the f64 image totals of the three terms (the outside part);
+//   2. the waves take the groups' rows r = wave, wave + 16, ...: per 64-px
+//      k-step, the B fragment (digits of Tq over that row segment, one per
+//      y slot) from the host table, and per plane one MFMA whose A rows are
+//      the 16 x origins' 64 pixels -- D[plane][x origin][digit, slot] sums
+//      sum_window Tq_digit (value - 128) exactly in int32;
+//   3. cross-wave sums in LDS (the planes are dead), then per crop
+//        sum_in Tq x = sum_digit 256^digit D + 128 sum_window Tq
+//      for x = edge, skin, sat, skin * edge, sat * edge, and the three terms
+//        detail     = 2^-q sum Tq e / 255
+//        skin       = 2^-q (sum Tq s e / 65025 + skin_bias sum Tq s / 255)
+//        saturation = 2^-q (sum Tq t e / 65025 + sat_bias sum Tq t / 255)
+//      are the exact-real sums of (importance - oi) a over the window, up to
+//      the quantisation of Tq; F = that + oi total(a) as in k_sc_score2;
+//   4. the rigorous bound, candidates, the exact sequential re-score and the
+//      argmax exactly as k_sc_score2 (maps reloaded into LDS when needed).
+// Bound per term (a >= 0: biases >= 0, host-checked):
+//   |python - F| <= [2 gamma(n+5) (imax + |oi|) + 2^-(q+1) + |oi| gamma(n+16)]
+//                   total(a) (1 + gamma(n+16)) + gamma(24) |F|_abs
+// python's per-term roundings and sequential sum, the rint of Tq, the parallel
+// image total, and the f64 combination of the integer sums (its absolute
+// value carried alongside).
+constexpr int kS3Threads = 1024;
+constexpr int kS3Waves = kS3Threads / 64;
+
+__global__ __launch_bounds__(kS3Threads) void k_sc_score3(const ScDesc *__restrict__ descs,
+                                                          const DevCrop *__restrict__ crops,
+                                                          const ScGroup *__restrict__ groups,
+                                                          const double *__restrict__ ad,
+                                                          CropScore *__restrict__ scores,
+                                                          ScResult *__restrict__ results, const ScParamsDev P,
+                                                          const int32_t *__restrict__ ai) {
+  typedef __attribute__((address_space(3))) const i32x2 l_ci32x2;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds3[];
+  __shared__ double lut[256];
+  __shared__ double part[kS3Waves][3];
+  __shared__ double T[3];
+  __shared__ double s_tot[kSgMaxCrops];
+  __shared__ double s_bnd[kSgMaxCrops];
+  __shared__ int32_t cand[kSgMaxCrops];
+  __shared__ int32_t ncand_s, first_cand_s;
+  const ScDesc &D = descs[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ncrops = D.ncrops;
+  CropScore *const sco = scores + D.score0;
+  const int W = D.aw, H = D.ah, npx = W * H;
+  const int pitch = sg_pitch(W), psz = H * pitch;
+  const int ng = D.ngrp;
+  const ScGroup *G = groups + D.sg0;
+  const double sb = P.skin_bias, tb = P.saturation_bias, oi = P.outside_importance;
+  if (tid < 256) lut[tid] = (double)tid / 255.0;  // Python int / 255 (correctly rounded)
+  __syncthreads();
+  // ---- 1. planes + image totals ----
+  {
+    const int nq = (W + 3) >> 2;
+    double t0 = 0, t1 = 0, t2 = 0;
+    for (int it = tid; it < H * nq; it += kS3Threads) {
+      const int y = it / nq, x = 4 * (it - y * nq);
+      uint32_t pl[kSgPlanes] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t m = x + k < W ? D.maps[(int64_t)y * W + x + k] : 0u;
+        const uint32_t s = m & 255u, e = (m >> 8) & 255u, t = (m >> 16) & 255u;
+        const uint32_t se = s * e, te = t * e;
+        pl[0] |= e << (8 * k);
+        pl[1] |= s << (8 * k);
+        pl[2] |= t << (8 * k);
+        pl[3] |= (se & 255u) << (8 * k);
+        pl[4] |= (se >> 8) << (8 * k);
+        pl[5] |= (te & 255u) << (8 * k);
+        pl[6] |= (te >> 8) << (8 * k);
+        if (x + k < W) {
+          const double d = lut[e];
+          t0 += d;
+          t1 += lut[s] * (d + sb);
+          t2 += lut[t] * (d + tb);
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < kSgPlanes; p++)
+        *reinterpret_cast<uint32_t *>(lds3 + p * psz + y * pitch + x) = pl[p] ^ 0x80808080u;  // value - 128
+    }
+    t0 = wave_sum(t0);
+    t1 = wave_sum(t1);
+    t2 = wave_sum(t2);
+    if (lane == 0) {
+      part[wave][0] = t0;
+      part[wave][1] = t1;
+      part[wave][2] = t2;
+    }
+    __syncthreads();
+    if (tid < 3) {
+      double s = 0;
+      for (int w = 0; w < kS3Waves; w++) s += part[w][tid];
+      T[tid] = s;
+    }
+  }
+  // ---- 2. MFMA pass: per group, rows wave, wave + 16, ... ----
+  i32x4 acc[kSgMax][kSgPlanes];
+#pragma unroll
+  for (int g = 0; g < kSgMax; g++)
+#pragma unroll
+    for (int p = 0; p < kSgPlanes; p++) acc[g][p] = i32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int g = 0; g < kSgMax; g++) {
+    if (g < ng) {
+      const int nrows = __builtin_amdgcn_readfirstlane(G[g].nrows);
+      const int ks = __builtin_amdgcn_readfirstlane(G[g].ks);
+      const int ybase = __builtin_amdgcn_readfirstlane(G[g].ybase);
+      const int nB = kSgDigits * __builtin_amdgcn_readfirstlane(G[g].nslot);
+      const int xl = G[g].x0[lane & 15];
+      const bool bl = (lane & 15) < nB;
+      const i32x4 *bf = reinterpret_cast<const i32x4 *>(ai + G[g].bfrag);
+      const int aoff = xl + 16 * (lane >> 4);
+      auto loadb = [&](int r, i32x4 *b) {
+#pragma unroll
+        for (int t = 0; t < kSgMaxKs; t++)
+          b[t] = (r < nrows && t < ks && bl) ? bf[((int64_t)r * ks + t) * 64 + lane] : i32x4{0, 0, 0, 0};
+      };
+      i32x4 b[kSgMaxKs], bn[kSgMaxKs];
+      loadb(wave, b);
+      for (int r = wave; r < nrows; r += kS3Waves) {
+        loadb(r + kS3Waves, bn);  // the next row's fragments in flight
+        const uint8_t *rowp = lds3 + (ybase + r) * pitch + aoff;
+#pragma unroll
+        for (int t = 0; t < kSgMaxKs; t++) {
+          if (t < ks) {
+#pragma unroll
+            for (int p = 0; p < kSgPlanes; p++) {
+              const uint8_t *a = rowp + p * psz + 64 * t;
+              const i32x2 lo = *(l_ci32x2 *)(const __attribute__((address_space(3))) uint8_t *)a;
+              const i32x2 hi = *(l_ci32x2 *)(const __attribute__((address_space(3))) uint8_t *)(a + 8);
+              acc[g][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(i32x4{lo.x, lo.y, hi.x, hi.y}, b[t], acc[g][p], 0,
+                                                                0, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < kSgMaxKs; t++) b[t] = bn[t];
+      }
+    }
+  }
+  // ---- 3. cross-wave sums (the planes are dead), then per crop ----
+  __syncthreads();
+  int32_t *red = reinterpret_cast<int32_t *>(lds3);  // [g][plane][16 x origins][16 (digit, slot)]
+  auto red_at = [&](int g, int p, int i) { return ((g * kSgPlanes + p) * 16 + 4 * (lane >> 4) + i) * 16 + (lane & 15); };
+  if (wave == 0) {
+#pragma unroll
+    for (int g = 0; g < kSgMax; g++)
+      if (g < ng)
+#pragma unroll
+        for (int p = 0; p < kSgPlanes; p++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) red[red_at(g, p, i)] = acc[g][p][i];
+  }
+  __syncthreads();
+  if (wave != 0) {
+#pragma unroll
+    for (int g = 0; g < kSgMax; g++)
+      if (g < ng)
+#pragma unroll
+        for (int p = 0; p < kSgPlanes; p++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) atomicAdd(&red[red_at(g, p, i)], acc[g][p][i]);
+  }
+  __syncthreads();
+  const double u = 1.1102230246251565e-16;  // 2^-53
+  auto gam = [&](double n) { return n * u / (1.0 - n * u); };
+  const double aoi = fabs(oi);
+  const double wd = P.detail_weight, ws = P.skin_weight, wt = P.saturation_weight;
+  for (int c = tid; c < ncrops; c += kS3Threads) {
+    const DevCrop cr = crops[D.crop0 + c];
+    const ScGroup &Gr = G[cr.sg];
+    double V[kSgPlanes], A[kSgPlanes];
+#pragma unroll
+    for (int p = 0; p < kSgPlanes; p++) {
+      V[p] = 0;
+      A[p] = 0;
+#pragma unroll
+      for (int k = 0; k < kSgDigits; k++) {
+        const double v = ldexp((double)red[((cr.sg * kSgPlanes + p) * 16 + cr.sm) * 16 + kSgDigits * cr.sj + k], 8 * k);
+        V[p] += v;
+        A[p] += fabs(v);
+      }
+    }
+    double S = 0, AS = 0;
+#pragma unroll
+    for (int k = 0; k < kSgDigits; k++) {
+      const double v = ldexp(128.0 * (double)Gr.S[k], 8 * k);
+      S += v;
+      AS += fabs(v);
+    }
+    // sum_window Tq x (x = e, s, t, s e, t e) and their absolute counterparts
+    const double xe = V[0] + S, xs = V[1] + S, xt = V[2] + S;
+    const double xse = 256.0 * (V[4] + S) + (V[3] + S), xte = 256.0 * (V[6] + S) + (V[5] + S);
+    const double ae = A[0] + AS, as = A[1] + AS, at = A[2] + AS;
+    const double ase = 256.0 * (A[4] + AS) + (A[3] + AS), ate = 256.0 * (A[6] + AS) + (A[5] + AS);
+    const double sc = ldexp(1.0, -Gr.q);
+    const double Fd = xe * sc / 255.0 + oi * T[0];
+    const double Fs = (xse / 65025.0 + sb * xs / 255.0) * sc + oi * T[1];
+    const double Ft = (xte / 65025.0 + tb * xt / 255.0) * sc + oi * T[2];
+    const double Ad = ae * sc / 255.0 + aoi * T[0];
+    const double As = (ase / 65025.0 + sb * as / 255.0) * sc + aoi * T[1];
+    const double At = (ate / 65025.0 + tb * at / 255.0) * sc + aoi * T[2];
+    const double nn = (double)npx;
+    const double kb = (2.0 * gam(nn + 5.0) * (cr.imax + aoi) + ldexp(1.0, -Gr.q - 1) + aoi * gam(nn + 16.0)) *
+                      (1.0 + gam(nn + 16.0));
+    const double Ed = kb * T[0] + gam(24.0) * Ad, Es = kb * T[1] + gam(24.0) * As, Et = kb * T[2] + gam(24.0) * At;
+    const double area = cr.fw * cr.fh;
+    const double tot = (Fd * wd + Fs * ws + Ft * wt) / area;
+    const double mag = fabs(wd) * (fabs(Fd) + Ed) + fabs(ws) * (fabs(Fs) + Es) + fabs(wt) * (fabs(Ft) + Et);
+    const double B = ((fabs(wd) * Ed + fabs(ws) * Es + fabs(wt) * Et) * (1.0 + 16.0 * u) + 16.0 * u * mag) /
+                     area * 1.01;
+    s_tot[c] = tot;
+    s_bnd[c] = B;
+    CropScore &o = sco[c];
+    o.detail = Fd;
+    o.saturation = Ft;
+    o.skin = Fs;
+    o.total = tot;
+    o.bound = B;
+    o.exact = 0;
+  }
+  __syncthreads();
+  // ---- 4. candidates, exact re-score, argmax (k_sc_score2's non-"big" path) ----
+  if (tid == 0) {
+    double best_lo = -1.0e308;
+    for (int c = 0; c < ncrops; c++) best_lo = fmax(best_lo, s_tot[c] - s_bnd[c]);
+    int k = 0, first = -1;
+    for (int c = 0; c < ncrops; c++)
+      if (D.exact_all || s_tot[c] + s_bnd[c] >= best_lo) {
+        if (first < 0) first = c;
+        cand[k++] = c;
+      }
+    ncand_s = k;
+    first_cand_s = first;
+  }
+  __syncthreads();
+  const int ncand = ncand_s;
+  const bool need_exact = D.exact_all || ncand > 1;
+  if (need_exact) {
+    uint32_t *smaps = reinterpret_cast<uint32_t *>(lds3);
+    for (int k = tid; k < npx; k += kS3Threads) smaps[k] = D.maps[k];
+    __syncthreads();
+    for (int k = tid; k < ncand; k += kS3Threads) {
+      const int c = cand[k];
+      const DevCrop cr = crops[D.crop0 + c];
+      const double *tab = ad + cr.table;
+      double skin = 0, detail = 0, sat = 0;
+      for (int y = 0; y < H; y++) {
+        const bool yin = y >= cr.y0 && y < cr.y0 + cr.nin_y;
+        const uint32_t *mrow = smaps + (int64_t)y * W;
+        const int64_t trow = (int64_t)(y - cr.y0) * cr.table_w - cr.x0;
+#pragma unroll 4
+        for (int x = 0; x < W; x++) {
+          const bool in = yin && x >= cr.x0 && x < cr.x0 + cr.nin_x;
+          const double tv = tab[in ? trow + x : 0];
+          const double imp = in ? tv : oi;
+          const uint32_t m = mrow[x];
+          const double det = lut[(m >> 8) & 255];
+          skin = skin + lut[m & 255] * (det + sb) * imp;
+          detail = detail + det * imp;
+          sat = sat + lut[(m >> 16) & 255] * (det + tb) * imp;
+        }
+      }
+      const double tot = (detail * wd + skin * ws + sat * wt) / (cr.fw * cr.fh);
+      s_tot[c] = tot;
+      CropScore &o = sco[c];
+      o.detail = detail;
+      o.saturation = sat;
+      o.skin = skin;
+      o.total = tot;
+      o.bound = 0;
+      o.exact = 1;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int top = first_cand_s;
+    double best = s_tot[top];
+    if (need_exact) {
+      best = -9223372036854775807.0;  // -sys.maxsize; strict > keeps the first max
+      for (int k = 0; k < ncand; k++) {
+        const int c = cand[k];
+        if (s_tot[c] > best) {
+          best = s_tot[c];
+          top = c;
+        }
+      }
+    }
+    results[D.result].top = top;
+    results[D.result].n_candidates = ncand;
+    results[D.result].total = best;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // convert <out> -crop WxH+X+Y with W = w + x, H = h + y as smartcrop.py prints
 // them (:372-377); CropImage clips to the image.  kApplyBands workgroups per
 // image, rows interleaved.
@@ -1547,6 +1848,14 @@ int launch_sc_score(hipStream_t s, int mode, const ScDesc *descs, int n, size_t 
     hipLaunchKernelGGL((k_sc_score2<0>), dim3(n), dim3(kScoreThreads), 0, s, descs, crops, ad, scores, results, P,
                        ai);
   }
+  return 0;
+}
+int launch_sc_score3(hipStream_t s, const ScDesc *descs, int n, size_t lds, const DevCrop *crops, const ScGroup *groups,
+                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P, const int32_t *ai) {
+  if (n <= 0) return 0;
+  if (lds > (size_t)kScore3Lds) return -1;
+  hipLaunchKernelGGL(k_sc_score3, dim3(n), dim3(kS3Threads), lds, s, descs, crops, groups, ad, scores, results, P,
+                     ai);
   return 0;
 }
 int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results) {

@@ -48,12 +48,13 @@ _ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_S
 PATHS = {
     # default kernels: k_rs_vr (block-major persistent MFMA resample; k_rs_vm
     # where its tables do not fit) / k_rs_hv; k_sc_fd fused prescale + maps
-    # (source rows by LDS-DMA); k_sc_score2
+    # (source rows by LDS-DMA); k_sc_score3 (exact-integer MFMA score fast pass)
     "vr": dict(_ENV),
     # the same with k_sc_fz (register-staged source rows, two workgroups per CU)
     "fz": dict(_ENV, FI_SC_FD="0"),
-    # the fallbacks: k_rs_vm streaming resample; k_sc_hmfma + k_sc_vq (H-stage rows through HBM)
-    "vm": dict(_ENV, FI_VR_RS="0", FI_DISABLE_SC_FZ="1"),
+    # the fallbacks: k_rs_vm streaming resample; k_sc_hmfma + k_sc_vq (H-stage rows through HBM);
+    # k_sc_score2 (f64 VALU score fast pass)
+    "vm": dict(_ENV, FI_VR_RS="0", FI_DISABLE_SC_FZ="1", FI_SC_MFMA="0"),
     # generic kernels: two-pass resample; per-row prescale/maps kernels
     "generic": dict(_ENV, FI_FORCE_GENERIC="1"),
 }

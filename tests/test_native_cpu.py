@@ -28,7 +28,7 @@ def test_mfma_tables_exact():
 
 @pytest.mark.parametrize("src,kernels", [
     ("fi_vr.hip", ["_ZN2fi7k_rs_vrILi0EE"]),
-    ("fi_smartcrop.hip", ["_ZN2fi11k_sc_score2ILi1EE"]),
+    ("fi_smartcrop.hip", ["_ZN2fi11k_sc_score2ILi1EE", "_ZN2fi11k_sc_score3E"]),
 ])
 def test_hot_kernels_do_not_spill(src, kernels):
     """The production kernels of the hot path keep every value in registers: a
