@@ -147,10 +147,11 @@ bool build_hv_v(const AxisTable &v, HvV *m);
 // follows the largest weight, so the precision relative to it is ~15 bits at
 // any factor), each output's W adjusted to keep its sum (quant_axis), so a
 // block costs 4 MFMAs per column tile instead of 6.  shift >= kVrMinShift,
-// else no k_rs_vr.  Outputs stay within +-1 LSB of the f64 resample and
-// >= 99.9 % identical to it in the model of tools/limbs_eval.py;
-// tests/test_gpu_vr.py checks every k_rs_vr class against k_rs_vm's 22-bit
-// path and the oracle.
+// else no k_rs_vr.  tests/native/vr_quant_bound.cpp rebuilds every table of the
+// BASELINE geometries and 200 random ones from its fragments and bounds the
+// worst case over all 8-bit inputs against IM's f64 weights: <= 0.1 LSB before
+// the final rounding (so within +-1 LSB); tests/test_gpu_vr.py checks every
+// k_rs_vr class against k_rs_vm's 22-bit path and the oracle.
 constexpr int kVrMaxShift = 22;
 constexpr int kVrMinShift = 15;
 struct VrV {

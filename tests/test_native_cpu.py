@@ -26,6 +26,33 @@ def test_mfma_tables_exact():
         assert "OK (0 failures)" in r.stdout
 
 
+def test_vr_two_limb_quantisation_bound():
+    """k_rs_vr's two-limb weights (fi_plan.cpp vr_quant / quant_axis): every
+    table of the BASELINE geometries and 200 random ones is rebuilt from its
+    fragment bytes, its integer algebra re-derived (row sums 2^shift, the
+    constant 128 * 2^shift bias, the Q16 hi/lo split), and the worst case over
+    all 8-bit inputs of |kernel - ImageMagick f64| bounded per output: < 1 LSB
+    (tests/native/vr_quant_bound.cpp)."""
+    import re
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "vqb")
+        subprocess.run([hipcc, "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests/native/vr_quant_bound.cpp"),
+                        os.path.join(ROOT, "flyimg_amd/csrc/fi_plan.cpp"), "-o", exe],
+                       check=True, capture_output=True, timeout=300)
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK (0 failures)" in r.stdout
+    worst = float(re.search(r"worst bound ([0-9.]+) LSB", r.stdout).group(1))
+    assert worst < 1.0
+    for cfg in ("cfg1", "cfg2", "cfg3", "cfg5"):
+        assert re.search(cfg + r" .*bound ([0-9.]+) LSB", r.stdout), cfg
+
+
 @pytest.mark.parametrize("src,kernels", [
     ("fi_vr.hip", ["_ZN2fi7k_rs_vrILi0EE"]),
     ("fi_smartcrop.hip", ["_ZN2fi11k_sc_score2ILi1EE", "_ZN2fi11k_sc_score3E"]),
