@@ -470,12 +470,26 @@ static void tap_range(const AxisTable &t, const std::vector<int32_t> &idx, int o
       *hi = std::max(*hi, li);
     }
 }
+// The 2^22-scaled weights of k_rs_vm (and k_sc-independent: AxisTable::w
+// order): k_rs_vr's two-limb weights (vr_quant, shift s) times 2^(22 - s) when
+// the axis has them, else rint(w 2^22).  k_rs_vm's float conversions then see
+// k_rs_vr's integer sums times a power of two, so the two kernels give the
+// same pixels bit for bit and an image's output does not depend on which of
+// them its batch ran (the choice is per batch: classes, ring fit).
+int axis_q22(const AxisTable &t, std::vector<int32_t> *q) {
+  std::vector<int32_t> wq;
+  const int s = vr_quant(t, &wq);
+  q->resize(t.w.size());
+  for (size_t i = 0; i < t.w.size(); i++) (*q)[i] = s > 0 ? wq[i] * (1 << (kMfmaWBits - s)) : quant_w(t.w[i]);
+  return s > 0 ? s : kMfmaWBits;
+}
 // quantized weight of output o at list index li (0 if not a tap)
-static int32_t tap_w(const AxisTable &t, const std::vector<int32_t> &list, int o, int li) {
+static int32_t tap_w(const AxisTable &t, const std::vector<int32_t> &q22, const std::vector<int32_t> &list, int o,
+                     int li) {
   if (li < 0 || li >= (int)list.size()) return 0;
   const int j = list[li] - t.start[o];
   if (j < 0 || j >= t.count[o]) return 0;
-  return quant_w(t.w[t.woff[o] + j]);
+  return q22[t.woff[o] + j];
 }
 static int32_t tap_wq(const AxisTable &t, const std::vector<int32_t> &wq, const std::vector<int32_t> &list, int o,
                       int li) {
@@ -501,9 +515,11 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
     if (hi[x] < lo[x]) return false;  // an output px without taps
     if (x > 0 && (lo[x] < lo[x - 1] || hi[x] < hi[x - 1])) return false;  // not monotone
   }
+  std::vector<int32_t> q22;
+  axis_q22(h, &q22);
   m->wsum.assign(nx, 0);
   for (int x = 0; x < nx; x++)
-    for (int j = 0; j < h.count[x]; j++) m->wsum[x] += quant_w(h.w[h.woff[x] + j]);
+    for (int j = 0; j < h.count[x]; j++) m->wsum[x] += q22[h.woff[x] + j];
   std::vector<int32_t> wq2;
   m->shift2 = vr_quant(h, &wq2);
   m->wsum2.assign(nx, 0);
@@ -569,7 +585,7 @@ bool build_mfma_h(const AxisTable &h, MfmaH *m, int max_nx) {
             const int x = x0 + 16 * ob + (l & 15);
             const int li = S.c_lo + m->s0[S.s0 + 2 * ob] + 64 * t + mfma_i8_k(l, j);
             int32_t limb[3];
-            limbs3(x < x1 ? tap_w(h, m->cols, x, li) : 0, limb);
+            limbs3(x < x1 ? tap_w(h, q22, m->cols, x, li) : 0, limb);
             put_frag(m->frag, S.frag + (size_t)(ob * S.ks + t) * 3 * 256, l, j, limb);
           }
     S.frag2 = m->frag2.size();
@@ -596,6 +612,8 @@ bool build_vm_v(const AxisTable &v, VmV *m) {
   *m = VmV();
   const int ny = (int)v.start.size();
   if (ny == 0) return false;
+  std::vector<int32_t> q22;
+  axis_q22(v, &q22);
   std::vector<int32_t> idx;
   touched_list(v, &m->rows, &idx);
   const int nl = (int)m->rows.size();
@@ -645,7 +663,7 @@ bool build_vm_v(const AxisTable &v, VmV *m) {
         for (int j = 0; j < 16; j++) {
           const int y = 16 * bb + (l & 15), k = mfma_i8_k(l, j);
           int32_t limb[3];
-          limbs3(y < ny && k < m->pn[p] ? tap_w(v, m->rows, y, m->plo[p] + k) : 0, limb);
+          limbs3(y < ny && k < m->pn[p] ? tap_w(v, q22, m->rows, y, m->plo[p] + k) : 0, limb);
           put_frag(m->frag, (size_t)(p * 2 + s) * 3 * 256, l, j, limb);
         }
     }
@@ -661,7 +679,7 @@ bool build_vm_v(const AxisTable &v, VmV *m) {
   }
   m->w128.assign((size_t)16 * (m->nblk + 2), 0);  // two zero blocks: k_rs_vm loads block b + 2 unconditionally
   for (int y = 0; y < ny; y++)
-    for (int j = 0; j < v.count[y]; j++) m->w128[y] += 128 * quant_w(v.w[v.woff[y] + j]);
+    for (int j = 0; j < v.count[y]; j++) m->w128[y] += 128 * q22[v.woff[y] + j];
   m->row0 = m->rows[0];
   m->rstep = nl > 1 ? m->rows[1] - m->rows[0] : 1;
   for (int k = 1; k < nl && m->rstep > 0; k++)

@@ -168,6 +168,10 @@ struct VrV {
 // quantised weight of the axis fits two signed-byte limbs (hi * 256 + lo, both
 // in [-128, 127]), the weights in *wq (AxisTable::w order); 0 if none
 int vr_quant(const AxisTable &t, std::vector<int32_t> *wq);
+// k_rs_vm's 2^22-scaled weights (AxisTable::w order): vr_quant's times
+// 2^(22 - shift) when the axis has two-limb weights, else rint(w 2^22); returns
+// the shift they carry (22 for the latter)
+int axis_q22(const AxisTable &t, std::vector<int32_t> *q);
 bool build_vr_v(const AxisTable &v, VrV *m);
 
 // Output indices [o0, o1) of a filter pass from `in_sampled` (sampled domain)

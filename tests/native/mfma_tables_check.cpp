@@ -50,6 +50,8 @@ static void check_vm(const AxisTable &v, const char *name) {
     return;
   }
   const int ny = (int)v.start.size(), np = (int)m.plo.size();
+  std::vector<int32_t> q22;  // k_rs_vm carries k_rs_vr's two-limb weights scaled to 2^22 (axis_q22)
+  axis_q22(v, &q22);
   std::mt19937 rng(4321);
   std::vector<int> px(v.src_hi);
   for (auto &x : px) x = (int)(rng() & 255);
@@ -82,7 +84,7 @@ static void check_vm(const AxisTable &v, const char *name) {
         const int y = 16 * b + r;
         if (y >= ny) continue;
         int64_t ref = 0;
-        for (int j = 0; j < v.count[y]; j++) ref += (int64_t)qw(v.w[v.woff[y] + j]) * px[v.start[y] + j];
+        for (int j = 0; j < v.count[y]; j++) ref += (int64_t)q22[v.woff[y] + j] * px[v.start[y] + j];
         CHECK(acc0[r] == ref, "%s: streaming vertical y=%d %lld != %lld", name, y, (long long)acc0[r],
               (long long)ref);
         CHECK(llabs(acc0[r]) < (1ll << 31), "%s: accumulator exceeds int32", name);
@@ -107,6 +109,8 @@ static void check_h(const AxisTable &h, const char *name) {
     return;
   }
   const int nx = (int)h.start.size();
+  std::vector<int32_t> q22;
+  axis_q22(h, &q22);
   std::mt19937 rng(99);
   std::vector<int> V(h.src_hi);
   for (auto &x : V) x = (int)(rng() % 65536);
@@ -154,7 +158,7 @@ static void check_h(const AxisTable &h, const char *name) {
         }
         const int64_t s = 256 * sh + sl + 32896 * (int64_t)m.wsum[x];
         int64_t ref = 0;
-        for (int j = 0; j < h.count[x]; j++) ref += (int64_t)qw(h.w[h.woff[x] + j]) * V[h.start[x] + j];
+        for (int j = 0; j < h.count[x]; j++) ref += (int64_t)q22[h.woff[x] + j] * V[h.start[x] + j];
         CHECK(s == ref, "%s: horizontal x=%d %lld != %lld", name, x, (long long)s, (long long)ref);
         CHECK(llabs(sh) < (1ll << 31) && llabs(sl) < (1ll << 31), "%s: horizontal limb sum exceeds int32", name);
       }

@@ -1,11 +1,10 @@
 """k_rs_vr (the persistent block-major resample, fi_vr.hip) on every geometry
 class it takes: the path actually ran (its image counter rose by the batch),
-the output is within +-1 LSB of k_rs_vm's 22-bit three-limb path and >= 99 %
-identical to it, and within +-1 LSB / >= 98 % exact of the oracle
-(ImageProcessor.php:86 -thumbnail / -resize, IM's VerticalFilter then
-HorizontalFilter).  k_rs_vr quantises the weights to two
-signed-byte limbs (fi_plan.h VrV), k_rs_vm to three, so the two are not
-bit-identical; the tolerance here is the north_star's."""
+the output is bit-identical to k_rs_vm's (which carries k_rs_vr's two-limb
+weights scaled to 2^22, fi_plan.cpp axis_q22 -- so an image's pixels do not
+depend on which kernel its batch took), and within +-1 LSB / >= 98 % exact of
+the oracle (ImageProcessor.php:86 -thumbnail / -resize, IM's VerticalFilter
+then HorizontalFilter)."""
 import numpy as np
 import pytest
 
@@ -77,7 +76,7 @@ def test_vr_takes_the_class_and_matches(pair, W, H, opts, n):
     oa, ra, rca = vm.process(srcs[:len(base)], [op] * len(base))
     assert rca == 0
     for k in range(len(base)):
-        _close(ob[k], oa[k], f"{opts} image {k} vs k_rs_vm", 0.99)
+        assert np.array_equal(ob[k], oa[k]), f"{opts} image {k}: k_rs_vr != k_rs_vm"
         for j in range(k, n, len(base)):  # repeated sources give identical outputs
             assert np.array_equal(ob[j], ob[k])
     if W * H <= 4_000_000:
@@ -103,6 +102,29 @@ def test_vr_mixed_batch(pair):
     oa, _, rca = vm.process(srcs, ops)
     assert rca == 0
     for k in range(len(srcs)):
-        _close(ob[k], oa[k], f"mixed {k} vs k_rs_vm", 0.99)
+        assert np.array_equal(ob[k], oa[k]), f"mixed {k}: k_rs_vr != k_rs_vm"
         if srcs[k].shape[0] * srcs[k].shape[1] <= 4_000_000:
             _close(ob[k], _oracle(srcs[k], ops[k]), f"mixed {k} vs oracle", 0.98)
+
+
+def test_output_independent_of_cobatched_images(pair):
+    """an image's pixels depend only on the image -- alone its batch
+    runs k_rs_vr; inside a batch of more than FI_VR_MAX_CLASSES (8) vertical
+    geometries the batch takes k_rs_vm; the bytes are the same."""
+    vr, _ = pair
+    W, H, opts = 1920, 1080, "w_500,clsp_Gray"
+    src = synth_rgb(W, H, 4242)
+    op = ImageProcessor(OptionsBag(opts), W, H).to_op()
+    before = vr.stats("path_vr")[1]
+    alone, _, rc = vr.process([src], [op])
+    assert rc == 0 and vr.stats("path_vr")[1] == before + 1
+    srcs, ops = [src], [op]
+    for k, (w, h) in enumerate([(1000, 700), (1100, 800), (1300, 900), (1500, 1000), (1700, 1100),
+                                (900, 1200), (1234, 987), (2000, 1500), (777, 555), (1600, 1300)]):
+        srcs.append(synth_rgb(w, h, 500 + k))
+        ops.append(ImageProcessor(OptionsBag("w_%d" % (150 + 10 * k)), w, h).to_op())
+    b_vr, b_vm = vr.stats("path_vr")[1], vr.stats("path_vm")[1]
+    mixed, recs, rc = vr.process(srcs, ops)
+    assert rc == 0 and all(r.status == 0 for r in recs)
+    assert vr.stats("path_vm")[1] - b_vm == len(srcs) and vr.stats("path_vr")[1] == b_vr  # > 8 classes
+    assert np.array_equal(mixed[0], alone[0])
