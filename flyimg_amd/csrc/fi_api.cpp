@@ -1571,13 +1571,13 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
         // the uneven list again, as each k_rs_vr loader wave walks it: class
         // rho = k & 3, entry j = the pair (rows[4 j + rho], rows[4 j + rho + 1]),
         // so a wave's own pairs (4 apart) are 16 consecutive ints per 8 pairs
-        const int n = (int)V.rows.size(), J = (n + 3) / 4 + 16;
+        const int n = (int)V.rows.size(), J = vr_pair_cls_len(n);
         std::vector<int32_t> p4(8 * (size_t)J);
-        for (int rho = 0; rho < 4; rho++)
-          for (int j = 0; j < J; j++) {
-            p4[(size_t)2 * (rho * J + j)] = V.rows[std::min(4 * j + rho, n - 1)];
-            p4[(size_t)2 * (rho * J + j) + 1] = V.rows[std::min(4 * j + rho + 1, n - 1)];
-          }
+        for (int k = 0; k < 4 * J; k++) {  // the pair starting at list row k (fi_internal.h vr_pair_off)
+          const size_t o = (size_t)(vr_pair_off(n, k) - (n + 32));
+          p4[o] = V.rows[std::min(k, n - 1)];
+          p4[o + 1] = V.rows[std::min(k + 1, n - 1)];
+        }
         put(p4);
       }
       align4();

@@ -3,9 +3,12 @@
 // warp-specialised, exact-integer matrix-core pipeline with a BLOCK-MAJOR
 // vertical pass: v_mfma_i32_16x16x64_i8.
 //
-// Same weights, limbs and float conversions as k_rs_vm (bit-identical
-// outputs); what differs is how the vertical pass walks the source rows
-// (fi_plan.h VrV):
+// Weights rint(w 2^s) in two signed-byte limbs, every output row summing to
+// 2^s (fi_plan.cpp vr_quant; bounded against IM's f64 weights by
+// tests/native/vr_quant_bound.cpp).  k_rs_vm carries the same weights scaled
+// to 2^22 in three limbs (axis_q22), so the two kernels give the same pixels;
+// what differs is how the vertical pass walks the source rows (DESIGN.md 3.0,
+// fi_plan.h VrV):
 //
 //  * k_rs_vm cuts the touched rows into pieces of <= 64 rows aligned to
 //    the 16-row output blocks, and every piece feeds two accumulator slots (its
@@ -16,8 +19,9 @@
 //  * here the touched rows stream through a RING of R rows in LDS (LDS-DMA,
 //    loader waves, as far ahead as the ring allows), and phase p computes ONE
 //    output block b from its own window [K0(b), K0(b) + 64 ks) of the ring:
-//    ks <= 2 k-steps x 3 weight limbs into three separate accumulators per
-//    column tile (no shifts; folded once per block), then the Q16 planes.
+//    ks <= 2 k-steps x 2 weight limbs into two separate accumulators per
+//    column tile (folded once per block, the MFMA bias the constant
+//    128 * 2^s), then the Q16 planes.
 //
 //  Roles per phase (one workgroup barrier per phase):
 //    V waves 0-7   block p: vertical MFMAs from the ring (both k-steps' reads
@@ -32,7 +36,9 @@
 //                  record of phase p + 2 (+ the strip's LUT); the end-of-phase
 //                  vmcnt waits exactly for the rows of block p + 1.
 //  Each workgroup walks its own tile range [t0, t1) (host: LPT over the
-//  XCD's workgroups); the touched rows are evenly spaced (build_vr_v).
+//  XCD's workgroups).  Touched rows evenly spaced (rstep > 0) stream from a
+//  base and a step; unevenly spaced ones (ThumbnailImage sampling at a
+//  non-integral step) from the tile's row list, in per-wave pair classes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -360,8 +366,9 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
     // Evenly spaced touched rows (rstep > 0): a loop with no loads, bases linear
     // in the pair index, the chunk swizzle from the ring slot.  Uneven ones
     // (ThumbnailImage sampling at a non-integral step, cfg1's 2000 -> 1250): the
-    // rows come from the touched-row list, 8 entries (two own pairs) per
-    // scalar load, the next group's load in flight while this one is issued.
+    // rows come from the pair-class copy of the touched-row list (vr_pair_off),
+    // PL own pairs (2 PL ints) per scalar load, each load waited for before its
+    // DMAs are issued.
     auto issue_rows = [&](int limit) -> int {
       int n = 0;
       while (rG < limit) {
@@ -377,9 +384,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           // the host's pair list (after the row list and its 32-entry pad):
           // class k0 & 3, own pair m at entry (k0 >> 2) + m, PL pairs per wait
           // (scalar loads complete out of order: each wait is lgkmcnt(0))
-          const int J = ((r_nrows + 3) >> 2) + 16;
-          const WL *lst =
-              reinterpret_cast<const WL *>(ai + r_rows + r_nrows + 32 + 2 * ((k0 & 3) * J + (k0 >> 2)));
+          const WL *lst = reinterpret_cast<const WL *>(ai + r_rows + vr_pair_off(r_nrows, k0));
           for (int j0 = 0; j0 < cnt; j0 += PL) {
             const WL c0 = ldc(lst + j0 / PL);
             const int jn = cnt - j0;

@@ -204,10 +204,11 @@ int fi_host_free(fi_ctx *ctx, void *p);
 int fi_process_batch_device(fi_ctx *ctx, fi_image *imgs, int32_t n);
 /* Asynchronous form of fi_process_batch_device for pipelined serving: plans,
  * uploads and launches the batch, then returns; `imgs` must stay valid until
- * fi_wait().  Batch k+1 is planned on the host while batch k runs on the GPU
- * (two pinned staging slots; a third submit waits for the oldest batch), and
- * batch k's smart-crop stage runs on a second stream concurrently with batch
- * k+1's resample -- so the dst buffers of two in-flight batches must not
+ * fi_wait().  Batch k+1 is planned and uploaded on the host while batch k runs
+ * on the GPU (two pinned staging slots; a third submit waits for the oldest
+ * batch).  Every kernel of both batches runs on the context's one stream, in
+ * submission order (the resample fills every CU, so a second stream only
+ * stretched both stages); the dst buffers of two in-flight batches must not
  * overlap (sources may be shared).
  * fi_wait(ctx, keep) finalizes submitted batches in order -- fills their
  * result fields -- until at most `keep` remain in flight (0 = drain all) and
