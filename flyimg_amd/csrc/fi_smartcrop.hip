@@ -1428,11 +1428,12 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
 // Bound per term (a >= 0: biases >= 0, host-checked):
 //   |python - F| <= [2 gamma(n+5) (imax + |oi|) + 2^-(q+1) + |oi| gamma(n+16)]
 //                   total(a) (1 + gamma(n+16)) + gamma(24) |F|_abs
-// python's per-term roundings and sequential sum, the rint of Tq, the parallel
-// image total, and the f64 combination of the integer sums (its absolute
+// python's per-term roundings and sequential sum, the rint of Tq, the f64
+// image totals (from exact integer sums), and the f64 combination of the integer sums (its absolute
 // value carried alongside).
 constexpr int kS3Threads = 1024;
 constexpr int kS3Waves = kS3Threads / 64;
+constexpr int kS3Pre = 8;  // plane items per thread with their map loads in flight together
 
 __global__ __launch_bounds__(kS3Threads) void k_sc_score3(const ScDesc *__restrict__ descs,
                                                           const DevCrop *__restrict__ crops,
@@ -1444,7 +1445,7 @@ __global__ __launch_bounds__(kS3Threads) void k_sc_score3(const ScDesc *__restri
   typedef __attribute__((address_space(3))) const i32x2 l_ci32x2;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds3[];
   __shared__ double lut[256];
-  __shared__ double part[kS3Waves][3];
+  __shared__ uint32_t ipart[kS3Waves][5];
   __shared__ double T[3];
   __shared__ double s_tot[kSgMaxCrops];
   __shared__ double s_bnd[kSgMaxCrops];
@@ -1462,48 +1463,68 @@ __global__ __launch_bounds__(kS3Threads) void k_sc_score3(const ScDesc *__restri
   if (tid < 256) lut[tid] = (double)tid / 255.0;  // Python int / 255 (correctly rounded)
   __syncthreads();
   // ---- 1. planes + image totals ----
+  // items (row, 4-pixel quad), kS3Pre per thread with every map load in flight
+  // before the first is used; the totals as exact integer sums (sum e, s, t,
+  // s e, t e) turned into the three f64 terms at the end (|error| <= 3 u T)
   {
-    const int nq = (W + 3) >> 2;
-    double t0 = 0, t1 = 0, t2 = 0;
-    for (int it = tid; it < H * nq; it += kS3Threads) {
-      const int y = it / nq, x = 4 * (it - y * nq);
-      uint32_t pl[kSgPlanes] = {0, 0, 0, 0, 0, 0, 0};
+    const int nq = (W + 3) >> 2, nit = H * nq;
+    uint32_t se_s = 0, te_s = 0, e_s = 0, s_s = 0, t_s = 0;
+#pragma unroll 1
+    for (int base = 0; base < nit; base += kS3Pre * kS3Threads) {
+      uint32_t mm[kS3Pre][4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t m = x + k < W ? D.maps[(int64_t)y * W + x + k] : 0u;
-        const uint32_t s = m & 255u, e = (m >> 8) & 255u, t = (m >> 16) & 255u;
-        const uint32_t se = s * e, te = t * e;
-        pl[0] |= e << (8 * k);
-        pl[1] |= s << (8 * k);
-        pl[2] |= t << (8 * k);
-        pl[3] |= (se & 255u) << (8 * k);
-        pl[4] |= (se >> 8) << (8 * k);
-        pl[5] |= (te & 255u) << (8 * k);
-        pl[6] |= (te >> 8) << (8 * k);
-        if (x + k < W) {
-          const double d = lut[e];
-          t0 += d;
-          t1 += lut[s] * (d + sb);
-          t2 += lut[t] * (d + tb);
-        }
+      for (int j = 0; j < kS3Pre; j++) {
+        const int it = base + tid + j * kS3Threads;
+        const int y = it / nq, x = 4 * (it - y * nq);
+#pragma unroll
+        for (int k = 0; k < 4; k++) mm[j][k] = (it < nit && x + k < W) ? D.maps[(int64_t)y * W + x + k] : 0u;
       }
 #pragma unroll
-      for (int p = 0; p < kSgPlanes; p++)
-        *reinterpret_cast<uint32_t *>(lds3 + p * psz + y * pitch + x) = pl[p] ^ 0x80808080u;  // value - 128
+      for (int j = 0; j < kS3Pre; j++) {
+        const int it = base + tid + j * kS3Threads;
+        if (it >= nit) break;
+        const int y = it / nq, x = 4 * (it - y * nq);
+        uint32_t pl[kSgPlanes] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t m = mm[j][k];  // 0 past the row end: adds nothing
+          const uint32_t sk = m & 255u, e = (m >> 8) & 255u, t = (m >> 16) & 255u;
+          const uint32_t se = sk * e, te = t * e;
+          pl[0] |= e << (8 * k);
+          pl[1] |= sk << (8 * k);
+          pl[2] |= t << (8 * k);
+          pl[3] |= (se & 255u) << (8 * k);
+          pl[4] |= (se >> 8) << (8 * k);
+          pl[5] |= (te & 255u) << (8 * k);
+          pl[6] |= (te >> 8) << (8 * k);
+          e_s += e;
+          s_s += sk;
+          t_s += t;
+          se_s += se;
+          te_s += te;
+        }
+#pragma unroll
+        for (int p = 0; p < kSgPlanes; p++)
+          *reinterpret_cast<uint32_t *>(lds3 + p * psz + y * pitch + x) = pl[p] ^ 0x80808080u;  // value - 128
+      }
     }
-    t0 = wave_sum(t0);
-    t1 = wave_sum(t1);
-    t2 = wave_sum(t2);
-    if (lane == 0) {
-      part[wave][0] = t0;
-      part[wave][1] = t1;
-      part[wave][2] = t2;
-    }
+    // wave sums (each < 2^32: <= 22.7 K pixels per image fit k_sc_score3's LDS)
+    uint32_t v5[5] = {e_s, s_s, t_s, se_s, te_s};
+#pragma unroll
+    for (int i = 0; i < 5; i++)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v5[i] += __shfl_xor(v5[i], o, 64);
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 5; i++) ipart[wave][i] = v5[i];
     __syncthreads();
-    if (tid < 3) {
-      double s = 0;
-      for (int w = 0; w < kS3Waves; w++) s += part[w][tid];
-      T[tid] = s;
+    if (tid == 0) {
+      uint64_t S5[5] = {0, 0, 0, 0, 0};
+      for (int w = 0; w < kS3Waves; w++)
+        for (int i = 0; i < 5; i++) S5[i] += ipart[w][i];
+      T[0] = (double)S5[0] / 255.0;
+      T[1] = (double)S5[3] / 65025.0 + sb * ((double)S5[1] / 255.0);
+      T[2] = (double)S5[4] / 65025.0 + tb * ((double)S5[2] / 255.0);
     }
   }
   // ---- 2. MFMA pass: per group, rows wave, wave + 16, ... ----
@@ -1709,7 +1730,10 @@ __global__ __launch_bounds__(kS3Threads) void k_sc_score3(const ScDesc *__restri
 // convert <out> -crop WxH+X+Y with W = w + x, H = h + y as smartcrop.py prints
 // them (:372-377); CropImage clips to the image.  kApplyBands workgroups per
 // image, rows interleaved.
-constexpr int kApplyChunks = 16;  // workgroups per image
+#ifndef FI_APPLY_WG
+#define FI_APPLY_WG 8
+#endif
+constexpr int kApplyChunks = FI_APPLY_WG;  // workgroups per image
 // The output is one contiguous byte array (oh rows of ow * C bytes): 16-byte
 // destination chunks, each assembled from 5 aligned source dwords with
 // v_alignbyte (the crop origin has any byte alignment); chunks that straddle a
@@ -1717,6 +1741,10 @@ constexpr int kApplyChunks = 16;  // workgroups per image
 __device__ __forceinline__ uint32_t ap_align(uint32_t hi, uint32_t lo, uint32_t sh) {
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
+#ifndef FI_APPLY_U
+#define FI_APPLY_U 2
+#endif
+constexpr int kApplyU = FI_APPLY_U;  // chunks per thread whose loads go out together
 __global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict__ descs,
                                                      const DevCrop *__restrict__ crops,
                                                      const ScResult *__restrict__ results) {
@@ -1765,37 +1793,48 @@ __global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict
     for (int64_t o = tid; o < min<int64_t>(head, total); o += 256) A.dst[o] = *src_of(o);
     for (int64_t o = tail0 + tid; o < total; o += 256) A.dst[o] = *src_of(o);
   }
-  for (int64_t k = (int64_t)blockIdx.x * 256 + tid; k < nchunk; k += (int64_t)gridDim.x * 256) {
-    const int64_t o = head + 16 * k;
-    int y, x;
-    rowcol(o, &y, &x);
-    uint4 out;
-    if (x + 16 <= rowb) {
-      const uint8_t *s = src0 + (int64_t)y * A.src_stride + x;
-      const uint32_t *sa = reinterpret_cast<const uint32_t *>((uintptr_t)s & ~(uintptr_t)3);
-      const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
-      const uint32_t w0 = sa[0], w1 = sa[1], w2 = sa[2], w3 = sa[3], w4 = sh ? sa[4] : 0u;
-      out.x = ap_align(w1, w0, sh);
-      out.y = ap_align(w2, w1, sh);
-      out.z = ap_align(w3, w2, sh);
-      out.w = ap_align(w4, w3, sh);
-    } else {
-      uint8_t b[16];
-      int yy = y, xx = x;
+  const int64_t cs = (int64_t)gridDim.x * 256;
+  for (int64_t k0 = (int64_t)blockIdx.x * 256 + tid; k0 < nchunk; k0 += kApplyU * cs) {
+    uint4 out[kApplyU];
 #pragma unroll
-      for (int j = 0; j < 16; j++) {  // straddles a row end
-        b[j] = src0[(int64_t)yy * A.src_stride + xx];
-        if (++xx == rowb) {
-          xx = 0;
-          yy++;
+    for (int u = 0; u < kApplyU; u++) {
+      const int64_t k = k0 + u * cs;
+      if (k >= nchunk) break;
+      const int64_t o = head + 16 * k;
+      int y, x;
+      rowcol(o, &y, &x);
+      if (x + 16 <= rowb) {
+        const uint8_t *s = src0 + (int64_t)y * A.src_stride + x;
+        const uint32_t *sa = reinterpret_cast<const uint32_t *>((uintptr_t)s & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
+        const uint32_t w0 = sa[0], w1 = sa[1], w2 = sa[2], w3 = sa[3], w4 = sh ? sa[4] : 0u;
+        out[u].x = ap_align(w1, w0, sh);
+        out[u].y = ap_align(w2, w1, sh);
+        out[u].z = ap_align(w3, w2, sh);
+        out[u].w = ap_align(w4, w3, sh);
+      } else {
+        uint8_t b[16];
+        int yy = y, xx = x;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {  // straddles a row end
+          b[j] = src0[(int64_t)yy * A.src_stride + xx];
+          if (++xx == rowb) {
+            xx = 0;
+            yy++;
+          }
         }
+        out[u].x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+        out[u].y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+        out[u].z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
+        out[u].w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
       }
-      out.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
-      out.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
-      out.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
-      out.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
     }
-    *reinterpret_cast<uint4 *>(A.dst + o) = out;
+#pragma unroll
+    for (int u = 0; u < kApplyU; u++) {
+      const int64_t k = k0 + u * cs;
+      if (k >= nchunk) break;
+      *reinterpret_cast<uint4 *>(A.dst + head + 16 * k) = out[u];
+    }
   }
 }
 
