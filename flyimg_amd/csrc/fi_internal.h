@@ -186,7 +186,7 @@ constexpr int kSgSlots = 3;
 constexpr int kSgDigits = 5;
 constexpr int kSgPlanes = 7;
 constexpr int kSgMax = 2;          // groups per image (accumulators in registers)
-constexpr int kSgMaxKs = 3;        // 64-px k-steps per window row
+constexpr int kSgMaxKs = 2;        // 64-px k-steps per window row
 constexpr int kSgMaxCrops = kSgMax * 16 * kSgSlots;
 constexpr int kScore3Lds = 160 * 1024 - 4608;  // dynamic LDS cap (k_sc_score3 has 4384 B of static LDS)
 __host__ __device__ inline int sg_pitch(int aw) { return (aw + 7) & ~7; }

@@ -1434,6 +1434,10 @@ __global__ __launch_bounds__(kScoreThreads) void k_sc_score2(const ScDesc *__res
 constexpr int kS3Threads = 1024;
 constexpr int kS3Waves = kS3Threads / 64;
 constexpr int kS3Pre = 8;  // plane items per thread with their map loads in flight together
+#ifndef FI_S3_ABL
+#define FI_S3_ABL 0
+#endif
+constexpr int kS3Abl = FI_S3_ABL;  // profiling ablations (wrong scores): 1 no MFMA pass, 2 no plane build, 4 no finalize
 
 __global__ __launch_bounds__(kS3Threads) void k_sc_score3(const ScDesc *__restrict__ descs,
                                                           const DevCrop *__restrict__ crops,
@@ -1470,7 +1474,7 @@ __global__ __launch_bounds__(kS3Threads) void k_sc_score3(const ScDesc *__restri
     const int nq = (W + 3) >> 2, nit = H * nq;
     uint32_t se_s = 0, te_s = 0, e_s = 0, s_s = 0, t_s = 0;
 #pragma unroll 1
-    for (int base = 0; base < nit; base += kS3Pre * kS3Threads) {
+    for (int base = 0; base < ((kS3Abl & 2) ? 0 : nit); base += kS3Pre * kS3Threads) {
       uint32_t mm[kS3Pre][4];
 #pragma unroll
       for (int j = 0; j < kS3Pre; j++) {
@@ -1527,80 +1531,98 @@ __global__ __launch_bounds__(kS3Threads) void k_sc_score3(const ScDesc *__restri
       T[2] = (double)S5[4] / 65025.0 + tb * ((double)S5[2] / 255.0);
     }
   }
-  // ---- 2. MFMA pass: per group, rows wave, wave + 16, ... ----
-  i32x4 acc[kSgMax][kSgPlanes];
+  // ---- 2. MFMA pass: the waves split between the groups in proportion to
+  // their rows (one group's accumulators per wave); a wave takes rows
+  // r, r + nw, ... of its group, each row's B fragments (L2) loaded three of
+  // its rows ahead ----
+  int gw = 0, w0 = 0, nw = kS3Waves;
+  if (ng == 2) {
+    const int r0 = G[0].nrows, r1 = G[1].nrows;
+    const int n0 = min(kS3Waves - 1, max(1, (kS3Waves * r0 + (r0 + r1) / 2) / (r0 + r1)));
+    if (wave >= n0) {
+      gw = 1;
+      w0 = n0;
+      nw = kS3Waves - n0;
+    } else {
+      nw = n0;
+    }
+  }
+  i32x4 acc[kSgPlanes];
 #pragma unroll
-  for (int g = 0; g < kSgMax; g++)
+  for (int p = 0; p < kSgPlanes; p++) acc[p] = i32x4{0, 0, 0, 0};
+  if (!(kS3Abl & 1)) {
+    const ScGroup *Gg = G + gw;
+    const int nrows = __builtin_amdgcn_readfirstlane(Gg->nrows);
+    const int ks = __builtin_amdgcn_readfirstlane(Gg->ks);
+    const int ybase = __builtin_amdgcn_readfirstlane(Gg->ybase);
+    const int nB = kSgDigits * __builtin_amdgcn_readfirstlane(Gg->nslot);
+    const bool bl = (lane & 15) < nB;
+    const i32x4 *bf = reinterpret_cast<const i32x4 *>(ai + Gg->bfrag);
+    const int aoff = Gg->x0[lane & 15] + 16 * (lane >> 4);
+    auto loadb = [&](int r, i32x4 (&b)[kSgMaxKs]) {
 #pragma unroll
-    for (int p = 0; p < kSgPlanes; p++) acc[g][p] = i32x4{0, 0, 0, 0};
+      for (int t = 0; t < kSgMaxKs; t++)
+        b[t] = (r < nrows && t < ks && bl) ? bf[((int64_t)r * ks + t) * 64 + lane] : i32x4{0, 0, 0, 0};
+    };
+    auto row = [&](int r, const i32x4 (&b)[kSgMaxKs]) {
+      const uint8_t *rowp = lds3 + (ybase + r) * pitch + aoff;
 #pragma unroll
-  for (int g = 0; g < kSgMax; g++) {
-    if (g < ng) {
-      const int nrows = __builtin_amdgcn_readfirstlane(G[g].nrows);
-      const int ks = __builtin_amdgcn_readfirstlane(G[g].ks);
-      const int ybase = __builtin_amdgcn_readfirstlane(G[g].ybase);
-      const int nB = kSgDigits * __builtin_amdgcn_readfirstlane(G[g].nslot);
-      const int xl = G[g].x0[lane & 15];
-      const bool bl = (lane & 15) < nB;
-      const i32x4 *bf = reinterpret_cast<const i32x4 *>(ai + G[g].bfrag);
-      const int aoff = xl + 16 * (lane >> 4);
-      auto loadb = [&](int r, i32x4 *b) {
+      for (int t = 0; t < kSgMaxKs; t++) {
+        if (t < ks) {
 #pragma unroll
-        for (int t = 0; t < kSgMaxKs; t++)
-          b[t] = (r < nrows && t < ks && bl) ? bf[((int64_t)r * ks + t) * 64 + lane] : i32x4{0, 0, 0, 0};
-      };
-      i32x4 b[kSgMaxKs], bn[kSgMaxKs];
-      loadb(wave, b);
-      for (int r = wave; r < nrows; r += kS3Waves) {
-        loadb(r + kS3Waves, bn);  // the next row's fragments in flight
-        const uint8_t *rowp = lds3 + (ybase + r) * pitch + aoff;
-#pragma unroll
-        for (int t = 0; t < kSgMaxKs; t++) {
-          if (t < ks) {
-#pragma unroll
-            for (int p = 0; p < kSgPlanes; p++) {
-              const uint8_t *a = rowp + p * psz + 64 * t;
-              const i32x2 lo = *(l_ci32x2 *)(const __attribute__((address_space(3))) uint8_t *)a;
-              const i32x2 hi = *(l_ci32x2 *)(const __attribute__((address_space(3))) uint8_t *)(a + 8);
-              acc[g][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(i32x4{lo.x, lo.y, hi.x, hi.y}, b[t], acc[g][p], 0,
-                                                                0, 0);
-            }
+          for (int p = 0; p < kSgPlanes; p++) {
+            const uint8_t *a = rowp + p * psz + 64 * t;
+            const i32x2 lo = *(l_ci32x2 *)(const __attribute__((address_space(3))) uint8_t *)a;
+            const i32x2 hi = *(l_ci32x2 *)(const __attribute__((address_space(3))) uint8_t *)(a + 8);
+            acc[p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(i32x4{lo.x, lo.y, hi.x, hi.y}, b[t], acc[p], 0, 0, 0);
           }
         }
-#pragma unroll
-        for (int t = 0; t < kSgMaxKs; t++) b[t] = bn[t];
       }
+    };
+    const int rs = wave - w0;
+    i32x4 b0[kSgMaxKs], b1[kSgMaxKs], b2[kSgMaxKs];
+    loadb(rs, b0);
+    loadb(rs + nw, b1);
+    loadb(rs + 2 * nw, b2);
+#pragma unroll 1
+    for (int r = rs; r < nrows; r += 3 * nw) {
+      row(r, b0);
+      loadb(r + 3 * nw, b0);
+      if (r + nw < nrows) row(r + nw, b1);
+      loadb(r + 4 * nw, b1);
+      if (r + 2 * nw < nrows) row(r + 2 * nw, b2);
+      loadb(r + 5 * nw, b2);
     }
   }
   // ---- 3. cross-wave sums (the planes are dead), then per crop ----
   __syncthreads();
   int32_t *red = reinterpret_cast<int32_t *>(lds3);  // [g][plane][16 x origins][16 (digit, slot)]
   auto red_at = [&](int g, int p, int i) { return ((g * kSgPlanes + p) * 16 + 4 * (lane >> 4) + i) * 16 + (lane & 15); };
-  if (wave == 0) {
+  // the first wave of each group stores, the others add
+  if (wave == w0) {
 #pragma unroll
-    for (int g = 0; g < kSgMax; g++)
-      if (g < ng)
+    for (int p = 0; p < kSgPlanes; p++)
 #pragma unroll
-        for (int p = 0; p < kSgPlanes; p++)
-#pragma unroll
-          for (int i = 0; i < 4; i++) red[red_at(g, p, i)] = acc[g][p][i];
+      for (int i = 0; i < 4; i++) red[red_at(gw, p, i)] = acc[p][i];
   }
   __syncthreads();
-  if (wave != 0) {
+  if (wave != w0) {
 #pragma unroll
-    for (int g = 0; g < kSgMax; g++)
-      if (g < ng)
+    for (int p = 0; p < kSgPlanes; p++)
 #pragma unroll
-        for (int p = 0; p < kSgPlanes; p++)
-#pragma unroll
-          for (int i = 0; i < 4; i++) atomicAdd(&red[red_at(g, p, i)], acc[g][p][i]);
+      for (int i = 0; i < 4; i++) atomicAdd(&red[red_at(gw, p, i)], acc[p][i]);
   }
   __syncthreads();
   const double u = 1.1102230246251565e-16;  // 2^-53
   auto gam = [&](double n) { return n * u / (1.0 - n * u); };
   const double aoi = fabs(oi);
   const double wd = P.detail_weight, ws = P.skin_weight, wt = P.saturation_weight;
-  for (int c = tid; c < ncrops; c += kS3Threads) {
+  if (kS3Abl & 4)
+    for (int c = tid; c < ncrops; c += kS3Threads) {
+      s_tot[c] = c;  // one candidate, no re-score
+      s_bnd[c] = 0;
+    }
+  for (int c = tid; c < ((kS3Abl & 4) ? 0 : ncrops); c += kS3Threads) {
     const DevCrop cr = crops[D.crop0 + c];
     const ScGroup &Gr = G[cr.sg];
     double V[kSgPlanes], A[kSgPlanes];
