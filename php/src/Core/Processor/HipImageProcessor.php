@@ -111,6 +111,9 @@ class HipImageProcessor extends ImageProcessor
 
     public function processNewImage(OutputImage $outputImage): OutputImage
     {
+        // a mark left by an earlier request for this path (its handler threw
+        // or skipped the smart crop) must not skip this request's smart crop
+        unset(self::$fusedCropped[$outputImage->getOutputImagePath()]);
         $this->sourceImageInfo = $outputImage->getInputImage()->sourceImageInfo();
         $this->options = $outputImage->getInputImage()->optionsBag();
         $path = $this->sourceImageInfo->path();
