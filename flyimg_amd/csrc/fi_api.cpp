@@ -1556,8 +1556,25 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     q16 = q16 || d.gray || d.rot != 0;
     nst += w.nstrips;
   }
-  const VrLayout L = vr_lds_layout(vpitch, q16);
+  VrLayout L = vr_lds_layout(vpitch, q16);
   if (L.R <= 0) return false;
+  // loader waves: 4 when every strip has one 16-px output block (3 items: one
+  // per H wave) and every touched-row list is evenly spaced (the pair-class copy
+  // of an uneven list is laid out for 2 loaders).  Measured (round 5): cfg5
+  // resize 8.45 -> 7.83 ms; cfg2 (two blocks a strip, two items per H wave)
+  // neutral, cfg3 1 % slower, so they keep 2.  FI_VR_NL=2 / 4 forces (4 only
+  // where it is valid: <= 2 blocks a strip)
+  {
+    int max_nocb = 0;
+    bool even = true;
+    for (const VrWork &w : work) {
+      for (int st = 0; st < w.nstrips; st++) max_nocb = std::max(max_nocb, Bp.vstrips[w.first_strip + st].nocb);
+      even = even && (w.V->rstep != 0 || w.V->rows.size() <= 1);
+    }
+    static const char *nl_env = getenv("FI_VR_NL");
+    const int want = nl_env ? atoi(nl_env) : (max_nocb <= 1 ? 4 : 2);
+    L.nl = (want == 4 && even && max_nocb <= 2) ? 4 : 2;
+  }
   // per image: a VDesc with the block-major tables
   std::vector<int32_t> desc_of(work.size());
   for (size_t k = 0; k < work.size(); k++) {

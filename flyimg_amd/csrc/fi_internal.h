@@ -282,6 +282,7 @@ struct VrLayout {
   int32_t otile_off;    // output tiles [2][otile_bytes]
   int32_t otile_bytes;
   int32_t total;        // dynamic LDS of the launch
+  int32_t nl;           // loader waves (2 or 4; the H waves are the other 7 - nl of waves 8-14)
 };
 
 // k_rs_hv (fi_hv.hip): streaming exact-integer MFMA resample, horizontal first

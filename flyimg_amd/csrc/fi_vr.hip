@@ -58,10 +58,11 @@ typedef __attribute__((address_space(3))) i32x2 l_i32x2;
 typedef __attribute__((address_space(3))) uint8_t l_u8;
 
 constexpr int kVW = 8;                   // V waves: 64 source bytes (4 column tiles) each
-constexpr int kHW = 5;                   // H waves 8-12: horizontal items hw, hw + 5 (3 nocb <= 10)
-constexpr int kSW = 1;                   // S wave 13: the stores of the output tile of phase p - 2
-constexpr int kLW = 2;                   // L waves 14-15
-static_assert(kVW + kHW + kSW + kLW == 16, "16 waves");
+constexpr int kSW = 1;                   // S wave: the stores of the output tile of phase p - 2
+// the other 7 waves: NL loader waves (the last ones) and 7 - NL H waves, whose
+// items are hw and hw + (7 - NL); the host picks NL per launch (VrLayout::nl):
+// 4 when every strip has <= 2 16-px output blocks (<= 6 items) and every
+// image's touched rows are evenly spaced, else 2
 constexpr int kABytes = 4096;            // [t][limb][64 lanes][16 B]: two limbs, <= 2 k-steps
 constexpr int kRecBytes = 32;
 constexpr int kLutSlots = 4;
@@ -238,12 +239,15 @@ __device__ uint64_t g_vr_stamps[kVrStampSlots * kVrStampN];
 // DMAs after the first two blocks, 5 / 6 loader
 // priority 1 / 0 (production pixels), 9 production + per-phase s_memtime sums;
 // 10 + k: ablation k with the stamps.
-template <int MODE>
+template <int MODE, int NL>
 __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ descs, const MStrip *__restrict__ strips,
                                                    const VrTile *__restrict__ tiles, int ntiles,
                                                    const int32_t *__restrict__ wginfo, const int32_t *__restrict__ ai,
                                                    VrLayout Lo) {
   constexpr int M = MODE >= 10 ? MODE - 10 : MODE;
+  constexpr int kLW = NL, kHW = 16 - kVW - kSW - NL;
+  static_assert(NL == 2 || NL == 4, "loader waves");
+  constexpr int kPS = 2 * NL;  // stream rows between a loader wave's own pairs
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = ufl(tid >> 6);
@@ -339,7 +343,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       for (int i = li; i < nf; i += kLW)
         dma16(m0 + 1024 * i, reinterpret_cast<const uint8_t *>(ai + r.frag) + 1024 * i, 16u * lane);
     };
-    // ---- row cursor: this wave's row pairs G = 4 m + 2 li of the stream ----
+    // ---- row cursor: this wave's row pairs G = kPS m + 2 li of the stream ----
     int rt = t0, rG = 2 * li, rslot = 2 * li, n_issued = 0;
     VrTile RT{};
     const uint8_t *r_src = nullptr;
@@ -379,7 +383,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         }
         const int seg = min(limit, RT.g0 + RT.glen);
         int k0 = RT.kbase + (rG - RT.g0);
-        if (r_rstep == 0 && k0 + 1 < r_nrows) {
+        if (NL == 2 && r_rstep == 0 && k0 + 1 < r_nrows) {
           const int cnt = min((seg - rG + 3) >> 2, (r_nrows - 1 - k0 + 3) >> 2);
           // the host's pair list (after the row list and its 32-entry pad):
           // class k0 & 3, own pair m at entry (k0 >> 2) + m, PL pairs per wait
@@ -407,82 +411,112 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         }
         if (k0 + 1 < r_nrows) {
           // pairs with k0 + 1 < nrows and rG < seg
-          const int cnt = min((seg - rG + 3) >> 2, (r_nrows - 1 - k0 + 3) >> 2);
+          const int cnt = min((seg - rG + kPS - 1) / kPS, (r_nrows - 1 - k0 + kPS - 1) / kPS);
           const int64_t rs = (int64_t)r_rstep * r_stride;
           const uint8_t *base = r_src + (int64_t)(r_row0 + r_rstep * k0) * r_stride + r_b0;
           if (pat_tile != rt) {
-            // this wave's own pair starts 2 li + 4 m have the chunk swizzle
-            // f = 2 li + 4 (m & 1) + 8 ((m >> 2) & 1): four lane patterns per tile
+            // this wave's own pair starts 2 li + kPS m have the chunk swizzle
+            // f = (s & 7) | 8 ((s >> 4) & 1) of slot s = 2 li + kPS m (R is a
+            // multiple of 32): NL 2: 2 li + 4 (m & 1) + 8 ((m >> 2) & 1), four
+            // lane patterns; NL 4: 2 li + 8 ((m >> 1) & 1), two
             pat_tile = rt;
             const uint32_t hoff = h ? (uint32_t)rs : 0u;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-              uint32_t lc = lane_c ^ (uint32_t)(2 * li + 4 * (q & 1) + 8 * (q >> 1));
+              uint32_t lc = lane_c ^ (uint32_t)(NL == 2 ? 2 * li + 4 * (q & 1) + 8 * (q >> 1) : 2 * li + 8 * (q & 1));
               if (16 * (int)lc >= r_nbytes) lc = 0;
               pat[q] = hoff + 16u * lc;
             }
           }
-          // straight-line DMAs: own pair m of the 8-pair cycle (m & 7) has lane
-          // pattern (m & 1) | ((m >> 2) & 1) << 1, and a cycle never crosses the
-          // ring end (R is a multiple of 32 rows), so the wrap is checked per cycle
+          // straight-line DMAs over the 32-row cycle of own pairs (32 / kPS of
+          // them: NL 2 pattern (m & 1) | ((m >> 2) & 1) << 1, NL 4 (m >> 1) & 1);
+          // a cycle never crosses the ring end (R is a multiple of 32 rows), so
+          // the wrap is checked per cycle
           {
             const int rslot0 = rslot;
             uint32_t m0 = lds_addr(lds) + (uint32_t)(O.ring + rslot * 512);
-            int left = cnt, ph = (rslot >> 2) & 7;
+            int left = cnt, ph = (rslot / kPS) & (32 / kPS - 1);
+            constexpr uint32_t kStep = 512u * kPS;
+            const int64_t bs = (int64_t)kPS * rs;
             for (;;) {
-              switch (ph) {
-              case 0:
-                dma16_p0(m0, base, pat[0]);
-                base += 4 * rs;
-                m0 += 2048;
-                if (--left == 0) goto stream_done;
-              case 1:
-                dma16_p1(m0, base, pat[1]);
-                base += 4 * rs;
-                m0 += 2048;
-                if (--left == 0) goto stream_done;
-              case 2:
-                dma16_p2(m0, base, pat[0]);
-                base += 4 * rs;
-                m0 += 2048;
-                if (--left == 0) goto stream_done;
-              case 3:
-                dma16_p3(m0, base, pat[1]);
-                base += 4 * rs;
-                m0 += 2048;
-                if (--left == 0) goto stream_done;
-              case 4:
-                dma16_p4(m0, base, pat[2]);
-                base += 4 * rs;
-                m0 += 2048;
-                if (--left == 0) goto stream_done;
-              case 5:
-                dma16_p5(m0, base, pat[3]);
-                base += 4 * rs;
-                m0 += 2048;
-                if (--left == 0) goto stream_done;
-              case 6:
-                dma16_p6(m0, base, pat[2]);
-                base += 4 * rs;
-                m0 += 2048;
-                if (--left == 0) goto stream_done;
-              case 7:
-                dma16_p7(m0, base, pat[3]);
-                base += 4 * rs;
-                m0 += 2048;
-                if (--left == 0) goto stream_done;
+              if constexpr (NL == 2) {
+                switch (ph) {
+                case 0:
+                  dma16_p0(m0, base, pat[0]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 1:
+                  dma16_p1(m0, base, pat[1]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 2:
+                  dma16_p2(m0, base, pat[0]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 3:
+                  dma16_p3(m0, base, pat[1]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 4:
+                  dma16_p4(m0, base, pat[2]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 5:
+                  dma16_p5(m0, base, pat[3]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 6:
+                  dma16_p6(m0, base, pat[2]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 7:
+                  dma16_p7(m0, base, pat[3]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                }
+              } else {
+                switch (ph) {
+                case 0:
+                  dma16_p0(m0, base, pat[0]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 1:
+                  dma16_p1(m0, base, pat[0]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 2:
+                  dma16_p2(m0, base, pat[1]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                case 3:
+                  dma16_p3(m0, base, pat[1]);
+                  base += bs;
+                  m0 += kStep;
+                  if (--left == 0) goto stream_done;
+                }
               }
               ph = 0;
-              int r2 = rslot0 + 4 * (cnt - left);  // the next cycle's first pair
+              int r2 = rslot0 + kPS * (cnt - left);  // the next cycle's first pair
               while (r2 >= R) r2 -= R;
               m0 = lds_addr(lds) + (uint32_t)(O.ring + r2 * 512);
             }
           stream_done:
-            rslot = rslot0 + 4 * cnt;
+            rslot = rslot0 + kPS * cnt;
             while (rslot >= R) rslot -= R;
           }
           n += cnt;
-          rG += 4 * cnt;
+          rG += kPS * cnt;
           continue;
         }
         // one pair clamped at the list end
@@ -497,14 +531,14 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         const uint32_t voff = (h ? (uint32_t)((int64_t)(r1 - r0) * r_stride) : 0u) + 16u * lc;
         dma16(lds_addr(lds) + (uint32_t)(O.ring + rslot * 512), base, voff);
         n++;
-        rG += 4;
-        rslot += 4;
+        rG += kPS;
+        rslot += kPS;
         if (rslot >= R) rslot -= R;
       }
       return n;
     };
-    // own pairs (starts 4 m + 2 li) below stream row x
-    auto own_below = [&](int x) -> int { return x > 2 * li ? (x - 2 * li + 3) >> 2 : 0; };
+    // own pairs (starts kPS m + 2 li) below stream row x
+    auto own_below = [&](int x) -> int { return x > 2 * li ? (x - 2 * li + kPS - 1) / kPS : 0; };
 
     // the loader's few instructions go first on its SIMD (MODE 5 / 6: priority 1 / 0)
     if (M == 5)
@@ -955,14 +989,21 @@ VrLayout vr_lds_layout(int vpitch, bool q16) {
 int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrTile *tiles, int ntiles,
               const int32_t *wginfo, int G, const int32_t *ai, VrLayout L) {
   if (ntiles <= 0 || G <= 0) return 0;
-  if (L.R <= 0 || L.total > kVrMaxLds) return -1;
+  if (L.R <= 0 || L.total > kVrMaxLds || (L.nl != 2 && L.nl != 4)) return -1;
   // FI_VR_VARIANT: profiling ablations (1-3, 11-13: wrong pixels, reported by
   // the return value 1, which the caller counts as stat "vr_ablation") and the
   // per-phase stamps (9: production pixels)
   static const char *variant = getenv("FI_VR_VARIANT");
   const int v = variant ? atoi(variant) : 0;
-#define FI_VR_LAUNCH(m) \
-  hipLaunchKernelGGL((k_rs_vr<m>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, wginfo, ai, L)
+#define FI_VR_LAUNCH(m)                                                                                    \
+  do {                                                                                                     \
+    if (L.nl == 4)                                                                                         \
+      hipLaunchKernelGGL((k_rs_vr<m, 4>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, wginfo, \
+                         ai, L);                                                                           \
+    else                                                                                                   \
+      hipLaunchKernelGGL((k_rs_vr<m, 2>), dim3(G), dim3(1024), L.total, s, descs, strips, tiles, ntiles, wginfo, \
+                         ai, L);                                                                           \
+  } while (0)
   switch (v) {
     case 1: FI_VR_LAUNCH(1); break;
     case 2: FI_VR_LAUNCH(2); break;

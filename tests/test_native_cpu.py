@@ -54,7 +54,7 @@ def test_vr_two_limb_quantisation_bound():
 
 
 @pytest.mark.parametrize("src,kernels", [
-    ("fi_vr.hip", ["_ZN2fi7k_rs_vrILi0EE"]),
+    ("fi_vr.hip", ["_ZN2fi7k_rs_vrILi0ELi2EE", "_ZN2fi7k_rs_vrILi0ELi4EE"]),
     ("fi_smartcrop.hip", ["_ZN2fi11k_sc_score2ILi1EE", "_ZN2fi11k_sc_score3E"]),
 ])
 def test_hot_kernels_do_not_spill(src, kernels):
