@@ -82,7 +82,7 @@ int vm_read_stamps(uint64_t *out, int slots);
 int launch_vm(hipStream_t s, const VDesc *descs, const MStrip *strips, const VTile *tiles, int ntiles,
               const int32_t *ai, size_t lds);
 // its persistent block-major form (fi_vr.hip)
-VrLayout vr_lds_layout(int vpitch, bool q16);
+VrLayout vr_lds_layout(int vpitch, bool q16, int pbuf);
 int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrTile *tiles, int ntiles,
               const int32_t *wginfo, int G, const int32_t *ai, VrLayout L);
 int vr_read_stamps(uint64_t *out, int slots);
@@ -515,6 +515,9 @@ static bool heap_fits(const fi_ctx *c, const Exec &E) {
 // at ab + *_off) behind the heaps' used marks; advance the marks (16-element
 // aligned, so 16-byte aligned fragment tables stay aligned).
 static int heap_commit(fi_ctx *c, Exec &E, const uint8_t *ab, size_t ai_off, size_t af_off, size_t ad_off) {
+  static const bool heap_debug = getenv("FI_HEAP_DEBUG") != nullptr;
+  if (heap_debug)
+    fprintf(stderr, "heap: ai %zu af %zu ad %zu\n", E.ai.size(), E.af.size(), E.ad.size());
   if (!E.ai.empty())
     HIP_TRY(hipMemcpyAsync((int32_t *)c->heap_i.p + E.bi, ab + ai_off, E.ai.size() * 4, hipMemcpyDeviceToDevice,
                            c->stream));
@@ -1556,7 +1559,7 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     q16 = q16 || d.gray || d.rot != 0;
     nst += w.nstrips;
   }
-  VrLayout L = vr_lds_layout(vpitch, q16);
+  VrLayout L = vr_lds_layout(vpitch, q16, 1);
   if (L.R <= 0) return false;
   // loader waves: 4 when every strip has one 16-px output block (3 items: one
   // per H wave) and every touched-row list is evenly spaced (the pair-class copy
@@ -1672,6 +1675,28 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   }
   const int ntiles = (int)all.size();
   if (ntiles == 0) return false;
+  VrLayout L1{};
+  {
+    // two Q16 plane buffers (by block parity: the V waves never wait for the H
+    // waves' reads) cost the ring 32 rows; taken when the smaller ring still
+    // holds every block's and its successor's rows with max(32, half a block
+    // step) to spare.  Measured (round 5): cfg2 (33 spare) 1.99 -> 1.93 ms;
+    // cfg3 (19) and cfg5 (3) slower.  FI_VR_PBUF=1 / 2 forces (2 where it fits)
+    int inner = 0, step = 0;
+    for (const auto &kv : spans) inner = std::max(inner, kv.second.inner);
+    for (const VrWork &w : work) {
+      const int32_t *bm = w.V->bmeta.data();
+      for (int b = 0; b + 1 < w.V->nblk; b++) step = std::max(step, bm[4 * (b + 1)] - bm[4 * b]);
+    }
+    const VrLayout L2 = vr_lds_layout(vpitch, q16, 2);
+    static const char *pb_env = getenv("FI_VR_PBUF");
+    const int want = pb_env ? atoi(pb_env) : (L2.R - inner >= std::max(32, step / 2) ? 2 : 1);
+    L1 = L;
+    if (want == 2 && L2.R >= inner) {
+      L = L2;
+      L.nl = L1.nl;
+    }
+  }
   int G = std::min(ntiles, c->n_cu);
   if (G > 8) G -= G % 8;
   // workgroup g runs on XCD g % 8; with fewer than 4 images per XCD (small
@@ -1722,30 +1747,52 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   // the streams: workgroup g walks tiles [t0(g), t1(g)); every phase's rows
   // [K0, Rend) and the next phase's must be resident together
   std::vector<VrTile> tiles;
-  tiles.reserve(ntiles);
-  std::vector<int32_t> info(4 * (size_t)G, 0);
-  for (int g = 0; g < G; g++) {
-    int64_t gpos = 0, prev_tail = -1;
-    info[4 * g + 2] = (int32_t)tiles.size();
-    for (const TC *tc : per[g]) {
-      VrTile T = tc->t;
-      const VrV &V = *work[T.pad].V;
-      const Span &sp = *tc->sp;
-      T.kbase = V.bmeta[4 * T.b0];
-      T.glen = sp.glen;
-      T.g0 = (int32_t)gpos;
-      // the seam: this tile's first block's rows and the previous tile's last
-      // block's window resident together
-      if (prev_tail >= 0 && T.g0 + sp.head - prev_tail > L.R) return false;
-      prev_tail = T.g0 + sp.tail;
-      info[4 * g] += T.b1 - T.b0;
-      gpos += T.glen;
-      if (gpos >= ((int64_t)1 << 30)) return false;
-      T.pad = 0;
-      tiles.push_back(T);
+  std::vector<int32_t> info;
+  auto streams = [&](int R) -> bool {
+    tiles.clear();
+    tiles.reserve(ntiles);
+    info.assign(4 * (size_t)G, 0);
+    for (int g = 0; g < G; g++) {
+      int64_t gpos = 0, prev_tail = -1;
+      info[4 * g + 2] = (int32_t)tiles.size();
+      for (const TC *tc : per[g]) {
+        VrTile T = tc->t;
+        const VrV &V = *work[T.pad].V;
+        const Span &sp = *tc->sp;
+        T.kbase = V.bmeta[4 * T.b0];
+        T.glen = sp.glen;
+        T.g0 = (int32_t)gpos;
+        // the seam: this tile's first block's rows and the previous tile's last
+        // block's window resident together
+        if (prev_tail >= 0 && T.g0 + sp.head - prev_tail > R) return false;
+        prev_tail = T.g0 + sp.tail;
+        info[4 * g] += T.b1 - T.b0;
+        gpos += T.glen;
+        if (gpos >= ((int64_t)1 << 30)) return false;
+        T.pad = 0;
+        tiles.push_back(T);
+      }
+      info[4 * g + 1] = (int32_t)gpos;
+      info[4 * g + 3] = (int32_t)tiles.size();
     }
-    info[4 * g + 1] = (int32_t)gpos;
-    info[4 * g + 3] = (int32_t)tiles.size();
+    return true;
+  };
+  if (!streams(L.R)) {
+    if (L.pbuf != 2) return false;
+    L = L1;  // a seam needs the bigger ring
+    if (!streams(L.R)) return false;
+  }
+  static const bool vr_debug = getenv("FI_VR_DEBUG") != nullptr;
+  if (vr_debug) {
+    int inner = 0, rpb = 0, nocb = 0;
+    for (const auto &kv : spans) inner = std::max(inner, kv.second.inner);
+    for (const VrWork &w : work) {
+      const int32_t *bm = w.V->bmeta.data();
+      for (int b = 0; b + 1 < w.V->nblk; b++) rpb = std::max(rpb, bm[4 * (b + 1)] - bm[4 * b]);
+      for (int st = 0; st < w.nstrips; st++) nocb = std::max(nocb, Bp.vstrips[w.first_strip + st].nocb);
+    }
+    fprintf(stderr, "vr: R %d pbuf %d nl %d vpitch %d inner %d K0 step max %d nocb %d tiles %d G %d\n", L.R, L.pbuf,
+            L.nl, vpitch, inner, rpb, nocb, ntiles, G);
   }
   Bp.vrtiles = std::move(tiles);
   Bp.vr_info = std::move(info);

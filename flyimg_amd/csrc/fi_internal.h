@@ -283,6 +283,7 @@ struct VrLayout {
   int32_t otile_bytes;
   int32_t total;        // dynamic LDS of the launch
   int32_t nl;           // loader waves (2 or 4; the H waves are the other 7 - nl of waves 8-14)
+  int32_t pbuf;         // Q16 plane buffers (1: the V waves wait for the H waves' reads; 2: by block parity)
 };
 
 // k_rs_hv (fi_hv.hip): streaming exact-integer MFMA resample, horizontal first

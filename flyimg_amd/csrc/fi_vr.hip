@@ -23,16 +23,19 @@
 //    column tile (folded once per block, the MFMA bias the constant
 //    128 * 2^s), then the Q16 planes.
 //
-//  Roles per phase (one workgroup barrier per phase):
+//  Roles per phase (one workgroup barrier per phase; NL = 2 or 4 loader waves,
+//  7 - NL H waves, chosen per launch by the host, VrLayout::nl):
 //    V waves 0-7   block p: vertical MFMAs from the ring (both k-steps' reads
-//                  issued first), fold, Q16 planes (single plane buffer: a wave
-//                  writes it only after the five H waves have counted their
-//                  reads of block p - 1 off an LDS counter);
-//    H waves 8-12  block p - 1: both items' plane reads, the counter, then the
+//                  issued first), fold, Q16 planes: into plane buffer p & 1
+//                  when there are two (VrLayout::pbuf, the host's choice when
+//                  the ring keeps enough rows), else into the single buffer
+//                  once the H waves have counted their reads of block p - 1 off
+//                  an LDS counter;
+//    H waves 8-    block p - 1: both items' plane reads (the counter), then the
 //                  horizontal MFMAs -> output tile slot (p - 1) & 1;
-//    S wave 13     the stores of block p - 2;
-//    L waves 14-15 the stream cursor: source row pairs by LDS-DMA (ring slot
-//                  G mod R, G < K0(p) + R), A fragments of block p + 1, the
+//    S wave        the stores of block p - 2;
+//    L waves (last NL) the stream cursor: source row pairs by LDS-DMA (ring
+//                  slot G mod R, G < K0(p) + R), A fragments of block p + 1, the
 //                  record of phase p + 2 (+ the strip's LUT); the end-of-phase
 //                  vmcnt waits exactly for the rows of block p + 1.
 //  Each workgroup walks its own tile range [t0, t1) (host: LPT over the
@@ -667,8 +670,9 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           for (int j = 0; j < kT; j++) acc[1][j] = mfma(At[1][1], Bt[1][j], acc[1][j]);
         }
         stamp(1);
-        // the H waves' reads of block p - 1's planes are done (single plane buffer)
-        if (M != 2) {
+        // the H waves' reads of block p - 1's planes are done (single plane
+        // buffer; with two, block p's buffer was read in phase p - 1)
+        if (M != 2 && Lo.pbuf == 1) {
           const uint32_t want = (uint32_t)kHW * (uint32_t)(p + 1);
           while (hcnt[0] < want) __builtin_amdgcn_s_sleep(1);
         }
@@ -689,8 +693,9 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           const uint32_t x01 = __builtin_bit_cast(uint32_t, p01) ^ 0x80808080u;
           const uint32_t x23 = __builtin_bit_cast(uint32_t, p23) ^ 0x80808080u;
           if (o != 0xFFFFu) {
-            *reinterpret_cast<uint32_t *>(planes + o) = __builtin_amdgcn_perm(x23, x01, 0x07050301u);
-            *reinterpret_cast<uint32_t *>(planes + o + 3 * plane) = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
+            uint8_t *pb = planes + ((Lo.pbuf == 2 && (p & 1)) ? 6 * plane : 0);
+            *reinterpret_cast<uint32_t *>(pb + o) = __builtin_amdgcn_perm(x23, x01, 0x07050301u);
+            *reinterpret_cast<uint32_t *>(pb + o + 3 * plane) = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
           }
         }
         stamp(2);
@@ -900,7 +905,8 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         const int it = hw + kHW * k;
         const int chn = it - 3 * (it / 3);
         const int hw0 = hw0k[k], hks = k < nk ? hksk[k] : 0;
-        const uint8_t *ph = planes + chn * plane, *pl = ph + 3 * plane;
+        const uint8_t *ph = planes + ((Lo.pbuf == 2 && ((p - 1) & 1)) ? 6 * plane : 0) + chn * plane,
+                      *pl = ph + 3 * plane;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
           if (t >= hks) break;
@@ -913,7 +919,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) atomicAdd(static_cast<unsigned *>(__builtin_assume_aligned(lds + O.cnt, 16)), 1u);
+      if (lane == 0 && Lo.pbuf == 1) atomicAdd(static_cast<unsigned *>(__builtin_assume_aligned(lds + O.cnt, 16)), 1u);
 #pragma unroll
       for (int k = 0; k < 2; k++) {
         if (k >= nk) break;
@@ -952,7 +958,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       stamp(2);
     } else if (M != 1 && M != 2 && p < N + 1) {
       // no block this phase (p == 0): count the (empty) plane reads
-      if (lane == 0) atomicAdd(static_cast<unsigned *>(__builtin_assume_aligned(lds + O.cnt, 16)), 1u);
+      if (lane == 0 && Lo.pbuf == 1) atomicAdd(static_cast<unsigned *>(__builtin_assume_aligned(lds + O.cnt, 16)), 1u);
     }
     stamp(3);
     if (p < N) rH = read_rec(p);
@@ -971,11 +977,12 @@ int vr_read_stamps(uint64_t *out, int slots) {
 
 // LDS of a launch: the ring takes what the other regions leave (R a multiple
 // of 32, at most 256 rows); R = 0 when even the smallest ring does not fit
-VrLayout vr_lds_layout(int vpitch, bool q16) {
+VrLayout vr_lds_layout(int vpitch, bool q16, int pbuf) {
   VrLayout L{};
   L.plane = 16 * vpitch + kPlanePad;
   L.otile_bytes = ((q16 ? kVmOtileBytes : 16 * kOt8Pitch) + 15) & ~15;
-  const int rest = 2 * kABytes + 8 * kRecBytes + 16 + kLutSlots * 1024 + 6 * L.plane;
+  L.pbuf = pbuf == 2 ? 2 : 1;
+  const int rest = 2 * kABytes + 8 * kRecBytes + 16 + kLutSlots * 1024 + 6 * L.pbuf * L.plane;
   const int fixed = ((rest + 15) & ~15) + 2 * L.otile_bytes;
   int R = (kVrMaxLds - fixed) / 512 / 32 * 32;
   if (R > 256) R = 256;
