@@ -216,6 +216,8 @@ struct fi_ctx {
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
   bool fast_rs = true;  // FI_FORCE_GENERIC=1: the generic two-pass resample (and smartcrop) kernels only
   bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
+  int vr_nl = 0;         // k_rs_vr loader waves forced (FI_VR_NL=2 / 4; 0: by geometry)
+  int vr_pbuf = 0;       // k_rs_vr plane buffers forced (FI_VR_PBUF=1 / 2; 0: by ring room)
   int vr_max_classes = 8;  // batches with more vertical tables stay on k_rs_vm (FI_VR_MAX_CLASSES)
   bool vm_lpt = true;      // k_rs_vm tiles: LPT images -> XCDs, longest tiles first (FI_VM_LPT=0: round robin)
   int res_align = 16;      // row pitch alignment of the resized image kept for smartcrop apply (FI_RES_ALIGN)
@@ -1562,21 +1564,16 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   VrLayout L = vr_lds_layout(vpitch, q16, 1);
   if (L.R <= 0) return false;
   // loader waves: 4 when every strip has one 16-px output block (3 items: one
-  // per H wave) and every touched-row list is evenly spaced (the pair-class copy
-  // of an uneven list is laid out for 2 loaders).  Measured (round 5): cfg5
-  // resize 8.45 -> 7.83 ms; cfg2 (two blocks a strip, two items per H wave)
-  // neutral, cfg3 1 % slower, so they keep 2.  FI_VR_NL=2 / 4 forces (4 only
-  // where it is valid: <= 2 blocks a strip)
+  // per H wave).  Measured (round 5): cfg5 resize 8.45 -> 7.83 ms; cfg2 (two
+  // blocks a strip, two items per H wave) neutral, cfg3 1 % slower, so they
+  // keep 2.  FI_VR_NL=2 / 4 forces (4 only where it is valid: <= 2 blocks a
+  // strip)
   {
     int max_nocb = 0;
-    bool even = true;
-    for (const VrWork &w : work) {
+    for (const VrWork &w : work)
       for (int st = 0; st < w.nstrips; st++) max_nocb = std::max(max_nocb, Bp.vstrips[w.first_strip + st].nocb);
-      even = even && (w.V->rstep != 0 || w.V->rows.size() <= 1);
-    }
-    static const char *nl_env = getenv("FI_VR_NL");
-    const int want = nl_env ? atoi(nl_env) : (max_nocb <= 1 ? 4 : 2);
-    L.nl = (want == 4 && even && max_nocb <= 2) ? 4 : 2;
+    const int want = c->vr_nl ? c->vr_nl : (max_nocb <= 1 ? 4 : 2);
+    L.nl = (want == 4 && max_nocb <= 2) ? 4 : 2;
   }
   // per image: a VDesc with the block-major tables
   std::vector<int32_t> desc_of(work.size());
@@ -1588,17 +1585,21 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
       o[0] = put(V.rows);
       E.ai.insert(E.ai.end(), 32, 0);
       if (V.rstep == 0 && !V.rows.empty()) {
-        // the uneven list again, as each k_rs_vr loader wave walks it: class
-        // rho = k & 3, entry j = the pair (rows[4 j + rho], rows[4 j + rho + 1]),
-        // so a wave's own pairs (4 apart) are 16 consecutive ints per 8 pairs
-        const int n = (int)V.rows.size(), J = vr_pair_cls_len(n);
-        std::vector<int32_t> p4(8 * (size_t)J);
-        for (int k = 0; k < 4 * J; k++) {  // the pair starting at list row k (fi_internal.h vr_pair_off)
-          const size_t o = (size_t)(vr_pair_off(n, k) - (n + 32));
-          p4[o] = V.rows[std::min(k, n - 1)];
-          p4[o + 1] = V.rows[std::min(k + 1, n - 1)];
+        // the uneven list again, as each k_rs_vr loader wave walks it (for 2
+        // and for 4 loader waves): class rho = k mod C, entry j = the pair
+        // (rows[C j + rho], rows[C j + rho + 1]), so a wave's own pairs (C = 2 NL
+        // apart) are consecutive ints
+        const int n = (int)V.rows.size(), J4 = vr_pair_cls_len(n, 4), J8 = vr_pair_cls_len(n, 8);
+        std::vector<int32_t> pc(8 * (size_t)J4 + 16 * (size_t)J8);
+        for (int C : {4, 8}) {
+          const int J = C == 4 ? J4 : J8;
+          for (int k = 0; k < C * J; k++) {  // the pair starting at list row k (fi_internal.h vr_pair_off)
+            const size_t o = (size_t)(vr_pair_off(n, k, C) - (n + 32));
+            pc[o] = V.rows[std::min(k, n - 1)];
+            pc[o + 1] = V.rows[std::min(k + 1, n - 1)];
+          }
         }
-        put(p4);
+        put(pc);
       }
       align4();
       o[1] = put(V.bmeta);
@@ -1689,8 +1690,7 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
       for (int b = 0; b + 1 < w.V->nblk; b++) step = std::max(step, bm[4 * (b + 1)] - bm[4 * b]);
     }
     const VrLayout L2 = vr_lds_layout(vpitch, q16, 2);
-    static const char *pb_env = getenv("FI_VR_PBUF");
-    const int want = pb_env ? atoi(pb_env) : (L2.R - inner >= std::max(32, step / 2) ? 2 : 1);
+    const int want = c->vr_pbuf ? c->vr_pbuf : (L2.R - inner >= std::max(32, step / 2) ? 2 : 1);
     L1 = L;
     if (want == 2 && L2.R >= inner) {
       L = L2;
@@ -2938,9 +2938,12 @@ int fi_create(fi_ctx **out, int32_t device) {
   // fallbacks testable on geometries that would not reach them otherwise:
   //   FI_FORCE_GENERIC=1   the generic two-pass resample and per-row smartcrop kernels
   //   FI_VR_RS=0           k_rs_vm instead of k_rs_vr (vertical-first)
+  //   FI_VR_NL=2|4, FI_VR_PBUF=1|2  k_rs_vr's loader waves / plane buffers (where valid)
   //   FI_DISABLE_SC_FZ=1   k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   if (const char *e = getenv("FI_FORCE_GENERIC")) c->fast_rs = c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
+  if (const char *e = getenv("FI_VR_NL")) c->vr_nl = atoi(e);
+  if (const char *e = getenv("FI_VR_PBUF")) c->vr_pbuf = atoi(e);
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';
   if (const char *e = getenv("FI_SC_MFMA")) c->sc_mf = e[0] == '1';

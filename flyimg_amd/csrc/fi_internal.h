@@ -266,12 +266,15 @@ constexpr int kVrMaxLds = 160 * 1024;  // k_rs_vr: one 1024-thread workgroup per
 // positions [g0, g0 + glen) (kbase, g0, glen multiples of 16), ring slot of
 // stream row G = G mod R.
 // k_rs_vr's uneven touched-row list (rows[nrows], a 32-entry pad) is followed
-// by a copy in per-wave pair classes: class rho = k & 3, entry j = the pair
-// (rows[4 j + rho], rows[4 j + rho + 1]) of J = ceil(nrows / 4) + 16 entries.
-// Offset (int32 units, from the list start) of the pair starting at row k:
-__host__ __device__ inline int vr_pair_cls_len(int nrows) { return (nrows + 3) / 4 + 16; }
-__host__ __device__ inline int vr_pair_off(int nrows, int k) {
-  return nrows + 32 + 2 * ((k & 3) * vr_pair_cls_len(nrows) + (k >> 2));
+// by two copies in per-wave pair classes, one per loader-wave count NL (a
+// wave's own pairs are C = 2 NL rows apart): class rho = k mod C, entry j = the
+// pair (rows[C j + rho], rows[C j + rho + 1]) of J_C = ceil(nrows / C) + 16
+// entries; the C = 4 copy first, then the C = 8 one.  Offset (int32 units,
+// from the list start) of the pair starting at row k:
+__host__ __device__ inline int vr_pair_cls_len(int nrows, int C) { return (nrows + C - 1) / C + 16; }
+__host__ __device__ inline int vr_pair_off(int nrows, int k, int C) {
+  const int base = nrows + 32 + (C == 8 ? 8 * vr_pair_cls_len(nrows, 4) : 0);
+  return base + 2 * ((k & (C - 1)) * vr_pair_cls_len(nrows, C) + k / C);
 }
 struct VrTile {
   int32_t img, strip, b0, b1, g0, kbase, glen, pad;

@@ -386,12 +386,13 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         }
         const int seg = min(limit, RT.g0 + RT.glen);
         int k0 = RT.kbase + (rG - RT.g0);
-        if (NL == 2 && r_rstep == 0 && k0 + 1 < r_nrows) {
-          const int cnt = min((seg - rG + 3) >> 2, (r_nrows - 1 - k0 + 3) >> 2);
-          // the host's pair list (after the row list and its 32-entry pad):
-          // class k0 & 3, own pair m at entry (k0 >> 2) + m, PL pairs per wait
-          // (scalar loads complete out of order: each wait is lgkmcnt(0))
-          const WL *lst = reinterpret_cast<const WL *>(ai + r_rows + vr_pair_off(r_nrows, k0));
+        if (r_rstep == 0 && k0 + 1 < r_nrows) {
+          const int cnt = min((seg - rG + kPS - 1) / kPS, (r_nrows - 1 - k0 + kPS - 1) / kPS);
+          // the host's pair list for kPS-row cycles (after the row list and its
+          // 32-entry pad): class k0 mod kPS, own pair m at entry k0 / kPS + m,
+          // PL pairs per wait (scalar loads complete out of order: each wait is
+          // lgkmcnt(0))
+          const WL *lst = reinterpret_cast<const WL *>(ai + r_rows + vr_pair_off(r_nrows, k0, kPS));
           for (int j0 = 0; j0 < cnt; j0 += PL) {
             const WL c0 = ldc(lst + j0 / PL);
             const int jn = cnt - j0;
@@ -404,12 +405,12 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
               if (16 * (int)lc >= r_nbytes) lc = 0;
               const uint32_t voff = (h ? (uint32_t)((int64_t)(r1 - r0) * r_stride) : 0u) + 16u * lc;
               dma16(lds_addr(lds) + (uint32_t)(O.ring + rslot * 512), r_src + (int64_t)r0 * r_stride + r_b0, voff);
-              rslot += 4;
+              rslot += kPS;
               if (rslot >= R) rslot -= R;
             }
           }
           n += cnt;
-          rG += 4 * cnt;
+          rG += kPS * cnt;
           continue;
         }
         if (k0 + 1 < r_nrows) {

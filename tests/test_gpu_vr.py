@@ -128,3 +128,35 @@ def test_output_independent_of_cobatched_images(pair):
     assert rc == 0 and all(r.status == 0 for r in recs)
     assert vr.stats("path_vm")[1] - b_vm == len(srcs) and vr.stats("path_vr")[1] == b_vr  # > 8 classes
     assert np.array_equal(mixed[0], alone[0])
+
+
+ROLE_CASES = [
+    (1920, 1080, "w_500", 6),  # cfg2: 3 output blocks a strip (4 loaders need <= 2: stays at 2)
+    (3840, 2160, "w_512,h_512,c_1", 4),
+    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", 3),
+    (4000, 3000, "w_150", 3),  # uneven rows: the 8-row pair classes with 4 loaders
+    (3000, 2000, "w_300,h_250,c_1", 5),
+    (333, 517, "w_97", 4),
+]
+
+
+@pytest.mark.parametrize("nl,pbuf", [(2, 1), (2, 2), (4, 1), (4, 2)])
+def test_vr_role_splits_and_plane_buffers(pair, nl, pbuf):
+    """every loader-wave count (FI_VR_NL, where valid) and plane-buffer count
+    (FI_VR_PBUF, where the ring fits) gives k_rs_vm's bytes"""
+    _, vm = pair
+    ctx = _context_with({"FI_VR_RS": "1", "FI_FORCE_GENERIC": "0", "FI_VR_NL": str(nl), "FI_VR_PBUF": str(pbuf)})
+    try:
+        for W, H, opts, n in ROLE_CASES:
+            op = ImageProcessor(OptionsBag(opts), W, H).to_op()
+            srcs = [synth_rgb(W, H, 900 + k) for k in range(n)]
+            before = ctx.stats("path_vr")[1]
+            ob, rb, rc = ctx.process(srcs, [op] * n)
+            assert rc == 0 and all(r.status == 0 for r in rb), L.lib().fi_last_error()
+            assert ctx.stats("path_vr")[1] == before + n
+            oa, _, rca = vm.process(srcs, [op] * n)
+            assert rca == 0
+            for k in range(n):
+                assert np.array_equal(ob[k], oa[k]), f"{opts} nl {nl} pbuf {pbuf} image {k}"
+    finally:
+        ctx.close()
