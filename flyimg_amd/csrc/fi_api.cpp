@@ -217,8 +217,9 @@ struct fi_ctx {
   bool fast_rs = true;  // FI_FORCE_GENERIC=1: the generic two-pass resample (and smartcrop) kernels only
   bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
   int vr_nl = 0;         // k_rs_vr loader waves forced (FI_VR_NL=2 / 4; 0: by geometry)
+  bool vr_split = true;  // k_rs_vr: one-block strips in a launch of their own (FI_VR_SPLIT=0: one launch)
   int vr_pbuf = 0;       // k_rs_vr plane buffers forced (FI_VR_PBUF=1 / 2; 0: by ring room)
-  int vr_max_classes = 8;  // batches with more vertical tables stay on k_rs_vm (FI_VR_MAX_CLASSES)
+  int vr_max_classes = 1 << 30;  // batches with more vertical tables stay on k_rs_vm (FI_VR_MAX_CLASSES)
   bool vm_lpt = true;      // k_rs_vm tiles: LPT images -> XCDs, longest tiles first (FI_VM_LPT=0: round robin)
   int res_align = 16;      // row pitch alignment of the resized image kept for smartcrop apply (FI_RES_ALIGN)
   bool timing_resize_only = false;  // fi_set_timing(2): stage timing events around the resample only
@@ -1154,10 +1155,14 @@ struct BatchPlan {
   std::vector<MStrip> vstrips;
   std::vector<VTile> vtiles;
   // k_rs_vr: persistent block-major tiles, per-workgroup {phases, stream rows}, LDS layout
+  // (one or more launches: their tiles and per-workgroup info back to back)
+  struct VrLaunch {
+    int32_t tile0, ntiles, info0, G, images;
+    VrLayout L;
+  };
   std::vector<VrTile> vrtiles;
   std::vector<int32_t> vr_info;
-  int vr_G = 0, vr_images = 0;
-  VrLayout vr_L{};
+  std::vector<VrLaunch> vrl;
   size_t vm_lds = 0;
   std::vector<HvDesc> hdescs;
   std::vector<HvStripD> hstrips;
@@ -1791,14 +1796,15 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
       for (int b = 0; b + 1 < w.V->nblk; b++) rpb = std::max(rpb, bm[4 * (b + 1)] - bm[4 * b]);
       for (int st = 0; st < w.nstrips; st++) nocb = std::max(nocb, Bp.vstrips[w.first_strip + st].nocb);
     }
-    fprintf(stderr, "vr: R %d pbuf %d nl %d vpitch %d inner %d K0 step max %d nocb %d tiles %d G %d\n", L.R, L.pbuf,
-            L.nl, vpitch, inner, rpb, nocb, ntiles, G);
+    int hist[4] = {0, 0, 0, 0};
+    for (const VrTile &t : tiles) hist[std::min(3, Bp.vstrips[t.strip].nocb)]++;
+    fprintf(stderr, "vr: R %d pbuf %d nl %d vpitch %d inner %d K0 step max %d nocb %d (tiles by nocb %d %d %d) tiles %d G %d\n",
+            L.R, L.pbuf, L.nl, vpitch, inner, rpb, nocb, hist[1], hist[2], hist[3], ntiles, G);
   }
-  Bp.vrtiles = std::move(tiles);
-  Bp.vr_info = std::move(info);
-  Bp.vr_G = G;
-  Bp.vr_L = L;
-  Bp.vr_images = (int)work.size();
+  Bp.vrl.push_back(BatchPlan::VrLaunch{(int32_t)Bp.vrtiles.size(), (int32_t)tiles.size(), (int32_t)Bp.vr_info.size(),
+                                        G, (int32_t)work.size(), L});
+  Bp.vrtiles.insert(Bp.vrtiles.end(), tiles.begin(), tiles.end());
+  Bp.vr_info.insert(Bp.vr_info.end(), info.begin(), info.end());
   return true;
 }
 
@@ -1920,10 +1926,13 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   }
   // k_rs_vr (default; FI_VR_RS=0 turns it off): the images whose vertical axis has block-major
   // tables (fi_plan.h VrV) run on the persistent block-major kernel
-  Bp.vr_G = 0;
+  Bp.vrl.clear();
+  Bp.vrtiles.clear();
+  Bp.vr_info.clear();
   if (c->vr_rs) {
     std::vector<Work1> rest;
     std::vector<VrWork> vr;
+    std::vector<Work1> vr_w;  // the Work1 of each vr entry (back to k_rs_vm if its launch cannot be built)
     for (const Work1 &w : work) {
       auto it = c->vrv_cache.find(w.vt);
       if (it == c->vrv_cache.end()) {
@@ -1935,18 +1944,43 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
       const int64_t gap = V.maxgap;  // the DMA's per-lane row offset
       bool narrow = true;  // five H waves take two horizontal items each: <= 3 16-px blocks per strip
       for (int st = 0; st < w.nstrips; st++) narrow = narrow && Bp.vstrips[w.first_strip + st].nocb <= 3;
-      if (V.nblk > 0 && w.hsh > 0 && narrow && gap * Bp.vdescs[w.img].src_stride < ((int64_t)1 << 31))
+      if (V.nblk > 0 && w.hsh > 0 && narrow && gap * Bp.vdescs[w.img].src_stride < ((int64_t)1 << 31)) {
         vr.push_back({w.img, w.first_strip, w.nstrips, &V, w.hwsum2, w.hsh});
-      else
+        vr_w.push_back(w);
+      } else {
         rest.push_back(w);
+      }
     }
-    // a persistent launch with static tile lists pays for mixed geometries
-    // (uneven tiles, per-tile table changes): measured on cfg4's mix (384 size
-    // classes x five ops) k_rs_vm took 385 ms against 432 with k_rs_vr, so a
-    // batch with more than kVrMaxClasses vertical tables stays on k_rs_vm
+    // mixed geometries (cfg4's 384 size classes x five ops) were slower on
+    // k_rs_vr than on k_rs_vm in round 4 (432 vs 385 ms), hence a class cap
+    // (FI_VR_MAX_CLASSES); since round 5 (4 loader waves for one-block strips,
+    // their own launch) k_rs_vr takes them: cfg4 resize 363 -> 329 ms per step
     std::set<const VrV *> classes;
     for (const VrWork &w : vr) classes.insert(w.V);
-    if (!vr.empty() && (int)classes.size() <= c->vr_max_classes && build_vr_tiles(c, E, Bp, vr)) work.swap(rest);
+    if (!vr.empty() && (int)classes.size() <= c->vr_max_classes) {
+      // two launches when the batch mixes strips of one 16-px output block
+      // (4 loader waves) with wider ones (2) and both halves fill the chip
+      std::vector<int> grp(vr.size(), 0);
+      int64_t nst[2] = {0, 0};
+      for (size_t k = 0; k < vr.size(); k++) {
+        int mx = 0;
+        for (int st = 0; st < vr[k].nstrips; st++) mx = std::max(mx, Bp.vstrips[vr[k].first_strip + st].nocb);
+        grp[k] = mx <= 1 ? 0 : 1;
+        nst[grp[k]] += vr[k].nstrips;
+      }
+      const bool split = c->vr_split && nst[0] >= 2 * c->n_cu && nst[1] >= 2 * c->n_cu;
+      for (int g = 0; g < (split ? 2 : 1); g++) {
+        std::vector<VrWork> part;
+        std::vector<Work1> part_w;
+        for (size_t k = 0; k < vr.size(); k++)
+          if (!split || grp[k] == g) {
+            part.push_back(vr[k]);
+            part_w.push_back(vr_w[k]);
+          }
+        if (!build_vr_tiles(c, E, Bp, part)) rest.insert(rest.end(), part_w.begin(), part_w.end());
+      }
+      work.swap(rest);
+    }
   }
   // bands of blocks only when the batch is too small to fill the chip
   int64_t nst = 0;
@@ -2207,14 +2241,14 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
     if (K.L0.tiles)
       hipLaunchKernelGGL(k_rs_copy, dim3(K.L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(K.L0),
                          pre_p(K.L0), K.L0.n);
-    if (!Bp.vrtiles.empty()) {
+    for (const BatchPlan::VrLaunch &V : Bp.vrl) {
       const int vrc = launch_vr(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
-                                (const VrTile *)(ab + K.vrtile_off), (int)Bp.vrtiles.size(),
-                                (const int32_t *)(ab + K.vrinfo_off), Bp.vr_G, ai, Bp.vr_L);
-      if (vrc < 0) return set_err(FI_EDEVICE, "block-major MFMA resample launch rejected (LDS %d)", Bp.vr_L.total);
+                                (const VrTile *)(ab + K.vrtile_off) + V.tile0, V.ntiles,
+                                (const int32_t *)(ab + K.vrinfo_off) + V.info0, V.G, ai, V.L);
+      if (vrc < 0) return set_err(FI_EDEVICE, "block-major MFMA resample launch rejected (LDS %d)", V.L.total);
       if (vrc == 1) c->stats["vr_ablation"].launches += 1;  // FI_VR_VARIANT ablation: wrong pixels
-      c->stats["path_vr"].launches += Bp.vr_images;
-      c->stats["path_vm"].launches -= Bp.vr_images;
+      c->stats["path_vr"].launches += V.images;
+      c->stats["path_vm"].launches -= V.images;
     }
     if (!Bp.vtiles.empty() &&
                launch_vm(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
@@ -2943,6 +2977,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_FORCE_GENERIC")) c->fast_rs = c->sc_prep = !(e[0] == '1');
   if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
   if (const char *e = getenv("FI_VR_NL")) c->vr_nl = atoi(e);
+  if (const char *e = getenv("FI_VR_SPLIT")) c->vr_split = e[0] == '1';
   if (const char *e = getenv("FI_VR_PBUF")) c->vr_pbuf = atoi(e);
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';

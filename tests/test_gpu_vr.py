@@ -109,9 +109,9 @@ def test_vr_mixed_batch(pair):
 
 def test_output_independent_of_cobatched_images(pair):
     """an image's pixels depend only on the image -- alone its batch
-    runs k_rs_vr; inside a batch of more than FI_VR_MAX_CLASSES (8) vertical
-    geometries the batch takes k_rs_vm; the bytes are the same."""
-    vr, _ = pair
+    runs k_rs_vr; inside a batch of more vertical geometries than a context's
+    FI_VR_MAX_CLASSES (8 here) the batch takes k_rs_vm; the bytes are the same."""
+    vr = _context_with({"FI_VR_RS": "1", "FI_FORCE_GENERIC": "0", "FI_VR_MAX_CLASSES": "8"})
     W, H, opts = 1920, 1080, "w_500,clsp_Gray"
     src = synth_rgb(W, H, 4242)
     op = ImageProcessor(OptionsBag(opts), W, H).to_op()
@@ -128,6 +128,7 @@ def test_output_independent_of_cobatched_images(pair):
     assert rc == 0 and all(r.status == 0 for r in recs)
     assert vr.stats("path_vm")[1] - b_vm == len(srcs) and vr.stats("path_vr")[1] == b_vr  # > 8 classes
     assert np.array_equal(mixed[0], alone[0])
+    vr.close()
 
 
 ROLE_CASES = [
@@ -160,3 +161,29 @@ def test_vr_role_splits_and_plane_buffers(pair, nl, pbuf):
                 assert np.array_equal(ob[k], oa[k]), f"{opts} nl {nl} pbuf {pbuf} image {k}"
     finally:
         ctx.close()
+
+
+def test_vr_split_launches(pair):
+    """a batch that mixes one-block strips (4 loader waves) with wider ones in
+    numbers that fill the chip twice runs as two k_rs_vr launches; every image
+    equals k_rs_vm's bytes"""
+    vr, vm = pair
+    geo = [(1920, 1080, "w_500"), (4000, 3000, "w_150"), (1920, 1080, "w_500"), (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray")]
+    uniq = sorted(set(geo))
+    base = {g: [synth_rgb(g[0], g[1], 1300 + 7 * k + i) for i in range(2)] for k, g in enumerate(uniq)}
+    srcs, ops, gk = [], [], []
+    for k in range(80):
+        g = geo[k % len(geo)]
+        srcs.append(base[g][(k // len(geo)) % 2])
+        ops.append(ImageProcessor(OptionsBag(g[2]), g[0], g[1]).to_op())
+        gk.append((g, (k // len(geo)) % 2))
+    before = vr.stats("path_vr")[1]
+    ob, rb, rc = vr.process(srcs, ops)
+    assert rc == 0 and all(r.status == 0 for r in rb), L.lib().fi_last_error()
+    assert vr.stats("path_vr")[1] == before + len(srcs)
+    for g in uniq:
+        oa, _, rca = vm.process(base[g], [ImageProcessor(OptionsBag(g[2]), g[0], g[1]).to_op()] * 2)
+        assert rca == 0
+        for k in range(len(srcs)):
+            if gk[k][0] == g:
+                assert np.array_equal(ob[k], oa[gk[k][1]]), f"{g} image {k}: split k_rs_vr != k_rs_vm"
