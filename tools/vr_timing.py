@@ -45,9 +45,10 @@ with Context(0) as ctx:
     a = buf.reshape(256, 16, 6).astype(np.float64)
     a = a[a[:, 0, 5] > 0]
     ph = a[:, 0, 5].mean()
+    nl = int(os.environ.get("VR_NL", "2"))  # the launch's loader waves (fi_api.cpp picks 4 for one-block strips)
     roles = {"V": (range(0, 8), ["tile entry", "V-MFMA issue", "planes", "barrier", "plane wait"]),
-             "H": (range(8, 13 if VR else 14), ["-", "tile entry", "horizontal", "-", "barrier"]),
-             "L": (range(14, 16), ["A DMA", "records + row DMA", "vmcnt wait", "barrier"])}
+             "H": (range(8, 15 - nl), ["-", "tile entry", "horizontal", "-", "barrier"]),
+             "L": (range(16 - nl, 16), ["A DMA", "records + row DMA", "vmcnt wait", "barrier"])}
     print(f"{len(a)} workgroups, phases/WG {ph:.0f}; per-phase ticks by wave (mean over workgroups)")
     for r, (waves, names) in roles.items():
         for w in waves:
