@@ -170,7 +170,7 @@ struct Slot {
   size_t blob_cap = 0;
   void *res = nullptr;
   size_t res_cap = 0;
-  hipEvent_t done = nullptr;  // recorded (on rb_stream) after the batch's last readback
+  hipEvent_t done = nullptr;  // recorded after the batch's last readback (rb_stream for host outputs, else the batch stream)
   hipEvent_t rs_done = nullptr;  // resample stage of the batch done (main stream)
   hipEvent_t up_done = nullptr;  // the batch's sources / blob uploaded (up_stream)
   hipEvent_t sc_end = nullptr;   // the batch's last kernel done (sc_stream)
@@ -2322,34 +2322,41 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
 static int queue_readback(fi_ctx *c, BatchPlan &Bp, int slot, uint8_t *wb, double t_start,
                           std::shared_ptr<HostIo> host) {
   Slot &S = c->slots[slot];
-  if (!S.sc_end) HIP_TRY(hipEventCreateWithFlags(&S.sc_end, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(S.sc_end, c->sc_stream));
-  HIP_TRY(hipStreamWaitEvent(c->rb_stream, S.sc_end, 0));
+  // device outputs: the few result bytes go back on the batch's own stream
+  // (a cross-stream event costs the next batch's first kernel ~20-30 us of
+  // idle GPU, measured in round 5's kernel trace); host outputs (image bytes)
+  // on the readback stream, so the next batch's kernels overlap their copies
+  hipStream_t rs = host ? c->rb_stream : c->sc_stream;
+  if (rs != c->sc_stream) {
+    if (!S.sc_end) HIP_TRY(hipEventCreateWithFlags(&S.sc_end, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(S.sc_end, c->sc_stream));
+    HIP_TRY(hipStreamWaitEvent(rs, S.sc_end, 0));
+  }
   if (host) {
     // outputs to the host, behind the batch's last kernel on sc_stream: the
     // planned (pre-apply) bytes cover the applied crop, which is never larger
     double obytes = 0;
     for (int i = 0; i < Bp.n; i++)
       if (Bp.status[i] == FI_OK && host->user[i].dst) obytes += (double)Bp.imgs[i].out_stride * Bp.imgs[i].out_h;
-    Timer t(c, "d2h_out", obytes, c->rb_stream, c->rb_stream);
+    Timer t(c, "d2h_out", obytes, rs, rs);
     for (int i = 0; i < Bp.n; i++) {
       const fi_image &d = Bp.imgs[i];
       if (Bp.status[i] != FI_OK || !host->user[i].dst) continue;
       const size_t bytes = (size_t)d.out_stride * d.out_h;
       uint8_t *to = host->pin_off[i] < 0 ? host->user[i].dst : (uint8_t *)S.hpin + host->pin_off[i];
       HIP_TRY(hipMemcpyAsync(to, (uint8_t *)S.hio.p + host->dev_dst_off[i], bytes, hipMemcpyDeviceToHost,
-                             c->rb_stream));
+                             rs));
     }
   }
   uint8_t *rp = (uint8_t *)S.res;
   const size_t res_bytes = sizeof(ScResult) * Bp.sitems.size();
   const size_t outwh_bytes = sizeof(int32_t) * 2 * (size_t)Bp.n;
   if (!Bp.sitems.empty())
-    HIP_TRY(hipMemcpyAsync(rp, wb + Bp.results_off, res_bytes, hipMemcpyDeviceToHost, c->rb_stream));
+    HIP_TRY(hipMemcpyAsync(rp, wb + Bp.results_off, res_bytes, hipMemcpyDeviceToHost, rs));
   if (!Bp.apply.empty())
-    HIP_TRY(hipMemcpyAsync(rp + res_bytes, wb + Bp.outwh_off, outwh_bytes, hipMemcpyDeviceToHost, c->rb_stream));
+    HIP_TRY(hipMemcpyAsync(rp + res_bytes, wb + Bp.outwh_off, outwh_bytes, hipMemcpyDeviceToHost, rs));
   if (!S.done) HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(S.done, c->rb_stream));
+  HIP_TRY(hipEventRecord(S.done, rs));
   S.busy = true;
   c->next_slot = (slot + 1) % kSlots;
   PendingBatch pb;
