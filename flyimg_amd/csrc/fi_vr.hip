@@ -239,7 +239,8 @@ __device__ uint64_t g_vr_stamps[kVrStampSlots * kVrStampN];
 
 // MODE (profiling ablations, FI_VR_VARIANT; wrong pixels): 0 production,
 // 1 DMA stream only, 2 no H role and no stores, 3 no stores, 4 no A-fragment
-// DMAs after the first two blocks, 5 / 6 loader
+// DMAs after the first two blocks, 7 no V fold / float conversion, 8 no H
+// conversion, 5 / 6 loader
 // priority 1 / 0 (production pixels), 9 production + per-phase s_memtime sums;
 // 10 + k: ablation k with the stamps.
 template <int MODE, int NL>
@@ -686,6 +687,10 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           uint32_t q[4];
 #pragma unroll
           for (int i = 0; i < 4; i++) {
+            if (M == 7) {  // ablation: no fold / float conversion (wrong pixels, same LDS traffic)
+              q[i] = (uint32_t)acc[0][j][i];
+              continue;
+            }
             const int32_t tot = fold2(acc[0][j][i], acc[1][j][i]);
             q[i] = __float2uint_rz(fmaf((float)tot, vscale, 0.5f));
           }
@@ -942,17 +947,27 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         const int hx = 16 * ob + (lane & 15);
         if (hx < nx) {
           const float hws = hwsk[k];
+          // the four rows' conversions first (independent chains, no branch
+          // between them), then the stores in the tile's format
+          uint32_t q[4];
 #pragma unroll
           for (int i = 0; i < 4; i++) {
-            const float tot = 256.0f * (float)fold2(hh[0][i], hh[1][i]) + (float)fold2(hl[0][i], hl[1][i]) + hws;
-            const uint32_t q = min(__float2uint_rz(fmaf(tot, hscale, 0.5f)), 65535u);
-            const int yl = 4 * (lane >> 4) + i;
-            if (fast8) {
+            // 256 a + b as one fma: 256 a is exact in f32, so the one rounding
+            // is the add's (bit-identical to the product then the sum)
+            const float tot = fmaf(256.0f, (float)fold2(hh[0][i], hh[1][i]), (float)fold2(hl[0][i], hl[1][i])) + hws;
+            q[i] = M == 8 ? ((uint32_t)hh[0][i] & 0xFFFFu)  // ablation: no H conversion
+                          : min(__float2uint_rz(fmaf(tot, hscale, 0.5f)), 65535u);
+          }
+          if (fast8) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const int yl = 4 * (lane >> 4) + i;
               const int sh = (int)((sh0 + (uint32_t)(16 * b + yl) * shs) & 3u);
-              ot[yl * kOt8Pitch + sh + 3 * hx + chn] = (uint8_t)q16_to_u8(q);
-            } else {
-              otile[yl * kVmOtilePitch + 3 * hx + chn] = (uint16_t)q;
+              ot[yl * kOt8Pitch + sh + 3 * hx + chn] = (uint8_t)q16_to_u8(q[i]);
             }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) otile[(4 * (lane >> 4) + i) * kVmOtilePitch + 3 * hx + chn] = (uint16_t)q[i];
           }
         }
       }
@@ -1019,6 +1034,8 @@ int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrT
     case 5: FI_VR_LAUNCH(5); break;
     case 4: FI_VR_LAUNCH(4); break;
     case 6: FI_VR_LAUNCH(6); break;
+    case 7: FI_VR_LAUNCH(7); break;
+    case 8: FI_VR_LAUNCH(8); break;
     case 9: FI_VR_LAUNCH(9); break;
     case 14: FI_VR_LAUNCH(14); break;
     case 11: FI_VR_LAUNCH(11); break;
@@ -1027,7 +1044,8 @@ int launch_vr(hipStream_t s, const VDesc *descs, const MStrip *strips, const VrT
     default: FI_VR_LAUNCH(0); break;
   }
 #undef FI_VR_LAUNCH
-  return (v == 1 || v == 2 || v == 3 || v == 4 || v == 11 || v == 12 || v == 13 || v == 14) ? 1 : 0;
+  return (v == 1 || v == 2 || v == 3 || v == 4 || v == 7 || v == 8 || v == 11 || v == 12 || v == 13 || v == 14) ? 1
+                                                                                                             : 0;
 }
 
 }  // namespace fi
