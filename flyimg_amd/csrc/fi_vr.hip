@@ -831,7 +831,18 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         }
       }
       // dword-aligned fast8 stores of block p - 2: rows sw, sw + kSW, ... as dwords
-      if (st_fast) {
+      if (st_fast && (st_nb >> 2) <= 64) {
+        // one destination dword per lane, row by row: the row base is scalar and
+        // the tile row an immediate, so the copy needs no per-element VALU
+        if (lane < (st_nb >> 2)) {
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            if (r >= st_nrow) break;
+            *(g_u32 *)(st_row0 + r * st_stride + 4 * lane) =
+                *reinterpret_cast<const uint32_t *>(st_ot + r * kSW * kOt8Pitch + 4 * lane);
+          }
+        }
+      } else if (st_fast) {
         const int U = st_nb >> 2;
         const float invU = 1.0f / (float)U;
         for (int it0 = 0; it0 < st_nrow * U; it0 += 64) {
@@ -856,6 +867,7 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
   uint32_t h_sh0 = 0, h_shs = 0;
   i32x4 hb[2][2][2];
   int hw0k[2] = {0, 0}, hksk[2] = {0, 0};
+  uint32_t hoff[2][2][2] = {};  // per item and k-step: this lane's two plane-column offsets (tile-constant)
   float hwsk[2] = {0.f, 0.f}, hscale = 0.f;
   __builtin_amdgcn_s_setprio(1);
   phase_barrier();
@@ -887,6 +899,12 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           const bool ok = it < 3 * S.nocb;
           hw0k[k] = ok ? ldc1(ai + S.s0 + 2 * ob) : 0;
           hksk[k] = ok ? ldc1(ai + S.s0 + 2 * ob + 1) : 0;
+#pragma unroll
+          for (int t = 0; t < 2; t++) {
+            const int cA = hw0k[k] + 64 * t + 16 * (lane >> 4) + ((lane & 15) >> 1);
+            hoff[k][t][0] = (uint32_t)(col_off(cA) + 8 * (lane & 1));
+            hoff[k][t][1] = (uint32_t)(col_off(cA + 8) + 8 * (lane & 1));
+          }
           const int hx = 16 * ob + (lane & 15);
           hwsk[k] = (ok && hx < nx) ? 32896.0f * (float)ai[D.hwsum + S.x0 + hx] : 0.0f;
 #pragma unroll
@@ -910,14 +928,13 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
       for (int k = 0; k < 2; k++) {
         const int it = hw + kHW * k;
         const int chn = it - 3 * (it / 3);
-        const int hw0 = hw0k[k], hks = k < nk ? hksk[k] : 0;
+        const int hks = k < nk ? hksk[k] : 0;
         const uint8_t *ph = planes + ((Lo.pbuf == 2 && ((p - 1) & 1)) ? 6 * plane : 0) + chn * plane,
                       *pl = ph + 3 * plane;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
           if (t >= hks) break;
-          const int cA = hw0 + 64 * t + 16 * (lane >> 4) + ((lane & 15) >> 1);
-          const int o0 = col_off(cA) + 8 * (lane & 1), o1 = col_off(cA + 8) + 8 * (lane & 1);
+          const uint32_t o0 = hoff[k][t][0], o1 = hoff[k][t][1];
           const i32x2 h0 = tr8(ph + o0), h1 = tr8(ph + o1);
           const i32x2 l0 = tr8(pl + o0), l1 = tr8(pl + o1);
           Ahk[k][t] = i32x4{h0.x, h0.y, h1.x, h1.y};
