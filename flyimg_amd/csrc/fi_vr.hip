@@ -685,14 +685,19 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
         for (int j = 0; j < kT; j++) {
           const uint32_t o = (vcolp[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
           uint32_t q[4];
+          if (M == 7) {  // ablation: no fold / float conversion (wrong pixels, same LDS traffic)
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            if (M == 7) {  // ablation: no fold / float conversion (wrong pixels, same LDS traffic)
-              q[i] = (uint32_t)acc[0][j][i];
-              continue;
+            for (int i = 0; i < 4; i++) q[i] = (uint32_t)acc[0][j][i];
+          } else {
+            // two rows per packed fma (v_pk_fma_f32: the same IEEE fma per element)
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int i = 0; i < 4; i += 2) {
+              const f32x2 t = {(float)fold2(acc[0][j][i], acc[1][j][i]), (float)fold2(acc[0][j][i + 1], acc[1][j][i + 1])};
+              const f32x2 r = __builtin_elementwise_fma(t, f32x2{vscale, vscale}, f32x2{0.5f, 0.5f});
+              q[i] = __float2uint_rz(r.x);
+              q[i + 1] = __float2uint_rz(r.y);
             }
-            const int32_t tot = fold2(acc[0][j][i], acc[1][j][i]);
-            q[i] = __float2uint_rz(fmaf((float)tot, vscale, 0.5f));
           }
           const auto p01 = __builtin_amdgcn_cvt_pk_u16(q[0], q[1]);
           const auto p23 = __builtin_amdgcn_cvt_pk_u16(q[2], q[3]);
@@ -967,13 +972,20 @@ __global__ __launch_bounds__(1024, 1) void k_rs_vr(const VDesc *__restrict__ des
           // the four rows' conversions first (independent chains, no branch
           // between them), then the stores in the tile's format
           uint32_t q[4];
+          // two rows per packed op (v_pk_fma_f32 / v_pk_add_f32: the same IEEE
+          // operations per element); 256 a + b as one fma: 256 a is exact in
+          // f32, so the one rounding is the add's (bit-identical to the product
+          // then the sum)
+          typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            // 256 a + b as one fma: 256 a is exact in f32, so the one rounding
-            // is the add's (bit-identical to the product then the sum)
-            const float tot = fmaf(256.0f, (float)fold2(hh[0][i], hh[1][i]), (float)fold2(hl[0][i], hl[1][i])) + hws;
+          for (int i = 0; i < 4; i += 2) {
+            const f32x2 a = {(float)fold2(hh[0][i], hh[1][i]), (float)fold2(hh[0][i + 1], hh[1][i + 1])};
+            const f32x2 c = {(float)fold2(hl[0][i], hl[1][i]), (float)fold2(hl[0][i + 1], hl[1][i + 1])};
+            const f32x2 tot = __builtin_elementwise_fma(f32x2{256.0f, 256.0f}, a, c) + f32x2{hws, hws};
+            const f32x2 r = __builtin_elementwise_fma(tot, f32x2{hscale, hscale}, f32x2{0.5f, 0.5f});
             q[i] = M == 8 ? ((uint32_t)hh[0][i] & 0xFFFFu)  // ablation: no H conversion
-                          : min(__float2uint_rz(fmaf(tot, hscale, 0.5f)), 65535u);
+                          : min(__float2uint_rz(r.x), 65535u);
+            q[i + 1] = M == 8 ? ((uint32_t)hh[0][i + 1] & 0xFFFFu) : min(__float2uint_rz(r.y), 65535u);
           }
           if (fast8) {
 #pragma unroll
