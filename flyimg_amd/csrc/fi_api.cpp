@@ -62,7 +62,8 @@ int launch_sc_score(hipStream_t s, int mode, const ScDesc *descs, int n, size_t 
                     const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P, const int32_t *ai);
 int launch_sc_score3(hipStream_t s, const ScDesc *descs, int n, size_t lds, const DevCrop *crops, const ScGroup *groups,
                      const double *ad, CropScore *scores, ScResult *results, const ScParamsDev &P, const int32_t *ai);
-int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results);
+int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results,
+                      int persistent_wgs);
 __global__ void k_synth(uint8_t *, int, int, int64_t, uint32_t);
 // tiled horizontal-first pass 1 (fi_kernels.hip)
 constexpr int kHTileRows = 16;  // fi_kernels.hip kHTRows
@@ -173,7 +174,9 @@ struct Slot {
   hipEvent_t done = nullptr;  // recorded after the batch's last readback (rb_stream for host outputs, else the batch stream)
   hipEvent_t rs_done = nullptr;  // resample stage of the batch done (main stream)
   hipEvent_t up_done = nullptr;  // the batch's sources / blob uploaded (up_stream)
-  hipEvent_t sc_end = nullptr;   // the batch's last kernel done (sc_stream)
+  hipEvent_t sc_end = nullptr;   // the batch's last kernel done (on its tail stream)
+  hipEvent_t sc_done = nullptr;  // the batch's smartcrop stage done (sc_stream; the crop apply waits for it)
+  hipStream_t tail = nullptr;    // the stream of the batch's last kernel (sc_stream, or ap_stream with the apply)
   bool busy = false;
   // device buffers of the in-flight batch: the uploaded blob (descriptors) and
   // the workspace (intermediates, smartcrop scratch, scores, results).  Per
@@ -198,6 +201,10 @@ struct fi_ctx {
   // kernels, batch k's readback during batch k+1's (the main stream waits for
   // up_done, the readback for sc_end; one slot's buffers per batch)
   hipStream_t up_stream = nullptr, rb_stream = nullptr;
+  // the crop apply of batch k beside batch k+1's resample (one workgroup per
+  // CU, no LDS: it fits next to k_rs_vr's); FI_APPLY_OVERLAP=0: on sc_stream
+  hipStream_t ap_stream = nullptr;
+  bool apply_overlap = true;
   std::mutex mu;
   DevBuf arena, work, io;
   DevBuf gather;  // RCCL record gather staging
@@ -275,6 +282,7 @@ static void sync_streams(fi_ctx *c) {
   if (c->sc_stream != c->stream) (void)hipStreamSynchronize(c->sc_stream);
   if (c->up_stream) (void)hipStreamSynchronize(c->up_stream);
   if (c->rb_stream) (void)hipStreamSynchronize(c->rb_stream);
+  if (c->ap_stream) (void)hipStreamSynchronize(c->ap_stream);
 }
 static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
   if (b->cap >= bytes) return FI_OK;
@@ -2229,6 +2237,7 @@ static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
 // resample (so they overlap the next batch's upload and resample).
 static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Packed &K, uint8_t *ab, uint8_t *wb,
                         Slot &S) {
+  S.tail = c->sc_stream;
   const int32_t *ai = (const int32_t *)c->heap_i.p;
   const float *af = (const float *)c->heap_f.p;
   const double *ad = (const double *)c->heap_d.p;
@@ -2308,9 +2317,19 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
                               (ScResult *)(wb + Bp.results_off), PD);
     if (rc) return rc;
     if (!Bp.apply.empty()) {
-      Timer t(c, "crop_apply", 0, c->sc_stream, c->sc_stream);
-      (void)launch_crop_apply(c->sc_stream, (const ApplyDesc *)(ab + K.apply_off), (int)Bp.apply.size(),
-                              (const DevCrop *)(ab + K.SX.crops_off), (const ScResult *)(wb + Bp.results_off));
+      hipStream_t as = c->sc_stream;
+      int pw = 0;
+      if (c->apply_overlap && c->ap_stream) {
+        if (!S.sc_done) HIP_TRY(hipEventCreateWithFlags(&S.sc_done, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(S.sc_done, c->sc_stream));
+        HIP_TRY(hipStreamWaitEvent(c->ap_stream, S.sc_done, 0));
+        as = c->ap_stream;
+        pw = c->n_cu;
+        S.tail = as;
+      }
+      Timer t(c, "crop_apply", 0, as, as);
+      (void)launch_crop_apply(as, (const ApplyDesc *)(ab + K.apply_off), (int)Bp.apply.size(),
+                              (const DevCrop *)(ab + K.SX.crops_off), (const ScResult *)(wb + Bp.results_off), pw);
     }
     HIP_TRY(hipGetLastError());
   }
@@ -2326,10 +2345,11 @@ static int queue_readback(fi_ctx *c, BatchPlan &Bp, int slot, uint8_t *wb, doubl
   // (a cross-stream event costs the next batch's first kernel ~20-30 us of
   // idle GPU, measured in round 5's kernel trace); host outputs (image bytes)
   // on the readback stream, so the next batch's kernels overlap their copies
-  hipStream_t rs = host ? c->rb_stream : c->sc_stream;
-  if (rs != c->sc_stream) {
+  hipStream_t tail = S.tail ? S.tail : c->sc_stream;
+  hipStream_t rs = host ? c->rb_stream : tail;
+  if (rs != tail) {
     if (!S.sc_end) HIP_TRY(hipEventCreateWithFlags(&S.sc_end, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(S.sc_end, c->sc_stream));
+    HIP_TRY(hipEventRecord(S.sc_end, tail));
     HIP_TRY(hipStreamWaitEvent(rs, S.sc_end, 0));
   }
   if (host) {
@@ -3001,8 +3021,10 @@ int fi_create(fi_ctx **out, int32_t device) {
     return set_err(FI_EDEVICE, "hipStreamCreate failed");
   }
   c->sc_stream = c->stream;
+  if (const char *e = getenv("FI_APPLY_OVERLAP")) c->apply_overlap = e[0] == '1';
   if (hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->ap_stream, hipStreamNonBlocking) != hipSuccess) {
     fi_destroy(c);
     return set_err(FI_EDEVICE, "hipStreamCreate failed");
   }
@@ -3037,6 +3059,7 @@ void fi_destroy(fi_ctx *c) {
   if (c->sc_stream != c->stream) (void)hipStreamDestroy(c->sc_stream);
   if (c->up_stream) (void)hipStreamDestroy(c->up_stream);
   if (c->rb_stream) (void)hipStreamDestroy(c->rb_stream);
+  if (c->ap_stream) (void)hipStreamDestroy(c->ap_stream);
   delete c;
 }
 

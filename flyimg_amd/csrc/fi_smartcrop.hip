@@ -1767,16 +1767,16 @@ __device__ __forceinline__ uint32_t ap_align(uint32_t hi, uint32_t lo, uint32_t 
 #define FI_APPLY_U 2
 #endif
 constexpr int kApplyU = FI_APPLY_U;  // chunks per thread whose loads go out together
-__global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict__ descs,
-                                                     const DevCrop *__restrict__ crops,
-                                                     const ScResult *__restrict__ results) {
-  const ApplyDesc &A = descs[blockIdx.y];
+// one (image, part) of the crop copy: part of nparts workgroup-sized slices
+__device__ __forceinline__ void crop_apply_item(const ApplyDesc *__restrict__ descs, const DevCrop *__restrict__ crops,
+                                                const ScResult *__restrict__ results, int img, int part, int nparts) {
+  const ApplyDesc &A = descs[img];
   const ScResult r = results[A.result];
   if (r.top < 0) return;
   const DevCrop c = crops[A.crop0 + r.top];
   const int gw = c.rw + c.rx, gh = c.rh + c.ry;
   const int ow = min(gw, A.W - c.rx), oh = min(gh, A.H - c.ry);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (part == 0 && threadIdx.x == 0) {
     A.out_wh[0] = ow;
     A.out_wh[1] = oh;
   }
@@ -1811,12 +1811,12 @@ __global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict
   const int64_t nchunk = head < total ? (total - head) / 16 : 0;
   const int64_t tail0 = head + 16 * nchunk;
   const int tid = threadIdx.x;
-  if (blockIdx.x == 0) {
+  if (part == 0) {
     for (int64_t o = tid; o < min<int64_t>(head, total); o += 256) A.dst[o] = *src_of(o);
     for (int64_t o = tail0 + tid; o < total; o += 256) A.dst[o] = *src_of(o);
   }
-  const int64_t cs = (int64_t)gridDim.x * 256;
-  for (int64_t k0 = (int64_t)blockIdx.x * 256 + tid; k0 < nchunk; k0 += kApplyU * cs) {
+  const int64_t cs = (int64_t)nparts * 256;
+  for (int64_t k0 = (int64_t)part * 256 + tid; k0 < nchunk; k0 += kApplyU * cs) {
     uint4 out[kApplyU];
 #pragma unroll
     for (int u = 0; u < kApplyU; u++) {
@@ -1858,6 +1858,20 @@ __global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict
       *reinterpret_cast<uint4 *>(A.dst + head + 16 * k) = out[u];
     }
   }
+}
+__global__ __launch_bounds__(256) void k_crop_apply3(const ApplyDesc *__restrict__ descs,
+                                                     const DevCrop *__restrict__ crops,
+                                                     const ScResult *__restrict__ results) {
+  crop_apply_item(descs, crops, results, blockIdx.y, blockIdx.x, gridDim.x);
+}
+// the same work from one workgroup per CU walking the (image, part) items: runs
+// beside the next batch's persistent resample (no LDS, few VGPRs: it fits next
+// to a 16-wave k_rs_vr workgroup, so neither kernel waits for the other's CUs)
+__global__ __launch_bounds__(256, 8) void k_crop_apply3p(const ApplyDesc *__restrict__ descs,
+                                                      const DevCrop *__restrict__ crops,
+                                                      const ScResult *__restrict__ results, int n) {
+  for (int item = blockIdx.x; item < n * kApplyChunks; item += gridDim.x)
+    crop_apply_item(descs, crops, results, item / kApplyChunks, item % kApplyChunks, kApplyChunks);
 }
 
 int launch_sc_h(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai) {
@@ -1919,9 +1933,14 @@ int launch_sc_score3(hipStream_t s, const ScDesc *descs, int n, size_t lds, cons
                      ai);
   return 0;
 }
-int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results) {
+int launch_crop_apply(hipStream_t s, const ApplyDesc *descs, int n, const DevCrop *crops, const ScResult *results,
+                      int persistent_wgs) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_crop_apply3, dim3(kApplyChunks, n), dim3(256), 0, s, descs, crops, results);
+  if (persistent_wgs > 0)
+    hipLaunchKernelGGL(k_crop_apply3p, dim3(min(persistent_wgs, n * kApplyChunks)), dim3(256), 0, s, descs, crops,
+                       results, n);
+  else
+    hipLaunchKernelGGL(k_crop_apply3, dim3(kApplyChunks, n), dim3(256), 0, s, descs, crops, results);
   return 0;
 }
 
