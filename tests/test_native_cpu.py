@@ -83,3 +83,21 @@ def test_hot_kernels_do_not_spill(src, kernels):
         sspill = int(re.search(r"SGPRs Spill: (\d+)", block).group(1))
         vspill = int(re.search(r"VGPRs Spill: (\d+)", block).group(1))
         assert scratch == 0 and vspill == 0 and sspill <= smax, (k, scratch, vspill, sspill)
+
+
+def test_vr_pair_class_list_layout():
+    """k_rs_vr's pair-class copies of an uneven row list for 2 and 4 loader
+    waves (fi_internal.h vr_pair_off): distinct slots inside each copy, a
+    wave's own pairs at consecutive entries (tests/native/vr_pair_list_check.cpp)."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "vpl")
+        subprocess.run([hipcc, "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"),
+                        "-I", os.path.join(ROOT, "flyimg_amd/csrc"),
+                        os.path.join(ROOT, "tests/native/vr_pair_list_check.cpp"), "-o", exe],
+                       check=True, capture_output=True, timeout=300)
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK (0 failures)" in r.stdout
