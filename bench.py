@@ -79,6 +79,7 @@ KERNEL_OF_PATH = {
 }
 # smartcrop prescale + maps kernel per image (counts kept by the library)
 SC_KERNEL_OF_PATH = {
+    "sc_path_ft": "k_sc_ft (prescale + maps, one workgroup per analysed-row chunk)",
     "sc_path_fd": "k_sc_fd (prescale + maps, source rows by LDS-DMA)",
     "sc_path_fz": "k_sc_fz (prescale + maps, register-staged source rows)",
 }
@@ -240,6 +241,27 @@ def launch_ranks(n: int) -> int:
     return 0
 
 
+def run_batches(ctx, arrs, nimg, k0, count, on_done):
+    """Batches k0 .. k0+count-1 of one rank, pipelined: submit batch k
+    (fi_submit_batch_device: planned and uploaded while batch k-1 runs), then
+    finalize batch k-1 (fi_wait(1)) and hand its records to on_done(k-1, arr).
+    Nothing here waits on another rank: the result gather is the caller's, once
+    after the last batch (RCCL on the library's gather stream), so no rank
+    blocks its next batch on a collective.  Returns after every batch is
+    finalized."""
+    from flyimg_amd import _lib as L
+
+    if count <= 0:
+        return
+    for k in range(k0, k0 + count):
+        L.check(ctx.submit_device(arrs[k % 2], nimg))
+        if k > k0:
+            L.check(ctx.wait(1))  # batch k-1 done (batch k still queued)
+            on_done(k - 1, arrs[(k - 1) % 2])
+    L.check(ctx.wait(0))
+    on_done(k0 + count - 1, arrs[(k0 + count - 1) % 2])
+
+
 def dry_run(args, rank, world, local_rank, comm):
     """Control-plane rehearsal of a multi-rank run: no library, no GPU.
     ``FI_DRY_RUN_FAIL_RANK=r`` makes rank r exit 3 after joining (launcher test)."""
@@ -330,24 +352,20 @@ def main():
             a.smartcrop_w, a.smartcrop_h = op.smartcrop_w, op.smartcrop_h
             a.dst, a.dst_capacity = dst + i * dst_cap, dst_cap
     bad = [0]
+    recs = []
 
-    def records(arr):
+    def records(k, arr):
         bad[0] += sum(1 for i in range(nimg) if arr[i].status != 0)
         if world > 1:
-            gather.gather([(rank * nimg + i, arr[i].status, arr[i].out_w, arr[i].out_h, arr[i].crop_x,
-                            arr[i].crop_y, arr[i].crop_w, arr[i].crop_h) for i in range(nimg)])
+            recs.extend((rank * nimg + i, arr[i].status, arr[i].out_w, arr[i].out_h, arr[i].crop_x,
+                         arr[i].crop_y, arr[i].crop_w, arr[i].crop_h) for i in range(nimg))
 
     def run(k0, count):
-        """Batches k0..k0+count-1, pipelined; returns after all are finalized."""
-        if count <= 0:
-            return
-        for k in range(k0, k0 + count):
-            L.check(ctx.submit_device(arrs[k % 2], nimg))
-            if k > k0:
-                L.check(ctx.wait(1))  # batch k-1 done (batch k still queued)
-                records(arrs[(k - 1) % 2])
-        L.check(ctx.wait(0))
-        records(arrs[(k0 + count - 1) % 2])
+        """Batches k0..k0+count-1, pipelined, then the final result gather."""
+        run_batches(ctx, arrs, nimg, k0, count, records)
+        if world > 1:
+            gather.gather(recs)  # the one exchange step: every batch's records to rank 0
+            recs.clear()
 
     run(0, args.warmup)
     bad[0] = 0

@@ -162,6 +162,9 @@ def lib():
     L.fi_rccl_get_unique_id.argtypes = [ctypes.c_char_p]
     L.fi_rccl_init.argtypes = [vp, i32, i32, ctypes.c_char_p]
     L.fi_rccl_gather_records.argtypes = [vp, P(FiRecord), i32, P(FiRecord)]
+    L.fi_rccl_gather_start.argtypes = [vp, P(FiRecord), i32, P(FiRecord)]
+    L.fi_rccl_gather_finish.argtypes = [vp]
+    L.fi_query.argtypes = [vp, P(i32)]
     L.fi_debug_monochrome.argtypes = [vp, vp, i32, i32, i32, vp, i32]
     L.fi_debug_convolve.argtypes = [vp, vp, i32, i32, i32, vp, ctypes.c_uint32, vp]
     L.fi_debug_skinsat.argtypes = [vp, vp, vp]

@@ -53,6 +53,8 @@ int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32
                  const uint16_t *skinsat);
 int launch_sc_fd(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
                  const uint16_t *skinsat);
+int launch_sc_ft(hipStream_t s, int ks, const ScDesc *descs, const int32_t *tiles, int ntiles, int lds,
+                 const int32_t *ai, const ScParamsDev &P, const uint16_t *skinsat);
 int launch_sc_skinsat(hipStream_t s, uint16_t *table, const ScParamsDev &P);
 int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c);
 int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *len, int n, uint8_t *const *dst,
@@ -177,6 +179,7 @@ struct Slot {
   hipEvent_t sc_end = nullptr;   // the batch's last kernel done (on its tail stream)
   hipEvent_t sc_done = nullptr;  // the batch's smartcrop stage done (sc_stream; the crop apply waits for it)
   hipStream_t tail = nullptr;    // the stream of the batch's last kernel (sc_stream, or ap_stream with the apply)
+  uintptr_t ap_lo = 0, ap_hi = 0;  // bytes its overlapped crop apply writes (empty: none pending)
   bool busy = false;
   // device buffers of the in-flight batch: the uploaded blob (descriptors) and
   // the workspace (intermediates, smartcrop scratch, scores, results).  Per
@@ -205,6 +208,22 @@ struct fi_ctx {
   // CU, no LDS: it fits next to k_rs_vr's); FI_APPLY_OVERLAP=0: on sc_stream
   hipStream_t ap_stream = nullptr;
   bool apply_overlap = true;
+  // recorded on ap_stream after every overlapped apply: entry points that
+  // launch on `stream` and may touch a batch's dst (face-blur, JPEG decode,
+  // synthetic fill, a later batch whose sources are an earlier batch's
+  // outputs) wait for it (order_after_apply), so the stream order the header
+  // promises holds across the two streams
+  hipEvent_t ap_tail = nullptr;
+  bool ap_pending = false;
+  // RCCL record gather: its own stream (no dependency on the batch streams),
+  // pinned staging, at most one gather in flight (fi_rccl_gather_start / _finish)
+  hipStream_t gx_stream = nullptr;
+  hipEvent_t gx_done = nullptr;
+  void *gx_pin = nullptr;
+  size_t gx_pin_cap = 0;
+  bool gx_pending = false;
+  fi_record *gx_recv = nullptr;  // caller's receive buffer of the gather in flight (rank 0)
+  size_t gx_recv_bytes = 0;
   std::mutex mu;
   DevBuf arena, work, io;
   DevBuf gather;  // RCCL record gather staging
@@ -233,6 +252,7 @@ struct fi_ctx {
   int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   bool sc_fd = true;        // FI_SC_FD=0: k_sc_fz instead of its LDS-DMA form k_sc_fd
+  bool sc_ft = true;        // FI_SC_FT=0: k_sc_fd (per image) instead of the chunk-tiled k_sc_ft
   bool sc_mf = true;        // FI_SC_MFMA=0: k_sc_score2 (f64 VALU fast pass) instead of k_sc_score3
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
   DevBuf jpeg[3];           // GPU JPEG decode: upload (compressed data + tables), -, coefficients + planes
@@ -260,6 +280,7 @@ struct fi_ctx {
   struct ScTabs {
     int32_t hb = 0, hk = 0, hkT = 0, vb = 0, vk = 0;
     int32_t hmB = 0, hmC = 0, hmS0 = 0, vqA = 0, vqC = 0, vqK0 = 0;
+    int32_t ftB = -1;
   };
   std::map<const AxisTable *, DevAxis> axis_at;
   std::map<const AxisTable *, int32_t> axis_wd_at;  // f64 weights (RGBA path) in heap_d
@@ -283,6 +304,16 @@ static void sync_streams(fi_ctx *c) {
   if (c->up_stream) (void)hipStreamSynchronize(c->up_stream);
   if (c->rb_stream) (void)hipStreamSynchronize(c->rb_stream);
   if (c->ap_stream) (void)hipStreamSynchronize(c->ap_stream);
+  if (c->gx_stream) (void)hipStreamSynchronize(c->gx_stream);
+}
+// Work about to run on c->stream that may read or write an earlier batch's
+// dst waits for the crop applies still running beside it on ap_stream.
+static int order_after_apply(fi_ctx *c) {
+  if (!c->ap_pending) return FI_OK;
+  if (hipStreamWaitEvent(c->stream, c->ap_tail, 0) != hipSuccess) return FI_EDEVICE;
+  c->ap_pending = false;
+  for (Slot &s : c->slots) s.ap_lo = s.ap_hi = 0;
+  return FI_OK;
 }
 static int ensure(fi_ctx *c, DevBuf *b, size_t bytes) {
   if (b->cap >= bytes) return FI_OK;
@@ -777,6 +808,11 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
             t.vqK0 = E.oi();
             E.ai.insert(E.ai.end(), P.vqK0.begin(), P.vqK0.end());
           }
+          if (!P.ftB.empty()) {
+            while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
+            t.ftB = E.oi();
+            E.ai.insert(E.ai.end(), P.ftB.begin(), P.ftB.end());
+          }
         }
         tp = c->sc_at.emplace(&P, t).first;
       }
@@ -904,6 +940,16 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
                    fd_lds(it.W, P.hm_pitch, P.aw, P.ah) <= kFdMaxLds
                ? 1
                : 0;
+    // k_sc_ft: the vertical tables (one 64-row window per chunk), the
+    // horizontal ones at <= 2 k-steps, 16-B aligned 3-channel rows readable to
+    // fd_rp(W) (the source's own alignment is checked at launch)
+    d.ft = d.vq && c->sc_ft && c->sc_fz && c->sc_fd && P.fx == 1 && P.fy == 1 && it.C == 3 && it.stride % 16 == 0 &&
+                   (it.padded || (it.W * 3) % 16 == 0) && P.hm_ks <= 2 && T.ftB >= 0 && P.ft_lds > 0 &&
+                   P.ft_lds <= kFtMaxLds
+               ? 1
+               : 0;
+    d.ftB = T.ftB;
+    d.ft_rows = P.ft_rows;
     d.vqA = T.vqA;
     d.vqC = T.vqC;
     d.vqK0 = T.vqK0;
@@ -912,6 +958,8 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     // workspace (offsets; converted to pointers after allocation)
     auto take = [&](size_t n) { return (uint8_t *)(uintptr_t)(E.work.take(n) + 1); };
     if (P.fx > 1 || P.fy > 1) d.red = take((size_t)P.rw * P.rh * 3);
+    // (k_sc_ft needs none, but a source that turns out unaligned at launch
+    // falls back to k_sc_hmfma + k_sc_vq when k_sc_fz cannot take it)
     if (P.thumb && P.need_h && !d.fz)  // generic kernels: pitch aw*3; k_sc_hmfma: pitch apitch
       d.hbuf = take((size_t)(prep ? (P.aw * 3 + 15) / 16 * 16 : P.aw * 3) * std::max(P.hrows, 1));
     if (P.thumb && (!prep || want_pre)) d.pre = take((size_t)P.aw * P.ah * 3);
@@ -965,6 +1013,8 @@ struct ScLaunches {
   int nhm = 0, hm_chunks = 0, hm_lds = 0, nvm = 0, v_chunks = 0, v_lds = 0;
   size_t fz_off = 0, fd_off = 0;  // k_sc_fz, k_sc_fd
   int nfz = 0, fz_lds = 0, nfd = 0, fd_lds = 0;
+  size_t ft_off = 0, ftt_off[2] = {0, 0};  // k_sc_ft: descriptors, tile lists per k-step count
+  int nft = 0, ft_tiles[2] = {0, 0}, ft_lds = 0;
   int nvq = 0, vq_chunks = 0, vq_lds = 0;
   size_t sl_off = 0, sg_off = 0;   // k_sc_score2 with maps in LDS / global
   int nsl = 0, nsg = 0, sl_px = 0;
@@ -975,13 +1025,18 @@ struct ScLaunches {
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> hm, sl, sg, vq, vm, fz, fd, s3;
+  std::vector<ScDesc> hm, sl, sg, vq, vm, fz, fd, s3, ft;
+  std::vector<int> ft_chunks;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
     const ScDesc &d = SL.descs[k];
     const ScPlan &P = *SL.plans[k];
     if (d.red) sred.push_back((int)k);
-    if (d.fz && d.fd && ((uintptr_t)d.img & 15) == 0) {
+    if (d.ft && ((uintptr_t)d.img & 15) == 0) {
+      ft.push_back(d);
+      ft_chunks.push_back(P.vq_chunks);
+      X->ft_lds = std::max(X->ft_lds, P.ft_lds);
+    } else if (d.fz && d.fd && ((uintptr_t)d.img & 15) == 0) {
       fd.push_back(d);
       X->fd_lds = std::max(X->fd_lds, fd_lds(d.W, d.hm_pitch, d.aw, d.ah));
     } else if (d.fz) {
@@ -1029,7 +1084,38 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->nfz = (int)fz.size();
   X->fd_off = B.addv(fd);
   X->nfd = (int)fd.size();
-  c->stats["sc_path_fd"].launches += X->nfd;  // images per smartcrop prescale kernel (fi_kernel_stats)
+  // k_sc_ft tiles (descriptor, chunk), one list per k-step count, XCD-aware:
+  // images round robin over the 8 XCDs, each XCD's tiles image by image, and
+  // workgroup g = 8 j + x takes XCD x's j-th tile (dispatch puts workgroup g on
+  // XCD g % 8), so an image's chunks run side by side in one L2
+  X->ft_off = B.addv(ft);
+  X->nft = (int)ft.size();
+  for (int ks = 1; ks <= 2; ks++) {
+    std::vector<int32_t> per[8];
+    int nimg = 0;
+    for (size_t k = 0; k < ft.size(); k++) {
+      if (ft[k].hm_ks != ks) continue;
+      std::vector<int32_t> &q = per[nimg++ % 8];
+      for (int ch = 0; ch < ft_chunks[k]; ch += kFtChunks) {
+        q.push_back((int32_t)k);
+        q.push_back(ch);
+      }
+    }
+    size_t len = 0;
+    for (auto &q : per) len = std::max(len, q.size() / 2);
+    std::vector<int32_t> tl;
+    tl.reserve(16 * len);
+    for (size_t j = 0; j < len; j++)
+      for (int x = 0; x < 8; x++) {
+        const bool have = 2 * j < per[x].size();
+        tl.push_back(have ? per[x][2 * j] : -1);
+        tl.push_back(have ? per[x][2 * j + 1] : 0);
+      }
+    X->ftt_off[ks - 1] = B.addv(tl);
+    X->ft_tiles[ks - 1] = (int)(tl.size() / 2);
+  }
+  c->stats["sc_path_ft"].launches += X->nft;  // images per smartcrop prescale kernel (fi_kernel_stats)
+  c->stats["sc_path_fd"].launches += X->nfd;
   c->stats["sc_path_fz"].launches += X->nfz;
   X->sl_off = B.addv(sl);
   X->nsl = (int)sl.size();
@@ -1050,7 +1136,7 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
   // on the stream that reads it, so batches queued before a parameter change
   // have read the old table first
   const uint16_t *skinsat = nullptr;
-  if (X.nfz > 0 || X.nfd > 0) {
+  if (X.nfz > 0 || X.nfd > 0 || X.nft > 0) {
     const std::string key(reinterpret_cast<const char *>(&PD), offsetof(ScParamsDev, pad));
     if (!c->skinsat.p || c->skinsat_key != key) {
       const int rc = ensure(c, &c->skinsat, (size_t)2 << 24);
@@ -1068,9 +1154,13 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
         launch_sc_vq(st, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0 ||
         launch_sc_v(st, (const ScDesc *)(ab + X.vm_off), X.nvm, X.v_chunks, X.v_lds, ai, PD) != 0 ||
         launch_sc_fz(st, (const ScDesc *)(ab + X.fz_off), X.nfz, X.fz_lds, ai, PD, skinsat) != 0 ||
-        launch_sc_fd(st, (const ScDesc *)(ab + X.fd_off), X.nfd, X.fd_lds, ai, PD, skinsat) != 0)
-      return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d/%d)", X.hm_lds, X.vq_lds, X.fz_lds,
-                     X.fd_lds);
+        launch_sc_fd(st, (const ScDesc *)(ab + X.fd_off), X.nfd, X.fd_lds, ai, PD, skinsat) != 0 ||
+        launch_sc_ft(st, 1, (const ScDesc *)(ab + X.ft_off), (const int32_t *)(ab + X.ftt_off[0]), X.ft_tiles[0],
+                     X.ft_lds, ai, PD, skinsat) != 0 ||
+        launch_sc_ft(st, 2, (const ScDesc *)(ab + X.ft_off), (const int32_t *)(ab + X.ftt_off[1]), X.ft_tiles[1],
+                     X.ft_lds, ai, PD, skinsat) != 0)
+      return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d/%d/%d)", X.hm_lds, X.vq_lds,
+                     X.fz_lds, X.fd_lds, X.ft_lds);
     if (X.hp.tiles)
       hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, st, desc(X.hp), pre(X.hp), X.hp.n, ai);
     if (X.vp.tiles)
@@ -2232,12 +2322,16 @@ static void pack_batch(fi_ctx *c, Exec &E, BatchPlan &Bp, Packed &K) {
   K.ad_off = B.addv(E.ad);
 }
 
-// Enqueue the batch: resample, convolutions and -monochrome on the main
-// stream; the smartcrop stage and crop apply on sc_stream behind this batch's
-// resample (so they overlap the next batch's upload and resample).
+// Enqueue the batch: resample, convolutions, -monochrome and the smartcrop
+// stage on the main stream (sc_stream is the same stream); the crop apply on
+// ap_stream behind this batch's smartcrop stage, so it runs beside the next
+// batch's resample (FI_APPLY_OVERLAP=0: on the main stream).  ap_tail marks
+// the last apply for the entry points that must not run before it
+// (order_after_apply).
 static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Packed &K, uint8_t *ab, uint8_t *wb,
                         Slot &S) {
   S.tail = c->sc_stream;
+  S.ap_lo = S.ap_hi = 0;
   const int32_t *ai = (const int32_t *)c->heap_i.p;
   const float *af = (const float *)c->heap_f.p;
   const double *ad = (const double *)c->heap_d.p;
@@ -2326,10 +2420,25 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
         as = c->ap_stream;
         pw = c->n_cu;
         S.tail = as;
+        tb.sb = as;  // the batch range ends with its apply
       }
-      Timer t(c, "crop_apply", 0, as, as);
-      (void)launch_crop_apply(as, (const ApplyDesc *)(ab + K.apply_off), (int)Bp.apply.size(),
-                              (const DevCrop *)(ab + K.SX.crops_off), (const ScResult *)(wb + Bp.results_off), pw);
+      {
+        Timer t(c, "crop_apply", 0, as, as);
+        (void)launch_crop_apply(as, (const ApplyDesc *)(ab + K.apply_off), (int)Bp.apply.size(),
+                                (const DevCrop *)(ab + K.SX.crops_off), (const ScResult *)(wb + Bp.results_off), pw);
+      }
+      if (as == c->ap_stream) {
+        if (!c->ap_tail) HIP_TRY(hipEventCreateWithFlags(&c->ap_tail, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->ap_tail, as));
+        c->ap_pending = true;
+        // the bytes this apply writes (a crop is at most the resized image)
+        S.ap_lo = UINTPTR_MAX;
+        S.ap_hi = 0;
+        for (const ApplyDesc &a : Bp.apply) {
+          S.ap_lo = std::min(S.ap_lo, (uintptr_t)a.dst);
+          S.ap_hi = std::max(S.ap_hi, (uintptr_t)a.dst + (uintptr_t)a.W * a.H * a.C);
+        }
+      }
     }
     HIP_TRY(hipGetLastError());
   }
@@ -2471,6 +2580,20 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async, std::shar
   host_stat(c, "host_plan_blob", t_planned - t_tiles);
   if (c->timing) c->stats["host_plan"].bytes += (double)B.b.size();
   uint8_t *ab = (uint8_t *)S.arena.p;
+  // a source that an earlier batch's overlapped crop apply is still writing
+  // (a chained request: this batch resizes that batch's output): the resample
+  // waits for the applies (bounding ranges: a false hit only costs the overlap)
+  for (const Slot &o : c->slots) {
+    if (&o == &S || o.ap_hi <= o.ap_lo) continue;
+    bool hit = false;
+    for (int i = 0; i < n && !hit; i++) {
+      const fi_image &im = imgs[i];
+      if (!im.src || im.src_h <= 0 || im.src_stride <= 0) continue;
+      const uintptr_t s0 = (uintptr_t)im.src, s1 = s0 + (uintptr_t)im.src_stride * (uintptr_t)im.src_h;
+      hit = s0 < o.ap_hi && o.ap_lo < s1;
+    }
+    if (hit && order_after_apply(c) != FI_OK) return set_err(FI_EDEVICE, "hipStreamWaitEvent failed");
+  }
   rc = heap_commit(c, E, ab, K.ai_off, K.af_off, K.ad_off);
   if (rc) return rc;
   rc = launch_batch(c, E, Bp, K, ab, wb, S);
@@ -2490,6 +2613,8 @@ static int finalize_front(fi_ctx *c) {
   const double t_wait = now_ms();
   HIP_TRY(hipEventSynchronize(S.done));
   S.busy = false;
+  S.ap_lo = S.ap_hi = 0;  // its apply is done (S.done follows it on the tail stream)
+  if (c->inflight.empty()) c->ap_pending = false;
   collect_ranges(c, pb.timers);
   const double t_done = now_ms();
   host_stat(c, "host_wait", t_done - t_wait);
@@ -2807,6 +2932,7 @@ int fi_jpeg_decode_device(fi_ctx *c, const uint8_t *const *data, const size_t *l
   if (n == 0) return FI_OK;
   HIP_TRY(hipSetDevice(c->device));
   std::lock_guard<std::mutex> lk(c->mu);
+  if (order_after_apply(c) != FI_OK) return set_err(FI_EDEVICE, "hipStreamWaitEvent failed");
   std::string err;
   const int rc = jpeg_decode_batch(c->stream, data, len, n, dst, dst_stride, out_channels, status, jpeg_alloc, c, &err);
   if (rc) return set_err(rc, "%s", err.c_str());
@@ -3008,6 +3134,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_VR_PBUF")) c->vr_pbuf = atoi(e);
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';
+  if (const char *e = getenv("FI_SC_FT")) c->sc_ft = e[0] == '1';
   if (const char *e = getenv("FI_SC_MFMA")) c->sc_mf = e[0] == '1';
   if (const char *e = getenv("FI_VR_MAX_CLASSES")) c->vr_max_classes = atoi(e);
   if (const char *e = getenv("FI_VM_LPT")) c->vm_lpt = e[0] == '1';
@@ -3024,7 +3151,8 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_APPLY_OVERLAP")) c->apply_overlap = e[0] == '1';
   if (hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->ap_stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->ap_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->gx_stream, hipStreamNonBlocking) != hipSuccess) {
     fi_destroy(c);
     return set_err(FI_EDEVICE, "hipStreamCreate failed");
   }
@@ -3051,6 +3179,7 @@ void fi_destroy(fi_ctx *c) {
     if (sl.rs_done) (void)hipEventDestroy(sl.rs_done);
     if (sl.up_done) (void)hipEventDestroy(sl.up_done);
     if (sl.sc_end) (void)hipEventDestroy(sl.sc_end);
+    if (sl.sc_done) (void)hipEventDestroy(sl.sc_done);
     for (DevBuf *b : {&sl.arena, &sl.work, &sl.hio})
       if (b->p) (void)hipFree(b->p);
   }
@@ -3060,6 +3189,10 @@ void fi_destroy(fi_ctx *c) {
   if (c->up_stream) (void)hipStreamDestroy(c->up_stream);
   if (c->rb_stream) (void)hipStreamDestroy(c->rb_stream);
   if (c->ap_stream) (void)hipStreamDestroy(c->ap_stream);
+  if (c->gx_stream) (void)hipStreamDestroy(c->gx_stream);
+  if (c->ap_tail) (void)hipEventDestroy(c->ap_tail);
+  if (c->gx_done) (void)hipEventDestroy(c->gx_done);
+  if (c->gx_pin) (void)hipHostFree(c->gx_pin);
   delete c;
 }
 
@@ -3087,6 +3220,8 @@ int fi_pixelate_regions_device(fi_ctx *c, uint8_t *img, int32_t w, int32_t h, in
   if (!c) return set_err(FI_EINVAL, "bad arguments");
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device));
+  // stream-ordered after earlier batches, including their crop applies on ap_stream
+  if (order_after_apply(c) != FI_OK) return set_err(FI_EDEVICE, "hipStreamWaitEvent failed");
   return pixelate_device(c, img, w, h, stride, channels, boxes, nboxes);
 }
 
@@ -3442,7 +3577,9 @@ int fi_memcpy_d2h(fi_ctx *c, void *dst, const void *src, uint64_t bytes) {
 }
 int fi_fill_synthetic(fi_ctx *c, uint8_t *dev, int32_t w, int32_t h, int32_t stride, uint32_t seed) {
   if (!c || !dev || w <= 0 || h <= 0 || stride < 3 * w) return set_err(FI_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device));
+  if (order_after_apply(c) != FI_OK) return set_err(FI_EDEVICE, "hipStreamWaitEvent failed");
   const int64_t n = (int64_t)w * h;
   hipLaunchKernelGGL(k_synth, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, dev, w, h, (int64_t)stride,
                      seed);
@@ -3492,33 +3629,117 @@ int fi_rccl_init(fi_ctx *c, int32_t rank, int32_t world, const uint8_t id[128]) 
   c->world = world;
   return FI_OK;
 }
-int fi_rccl_gather_records(fi_ctx *c, const fi_record *send, int32_t count, fi_record *recv) {
-  if (!c || !c->comm || count < 0) return set_err(FI_EINVAL, "RCCL not initialised");
-  std::lock_guard<std::mutex> g(c->mu);
-  HIP_TRY(hipSetDevice(c->device));
-  const size_t bytes = sizeof(fi_record) * (size_t)count;
-  const size_t total = bytes * (1 + (c->rank == 0 ? c->world : 0));
-  int rc = ensure(c, &c->gather, total + 256);  // its own buffer: in-flight batches never read it
+// The record gather runs on gx_stream, a stream of its own: the records are on
+// the host once fi_wait has filled them, so nothing orders the gather after
+// the batch streams, and a gather started while the next batch runs returns
+// at once (fi_rccl_gather_start); fi_rccl_gather_finish waits for it.  Send
+// and receive go through the context's pinned staging, so the caller's
+// buffers are plain host memory.
+static int gather_finish(fi_ctx *c) {
+  if (!c->gx_pending) return FI_OK;
+  c->gx_pending = false;
+  HIP_TRY(hipEventSynchronize(c->gx_done));
+  if (c->gx_recv && c->gx_recv_bytes)
+    memcpy(c->gx_recv, (const uint8_t *)c->gx_pin + c->gx_pin_cap / 2, c->gx_recv_bytes);
+  c->gx_recv = nullptr;
+  c->gx_recv_bytes = 0;
+  return FI_OK;
+}
+static int gather_start(fi_ctx *c, const fi_record *send, int32_t count, fi_record *recv) {
+  int rc = gather_finish(c);  // one gather in flight: its staging is reused
   if (rc) return rc;
-  uint8_t *sb = (uint8_t *)c->gather.p, *rb = sb + bytes;
-  HIP_TRY(hipMemcpyAsync(sb, send, bytes, hipMemcpyHostToDevice, c->stream));
-  if (c->rank == 0) HIP_TRY(hipMemcpyAsync(rb, sb, bytes, hipMemcpyDeviceToDevice, c->stream));
+  const size_t bytes = sizeof(fi_record) * (size_t)count;
+  const size_t rbytes = c->rank == 0 ? bytes * (size_t)c->world : 0;
+  const size_t total = bytes * (1 + (c->rank == 0 ? c->world : 0));
+  if (c->gather.cap < total + 256) {  // its own buffer: batches never read it (no stream drain to grow it)
+    if (c->gx_stream) HIP_TRY(hipStreamSynchronize(c->gx_stream));
+    if (c->gather.p) HIP_TRY(hipFree(c->gather.p));
+    c->gather.p = nullptr;
+    c->gather.cap = 0;
+    const size_t cap = std::max(total + total / 4 + 256, (size_t)1 << 16);
+    if (hipMalloc(&c->gather.p, cap) != hipSuccess) {
+      c->gather.p = nullptr;
+      return set_err(FI_ENOMEM, "hipMalloc(%zu) for the record gather failed", cap);
+    }
+    c->gather.cap = cap;
+  }
+  // pinned staging: send in the first half, receive in the second
+  const size_t half = std::max(bytes, rbytes);
+  if (c->gx_pin_cap < 2 * half + 64) {
+    if (c->gx_pin) HIP_TRY(hipHostFree(c->gx_pin));
+    c->gx_pin = nullptr;
+    c->gx_pin_cap = 0;
+    const size_t cap = 2 * std::max(half + half / 4, (size_t)4096);
+    if (hipHostMalloc(&c->gx_pin, cap, hipHostMallocDefault) != hipSuccess) {
+      c->gx_pin = nullptr;
+      return set_err(FI_ENOMEM, "hipHostMalloc(%zu) for the record gather failed", cap);
+    }
+    c->gx_pin_cap = cap;
+  }
+  if (!c->gx_done) HIP_TRY(hipEventCreateWithFlags(&c->gx_done, hipEventDisableTiming));
+  uint8_t *pin_s = (uint8_t *)c->gx_pin, *pin_r = pin_s + c->gx_pin_cap / 2;
+  hipStream_t st = c->gx_stream;
+  uint8_t *sb = (uint8_t *)c->gather.p, *rb = sb + bytes;  // device: send, then world x count receive
+  if (c->rank == 0) {
+    if (bytes) memcpy(pin_r, send, bytes);  // rank 0's own records: no device round trip
+  } else if (bytes) {
+    memcpy(pin_s, send, bytes);
+    HIP_TRY(hipMemcpyAsync(sb, pin_s, bytes, hipMemcpyHostToDevice, st));
+  }
   // nothing between ncclGroupStart and ncclGroupEnd may return early: the
   // group is always closed, then the first error is reported
   ncclResult_t r = ncclGroupStart();
   if (r != ncclSuccess) return set_err(FI_EDEVICE, "ncclGroupStart: %s", ncclGetErrorString(r));
   if (c->rank == 0) {
     for (int p = 1; p < c->world && r == ncclSuccess; p++)
-      r = ncclRecv(rb + bytes * p, bytes, ncclUint8, p, c->comm, c->stream);
+      r = ncclRecv(rb + bytes * p, bytes, ncclUint8, p, c->comm, st);
   } else {
-    r = ncclSend(sb, bytes, ncclUint8, 0, c->comm, c->stream);
+    r = ncclSend(sb, bytes, ncclUint8, 0, c->comm, st);
   }
   const ncclResult_t re = ncclGroupEnd();
   if (r != ncclSuccess || re != ncclSuccess)
     return set_err(FI_EDEVICE, "RCCL gather: %s", ncclGetErrorString(r != ncclSuccess ? r : re));
-  if (c->rank == 0 && recv)
-    HIP_TRY(hipMemcpyAsync(recv, rb, bytes * c->world, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->rank == 0 && recv && rbytes > bytes)
+    HIP_TRY(hipMemcpyAsync(pin_r + bytes, rb + bytes, rbytes - bytes, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipEventRecord(c->gx_done, st));
+  c->gx_pending = true;
+  c->gx_recv = c->rank == 0 ? recv : nullptr;
+  c->gx_recv_bytes = c->rank == 0 && recv ? rbytes : 0;
+  return FI_OK;
+}
+int fi_rccl_gather_start(fi_ctx *c, const fi_record *send, int32_t count, fi_record *recv) {
+  if (!c || !c->comm || count < 0 || (count > 0 && !send)) return set_err(FI_EINVAL, "RCCL not initialised");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  return gather_start(c, send, count, recv);
+}
+int fi_rccl_gather_finish(fi_ctx *c) {
+  if (!c) return set_err(FI_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  return gather_finish(c);
+}
+int fi_rccl_gather_records(fi_ctx *c, const fi_record *send, int32_t count, fi_record *recv) {
+  if (!c || !c->comm || count < 0 || (count > 0 && !send)) return set_err(FI_EINVAL, "RCCL not initialised");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  const int rc = gather_start(c, send, count, recv);
+  return rc ? rc : gather_finish(c);
+}
+int fi_query(fi_ctx *c, int32_t *running) {
+  if (!c || !running) return set_err(FI_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  int n = 0;
+  for (const PendingBatch &pb : c->inflight) {
+    const hipError_t e = hipEventQuery(c->slots[pb.slot].done);
+    if (e == hipErrorNotReady) {
+      n++;
+    } else if (e != hipSuccess) {
+      return set_err(FI_EDEVICE, "hipEventQuery: %s", hipGetErrorString(e));
+    }
+  }
+  *running = n;
   return FI_OK;
 }
 

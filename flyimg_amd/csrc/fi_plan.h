@@ -212,6 +212,14 @@ struct ScPlan {
   // 16-row MFMA block), its H-stage window starts at vqK0[chunk] (<= 64 rows)
   bool vq_ok = false;
   int vq_chunks = 0, vq_lds = 0;
+  // k_sc_ft (chunk tiles): the horizontal B fragments in the kernel's
+  // coalesced source order -- lane group g of a fragment row loads the 16-B
+  // chunks g, g + 4, g + 8 of the 192-byte window, so its bytes are an RGB
+  // stream whose channel phase is rotated by g: [nb][ks][3 ch][3 limbs] x 256
+  // int32 (fi_plan.cpp sc_ft_tables); ft_rows = the H-stage rows the widest
+  // tile of kFtChunks chunks needs (16-row blocks), ft_lds its LDS
+  std::vector<int32_t> ftB;
+  int ft_rows = 0, ft_lds = 0;
   bool fz_ok = false;  // k_sc_fz (fused per-image prescale + maps)
   int fz_lds = 0;
   std::vector<int32_t> vqA;   // [chunk][3 limbs] fragments of 64 lanes x 16 B (256 int32)

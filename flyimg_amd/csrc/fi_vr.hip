@@ -63,9 +63,11 @@ typedef __attribute__((address_space(3))) uint8_t l_u8;
 constexpr int kVW = 8;                   // V waves: 64 source bytes (4 column tiles) each
 constexpr int kSW = 1;                   // S wave: the stores of the output tile of phase p - 2
 // the other 7 waves: NL loader waves (the last ones) and 7 - NL H waves, whose
-// items are hw and hw + (7 - NL); the host picks NL per launch (VrLayout::nl):
-// 4 when every strip has <= 2 16-px output blocks (<= 6 items) and every
-// image's touched rows are evenly spaced, else 2
+// items are hw and hw + (7 - NL); the host picks NL per launch (VrLayout::nl,
+// fi_api.cpp build_vr_tiles): 4 when every strip of the launch has one 16-px
+// output block (3 items; FI_VR_NL=4 forces it where every strip has <= 2),
+// else 2 -- evenly or unevenly spaced touched rows alike (the row list's
+// 8-row pair classes serve 4 loaders, vr_pair_off)
 constexpr int kABytes = 4096;            // [t][limb][64 lanes][16 B]: two limbs, <= 2 k-steps
 constexpr int kRecBytes = 32;
 constexpr int kLutSlots = 4;

@@ -169,11 +169,22 @@ class RecordGather:
 
     def gather(self, records):
         """records: list of 8-int tuples (fi_record).  Rank 0 gets all ranks'."""
-        if self.backend == "local":
-            return list(records)
-        if self.backend == "rccl":
-            import ctypes
+        self.start(records)
+        return self.finish()
 
+    # Non-blocking form (bench.py's batch loop): start() enqueues the gather
+    # on the library's gather stream and returns; finish() waits for it and
+    # returns rank 0's records.  One gather in flight: a start() with one
+    # pending finishes it first (whose records are then dropped).
+    _pending = None
+
+    def start(self, records):
+        if self._pending is not None:
+            self.finish()
+        if self.backend == "local":
+            self._pending = ("local", list(records))
+            return
+        if self.backend == "rccl":
             from . import _lib as L
 
             n = len(records)
@@ -181,9 +192,26 @@ class RecordGather:
             for i, r in enumerate(records):
                 send[i] = L.FiRecord(*r)
             recv = (L.FiRecord * max(n * self.comm.world, 1))() if self.comm.rank == 0 else None
-            L.check(L.lib().fi_rccl_gather_records(self.ctx.h, send, n, recv))
+            L.check(L.lib().fi_rccl_gather_start(self.ctx.h, send, n, recv))
+            self._pending = ("rccl", (n, recv))
+            return
+        self._pending = ("comm", [list(r) for r in records])
+
+    def finish(self):
+        if self._pending is None:
+            return None
+        kind, data = self._pending
+        self._pending = None
+        if kind == "local":
+            return data
+        if kind == "rccl":
+            from . import _lib as L
+
+            L.check(L.lib().fi_rccl_gather_finish(self.ctx.h))
+            n, recv = data
             if self.comm.rank != 0:
                 return None
             return [tuple(getattr(recv[i], f) for f, _ in L.FiRecord._fields_) for i in range(n * self.comm.world)]
-        allr = self.comm.allgather_obj([list(r) for r in records])
+        # the control-plane gather is a rendezvous: it runs at finish()
+        allr = self.comm.allgather_obj(data)
         return [tuple(r) for part in allr for r in part] if self.comm.rank == 0 else None

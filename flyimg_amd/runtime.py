@@ -350,6 +350,13 @@ class Context:
         ``keep`` remain in flight, filling their records."""
         return self._lib.fi_wait(self.h, keep)
 
+    def query(self) -> int:
+        """fi_query: how many submitted batches are still running on the GPU
+        (does not block)."""
+        n = ctypes.c_int32()
+        L.check(self._lib.fi_query(self.h, ctypes.byref(n)))
+        return n.value
+
     # ---- timing ----------------------------------------------------------------
     def set_timing(self, on):
         """True / 1: every stage timed; 2: the resample stage only; False / 0: off."""

@@ -206,15 +206,23 @@ int fi_process_batch_device(fi_ctx *ctx, fi_image *imgs, int32_t n);
  * uploads and launches the batch, then returns; `imgs` must stay valid until
  * fi_wait().  Batch k+1 is planned and uploaded on the host while batch k runs
  * on the GPU (two pinned staging slots; a third submit waits for the oldest
- * batch).  Every kernel of both batches runs on the context's one stream, in
- * submission order (the resample fills every CU, so a second stream only
- * stretched both stages); the dst buffers of two in-flight batches must not
- * overlap (sources may be shared).
+ * batch).  Streams: the resample, smartcrop and -monochrome / convolution
+ * kernels of every batch run on the context's main stream in submission
+ * order; the FI_OP_SMARTCROP_APPLY crop of batch k runs on a second stream
+ * beside batch k+1's resample (one small workgroup per CU), and batch k's
+ * records and outputs are final once that apply is done (fi_wait covers it).
+ * Ordering across the two streams is kept for the caller: a later batch whose
+ * sources overlap an earlier batch's dst, and the device-ordered entry points
+ * (fi_pixelate_regions_device, fi_jpeg_decode_device, fi_fill_synthetic) wait
+ * for the applies still running.  The dst buffers of two in-flight batches
+ * must not overlap (sources may be shared).
  * fi_wait(ctx, keep) finalizes submitted batches in order -- fills their
  * result fields -- until at most `keep` remain in flight (0 = drain all) and
- * returns the first error. */
+ * returns the first error.  fi_query(ctx, &running) returns, without
+ * blocking, how many submitted batches are still running on the GPU. */
 int fi_submit_batch_device(fi_ctx *ctx, fi_image *imgs, int32_t n);
 int fi_wait(fi_ctx *ctx, int32_t keep);
+int fi_query(fi_ctx *ctx, int32_t *running);
 
 /* smartcrop.py SmartCrop().crop(rgb, target_w, target_h) on host RGB8.
  * out_xywh = top_crop x, y, width, height; *out_score = its total. */
@@ -264,7 +272,15 @@ typedef struct fi_record {
 int fi_rccl_get_unique_id(uint8_t id[128]);
 int fi_rccl_init(fi_ctx *ctx, int32_t rank, int32_t world, const uint8_t id[128]);
 /* Every rank sends `count` records (same count on every rank); rank 0
- * receives world*count records in rank order. */
+ * receives world*count records in rank order.  The gather runs on a stream
+ * of its own (no dependency on the batch streams: the records are host data
+ * once fi_wait has filled them).  fi_rccl_gather_start enqueues it and
+ * returns (send is copied before it returns; recv is written by the matching
+ * fi_rccl_gather_finish, which waits); one gather is in flight at a time (a
+ * second start finishes the first).  fi_rccl_gather_records = start +
+ * finish.  Every rank issues the same sequence of gathers. */
+int fi_rccl_gather_start(fi_ctx *ctx, const fi_record *send, int32_t count, fi_record *recv);
+int fi_rccl_gather_finish(fi_ctx *ctx);
 int fi_rccl_gather_records(fi_ctx *ctx, const fi_record *send, int32_t count, fi_record *recv);
 
 /* Test hook (not a reference interface): the -monochrome kernels on a

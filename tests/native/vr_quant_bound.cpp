@@ -28,6 +28,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <map>
@@ -58,6 +59,10 @@ static int64_t limb2(const std::vector<int32_t> &f, size_t base, int l, int j) {
 
 static double g_worst = 0;  // over every table checked
 static int g_tables = 0;
+static long g_cmp_taps = 0;  // weights compared with the oracle's
+static int g_cmp_tables = 0;
+extern "C" int or_im_axis_taps(int W, int H, int ow, int oh, int thumbnail, int matte, int axis, int o, int *start,
+                               double *w, int cap);
 
 // returns false when the geometry does not take k_rs_vr
 static bool check(int W, int H, int tw, int th, uint32_t flags, const char *name, bool verbose) {
@@ -74,6 +79,30 @@ static bool check(int W, int H, int tw, int th, uint32_t flags, const char *name
   AxisTable v, h;
   build_axis(P.filter, P.yf, P.sh, P.th, P.ey0, P.ey0 + P.eh, P.sample, P.H, &v);
   build_axis(P.filter, P.xf, P.sw, P.tw, P.ex0, P.ex0 + P.ew, P.sample, P.W, &h);
+  // the f64 weights bounded below ARE the oracle's: every output's taps (first
+  // source index, count, each weight bit for bit) equal or_im_axis_taps, the
+  // oracle's resample on the same geometry
+  {
+    const int thumb = (flags & FI_OP_THUMBNAIL) ? 1 : 0;
+    std::vector<double> ow(8192);
+    for (int axis = 0; axis < 2; axis++) {
+      const AxisTable &t = axis ? v : h;
+      const int o0 = axis ? P.ey0 : P.ex0, o1 = o0 + (axis ? P.eh : P.ew);
+      for (int o = o0; o < o1; o++) {
+        const size_t k = (size_t)(o - o0);
+        int s = -1;
+        const int n = or_im_axis_taps(W, H, P.tw, P.th, thumb, 0, axis, o, &s, ow.data(), (int)ow.size());
+        CHECK(n == t.count[k] && s == t.start[k], "%s: axis %d out %d: oracle %d taps at %d, planner %d at %d", name,
+              axis, o, n, s, t.count[k], t.start[k]);
+        if (n != t.count[k]) continue;
+        int same = 0;
+        for (int j = 0; j < n; j++) same += memcmp(&ow[j], &t.wd[t.woff[k] + j], sizeof(double)) == 0;
+        CHECK(same == n, "%s: axis %d out %d: %d of %d weights differ from the oracle's", name, axis, o, n - same, n);
+        g_cmp_taps += n;
+      }
+    }
+    g_cmp_tables++;
+  }
   VrV m;
   MfmaH mh;
   if (!build_vr_v(v, &m) || !build_mfma_h(h, &mh) || mh.shift2 == 0) return false;
@@ -213,6 +242,9 @@ int main() {
   }
   printf("  %d of 200 random geometries on k_rs_vr\n", taken);
   CHECK(taken >= 100, "only %d random geometries took k_rs_vr", taken);
+  printf("planner tap tables == oracle's: %ld weights of %d geometries compared bit for bit\n", g_cmp_taps,
+         g_cmp_tables);
+  CHECK(g_cmp_tables >= 100 && g_cmp_taps > 0, "too few geometries compared with the oracle");
   printf("worst bound %.4f LSB over %d tables\n", g_worst, g_tables);
   printf("%s (%d failures)\n", g_fail ? "FAILED" : "OK", g_fail);
   return g_fail ? 1 : 0;

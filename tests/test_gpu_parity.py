@@ -44,11 +44,11 @@ def _context_with(env):
                 os.environ[k] = v
 
 
-_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_SC_FD": "1"}
+_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_SC_FD": "1", "FI_SC_FT": "1"}
 PATHS = {
     # default kernels: k_rs_vr (block-major persistent MFMA resample; k_rs_vm
-    # where its tables do not fit) / k_rs_hv; k_sc_fd fused prescale + maps
-    # (source rows by LDS-DMA); k_sc_score3 (exact-integer MFMA score fast pass)
+    # where its tables do not fit) / k_rs_hv; k_sc_ft chunk-tiled prescale +
+    # maps; k_sc_score3 (exact-integer MFMA score fast pass)
     "vr": dict(_ENV),
     # the same with k_sc_fz (register-staged source rows, two workgroups per CU)
     "fz": dict(_ENV, FI_SC_FD="0"),
@@ -71,7 +71,9 @@ def rctx(request):
 
 EXPECTED_PATH = {"vr": "path_vr", "fz": "path_vr", "vm": "path_vm", "generic": "path_generic_v"}
 # smartcrop prescale kernel of each path (images counted by fi_kernel_stats)
-EXPECTED_SC = {"vr": "sc_path_fd", "fz": "sc_path_fz", "vm": None, "generic": None}
+EXPECTED_SC = {"vr": "sc_path_ft", "fd": "sc_path_fd", "fz": "sc_path_fz", "vm": None, "generic": None}
+# the smartcrop tests also run k_sc_fd (per-image streamed prescale, FI_SC_FT=0)
+SC_PATHS = dict(PATHS, fd=dict(_ENV, FI_SC_FT="0"))
 
 
 @pytest.mark.parametrize("W,H,opts,even_rows", [
@@ -95,9 +97,9 @@ def test_baseline_geometries_take_the_path(rctx, W, H, opts, even_rows):
     assert rctx.stats(want)[1] == before + 1, (want, {k: rctx.stats(k)[1] for k in EXPECTED_PATH.values()})
 
 
-@pytest.fixture(scope="module", params=sorted(PATHS))
+@pytest.fixture(scope="module", params=sorted(SC_PATHS))
 def sctx(request):
-    c = _context_with(PATHS[request.param])
+    c = _context_with(SC_PATHS[request.param])
     c.path_name = request.param
     yield c
     c.close()
@@ -176,15 +178,55 @@ def test_smartcrop_fast_bounds_contain_exact(sctx, case):
             assert abs(c.total - exact) <= 1e-9 * max(1.0, abs(exact)), (c.total, exact)
 
 
+@pytest.fixture(scope="module")
+def s2ctx():
+    """the score's f64 VALU fast pass (k_sc_score2) forced"""
+    c = _context_with(dict(_ENV, FI_SC_MFMA="0"))
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("w,h", [(500, 281), (450, 300), (600, 338)])
+def test_score3_runs_and_agrees_with_score2(ctx, s2ctx, w, h):
+    """k_sc_score3 (exact-integer MFMA fast pass) is the kernel that
+    ran on these geometries (sc_score_mfma counts its images; no silent
+    k_sc_score2 fallback), every crop's fast total lies within 1e-9 of the
+    oracle's exact one (its rigorous bound is far tighter), and the top crop
+    and its score equal k_sc_score2's (FI_SC_MFMA=0) and the oracle's."""
+    src = synth_rgb(w, h, 0xB0 + w)
+    m0, v0 = ctx.stats("sc_score_mfma")[1], ctx.stats("sc_score_valu")[1]
+    r3 = ctx.smartcrop_ex(src, 100, 100, options=_opts(False))
+    assert ctx.stats("sc_score_mfma")[1] == m0 + 1 and ctx.stats("sc_score_valu")[1] == v0
+    n0 = s2ctx.stats("sc_score_valu")[1]
+    r2 = s2ctx.smartcrop_ex(src, 100, 100, options=_opts(False))
+    assert s2ctx.stats("sc_score_valu")[1] == n0 + 1
+    ref = orc.sc_crop(src, 100, 100)
+    assert r3["top_index"] == r2["top_index"] == ref["top_index"]
+    t3, t2 = r3["crops"][r3["top_index"]], r2["crops"][r2["top_index"]]
+    exact_top = ref["top_crop"]["score"]["total"]
+    for t in (t3, t2):
+        if t.exact:
+            assert t.total.hex() == exact_top.hex()
+        else:
+            assert abs(t.total - exact_top) <= 1e-9 * max(1.0, abs(exact_top))
+    for c, g in zip(r3["crops"], ref["crops"]):
+        e = g["score"]["total"]
+        if c.exact:
+            assert c.total.hex() == e.hex()
+        else:
+            assert abs(c.total - e) <= 1e-9 * max(1.0, abs(e)), (c.total, e)
+
+
 @pytest.mark.parametrize("w,h", [(500, 281), (333, 500), (450, 300), (301, 201)])
 def test_smartcrop_prescale_kernel_of_path(sctx, w, h):
     """fi_smartcrop runs its prescale + maps on the kernel the path names
-    (k_sc_fd on the default path for 3-channel images at the staged 16-B
-    rounded pitch, k_sc_fz with FI_SC_FD=0; no silent fallback), and the
-    result is the oracle's: every crop's scores bit-exact (exact_all).  The
-    sizes prescale by 1.8-3 (a 14-row chunk's window within 64 H-stage rows)."""
+    (k_sc_ft on the default path for 3-channel images at the staged 16-B
+    rounded pitch, k_sc_fd with FI_SC_FT=0, k_sc_fz with FI_SC_FD=0; no
+    silent fallback), and the result is the oracle's: every crop's scores
+    bit-exact (exact_all).  The sizes prescale by 1.8-3 (a 14-row chunk's
+    window within 64 H-stage rows)."""
     src = synth_rgb(w, h, 0x5C + w)
-    names = ("sc_path_fd", "sc_path_fz")
+    names = ("sc_path_ft", "sc_path_fd", "sc_path_fz")
     before = {k: sctx.stats(k)[1] for k in names}
     r = sctx.smartcrop_ex(src, 100, 100, options=_opts(True), want_images=True)
     ran = {k: sctx.stats(k)[1] - before[k] for k in names}
@@ -512,15 +554,24 @@ def test_cfg4_slice_one_batch(ctx):
     assert len(exact) == len(picks) >= 55 and min(exact) >= 0.98
 
 
-def test_pipelined_submit_matches_synchronous(ctx):
+@pytest.fixture(scope="module", params=["1", "0"], ids=["apply_overlap", "apply_serial"])
+def octx(request):
+    """FI_APPLY_OVERLAP=1 (default: the crop apply beside the next batch's
+    resample, k_crop_apply3p) and =0 (on the batch stream, k_crop_apply3)."""
+    c = _context_with({"FI_APPLY_OVERLAP": request.param})
+    yield c
+    c.close()
+
+
+def test_pipelined_submit_matches_synchronous(octx):
     """fi_submit_batch_device x3 + fi_wait (two pinned slots, a third submit
     waits for the oldest) gives the same pixels and records as the
-    synchronous fi_process_batch_device, batch by batch."""
-    import ctypes
-
+    synchronous fi_process_batch_device, batch by batch -- with the crop apply
+    overlapped and serial."""
     from flyimg_amd.processor import ImageProcessor, OptionsBag
     from flyimg_amd.runtime import plan as fi_plan
 
+    ctx = octx
     W, H, n = 960, 540, 6
     op = ImageProcessor(OptionsBag("w_300,smc_1"), W, H).to_op()
     stride = W * 3

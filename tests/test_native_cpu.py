@@ -32,7 +32,10 @@ def test_vr_two_limb_quantisation_bound():
     fragment bytes, its integer algebra re-derived (row sums 2^shift, the
     constant 128 * 2^shift bias, the Q16 hi/lo split), and the worst case over
     all 8-bit inputs of |kernel - ImageMagick f64| bounded per output: < 1 LSB
-    (tests/native/vr_quant_bound.cpp)."""
+    (tests/native/vr_quant_bound.cpp).  The f64 weights the bound is taken
+    against are checked first to be the oracle's own (or_im_axis_taps, bit for
+    bit on every output of every geometry), so the bound chains to the
+    oracle and not only to the planner's restatement."""
     import re
 
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
@@ -40,14 +43,22 @@ def test_vr_two_limb_quantisation_bound():
         pytest.skip("hipcc not available")
     with tempfile.TemporaryDirectory() as d:
         exe = os.path.join(d, "vqb")
+        # the oracle's tap restatement (or_im_axis_taps), with the oracle's own flags
+        obj = os.path.join(d, "fi_oracle.o")
+        subprocess.run(["gcc", "-O2", "-std=c99", "-D_GNU_SOURCE", "-ffp-contract=off", "-fno-fast-math", "-c",
+                        os.path.join(ROOT, "oracle/fi_oracle.c"), "-o", obj], check=True, capture_output=True,
+                       timeout=300)
         subprocess.run([hipcc, "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"),
                         os.path.join(ROOT, "tests/native/vr_quant_bound.cpp"),
-                        os.path.join(ROOT, "flyimg_amd/csrc/fi_plan.cpp"), "-o", exe],
+                        os.path.join(ROOT, "flyimg_amd/csrc/fi_plan.cpp"), "-Xlinker", obj, "-o", exe, "-lm"],
                        check=True, capture_output=True, timeout=300)
         r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK (0 failures)" in r.stdout
     worst = float(re.search(r"worst bound ([0-9.]+) LSB", r.stdout).group(1))
+    # the bound is against the oracle's weights: the planner's tables equal them bit for bit
+    m = re.search(r"planner tap tables == oracle's: (\d+) weights of (\d+) geometries", r.stdout)
+    assert m and int(m.group(1)) > 100000 and int(m.group(2)) >= 100, r.stdout
     assert worst < 1.0
     for cfg in ("cfg1", "cfg2", "cfg3", "cfg5"):
         assert re.search(cfg + r" .*bound ([0-9.]+) LSB", r.stdout), cfg
@@ -55,7 +66,8 @@ def test_vr_two_limb_quantisation_bound():
 
 @pytest.mark.parametrize("src,kernels", [
     ("fi_vr.hip", ["_ZN2fi7k_rs_vrILi0ELi2EE", "_ZN2fi7k_rs_vrILi0ELi4EE"]),
-    ("fi_smartcrop.hip", ["_ZN2fi11k_sc_score2ILi1EE", "_ZN2fi11k_sc_score3E", ("_ZN2fi7k_sc_fdE", 12)]),
+    ("fi_smartcrop.hip", ["_ZN2fi11k_sc_score2ILi1EE", "_ZN2fi11k_sc_score3E", ("_ZN2fi7k_sc_fdE", 12),
+                          "_ZN2fi7k_sc_ftILi1EE", "_ZN2fi7k_sc_ftILi2EE"]),
 ])
 def test_hot_kernels_do_not_spill(src, kernels):
     """The production kernels of the hot path keep every value in registers: a
