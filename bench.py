@@ -626,7 +626,8 @@ def run_cfg4(args, rank, world, local_rank, comm):
     comm.barrier()
     ctx.set_timing(False)
     names = ("batch", "resize", "sc_prep", "sc_score", "crop_apply", "mono", "host_plan", "host_plan_images",
-             "host_plan_sc", "host_plan_tiles", "host_plan_vmtiles", "host_plan_blob", "host_launch", "host_wait",
+             "host_plan_sc", "host_plan_tiles", "host_plan_vmtiles", "host_plan_vr", "host_plan_hv", "host_plan_blob",
+             "host_launch", "host_wait",
              "host_total")
     stats = {k: ctx.stats(k) for k in names}
     paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in KERNEL_OF_PATH}

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <map>
+#include <unordered_map>
 #include <queue>
 #include <set>
 #include <memory>
@@ -193,6 +194,36 @@ struct Slot {
   size_t hpin_cap = 0;
 };
 constexpr int kSlots = 2;
+// hash of the planner's cache keys (tuples / pairs of ints, doubles' bits and
+// pointers): the per-image lookups of a mixed batch run in O(1) (a std::map
+// over thousands of tables cost ~1 us per lookup in cache misses)
+struct KeyHash {
+  template <class T>
+  static void mix(size_t &h, const T &v) {
+    h ^= std::hash<T>()(v) + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+  }
+  template <class... A>
+  size_t operator()(const std::tuple<A...> &t) const {
+    size_t h = 0;
+    std::apply([&](const auto &...x) { (mix(h, x), ...); }, t);
+    return h;
+  }
+  template <class A, class B>
+  size_t operator()(const std::pair<A, B> &p) const {
+    size_t h = 0;
+    mix(h, p.first);
+    mix(h, p.second);
+    return h;
+  }
+  template <class T>
+  size_t operator()(T *p) const {
+    size_t h = 0;
+    mix(h, (uintptr_t)p);
+    return h;
+  }
+};
+template <class K, class V>
+using HashMap = std::unordered_map<K, V, KeyHash>;
 struct fi_ctx {
   int device = 0;
   Slot slots[kSlots];
@@ -237,8 +268,8 @@ struct fi_ctx {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
   // caches (host planning is deterministic, keyed by geometry)
-  std::map<std::tuple<int, uint64_t, int, int, int, int, int, int>, AxisTable> axis_cache;
-  std::map<std::tuple<int, int, int, int, uint64_t>, ScPlan> sc_cache;
+  HashMap<std::tuple<int, uint64_t, int, int, int, int, int, int>, AxisTable> axis_cache;
+  HashMap<std::tuple<int, int, int, int, uint64_t>, ScPlan> sc_cache;
   std::map<std::tuple<uint64_t, uint64_t, int, int, uint64_t>, std::vector<double>> imp_cache;
   bool fast_rs = true;  // FI_FORCE_GENERIC=1: the generic two-pass resample (and smartcrop) kernels only
   bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
@@ -259,11 +290,11 @@ struct fi_ctx {
   void *jpeg_host = nullptr;  // its pinned staging
   size_t jpeg_host_cap = 0;
   std::string skinsat_key;
-  std::map<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
-  std::map<const AxisTable *, VrV> vrv_cache;   // ok iff nblk > 0
-  std::map<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
-  std::map<const AxisTable *, HvV> hvv_cache;  // ok iff nblk > 0
-  std::map<const AxisTable *, HvH> hvh_cache;  // ok iff !strips.empty()
+  HashMap<const AxisTable *, VmV> vmv_cache;   // ok iff nblk > 0
+  HashMap<const AxisTable *, VrV> vrv_cache;   // ok iff nblk > 0
+  HashMap<std::pair<const AxisTable *, bool>, MfmaH> vmh_cache; // strips of <= kVmMaxNx px; ok iff !strips.empty()
+  HashMap<const AxisTable *, HvV> hvv_cache;  // ok iff nblk > 0
+  HashMap<const AxisTable *, HvH> hvh_cache;  // ok iff !strips.empty()
   bool sc_prep = true;  // FI_DISABLE_SC_PREP=1 forces the generic per-row smartcrop kernels
   // Device-resident table heaps: every per-geometry table (tap tables, MFMA
   // fragments, Pillow coefficients, importance tables) is uploaded once and
@@ -282,23 +313,34 @@ struct fi_ctx {
     int32_t hmB = 0, hmC = 0, hmS0 = 0, vqA = 0, vqC = 0, vqK0 = 0;
     int32_t ftB = -1;
   };
-  std::map<const AxisTable *, DevAxis> axis_at;
-  std::map<const AxisTable *, int32_t> axis_wd_at;  // f64 weights (RGBA path) in heap_d
-  std::map<const ScPlan *, ScTabs> sc_at;
+  HashMap<const AxisTable *, DevAxis> axis_at;
+  HashMap<const AxisTable *, int32_t> axis_wd_at;  // f64 weights (RGBA path) in heap_d
+  HashMap<const ScPlan *, ScTabs> sc_at;
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp_at;
   std::map<std::pair<const std::vector<double> *, int>, std::pair<int32_t, double>> imp2_at;  // importance - oi
   // k_sc_score3 B fragments: (table, nx, nslot, step) -> heap offset + the table's digit sums / q
   std::map<std::tuple<const std::vector<double> *, int, int, int>, std::pair<int32_t, ScoreBTab>> sgb_at;
-  std::map<const VmV *, std::array<int32_t, 8>> vv_at;
-  std::map<const VrV *, std::array<int32_t, 4>> vr_at;    // rows, bmeta, w128, frag
-  std::map<const MfmaH *, std::array<int32_t, 6>> mh_at;  // wsum, frag, s0, lut, frag2, wsum2
-  std::map<const HvV *, std::array<int32_t, 3>> hvv_at;   // k0ks, frag, wsum
-  std::map<const HvH *, std::array<int32_t, 3>> hvh_at;   // w128, frag, s0
+  HashMap<const VmV *, std::array<int32_t, 8>> vv_at;
+  HashMap<const VrV *, std::array<int32_t, 4>> vr_at;    // rows, bmeta, w128, frag
+  // horizontal tables placed: the strips' device descriptors (heap offsets
+  // resolved) and the k_rs_vm LDS of their widest strip, kept with the
+  // placement so a batch copies them contiguously instead of re-deriving them
+  // from the (cold) MfmaH per batch
+  struct MhPlaced {
+    int32_t hwsum = 0, hwsum2 = 0;
+    size_t lds8 = 0, lds16 = 0;  // k_rs_vm LDS with an 8-bit / Q16 output tile
+    std::vector<MStrip> strips;
+  };
+  HashMap<const MfmaH *, MhPlaced> mh_at;
+  HashMap<const HvV *, std::array<int32_t, 3>> hvv_at;   // k0ks, frag, wsum
+  HashMap<const HvH *, std::array<int32_t, 3>> hvh_at;   // w128, frag, s0
   int32_t mono_wts_at = -1;
   bool heap_retry = false;
+  bool host_only = false;  // fi_debug_host_plan: planner only, no device (no allocation, no stream)
 };
 
 static void sync_streams(fi_ctx *c) {
+  if (c->host_only) return;
   (void)hipStreamSynchronize(c->stream);
   if (c->sc_stream != c->stream) (void)hipStreamSynchronize(c->sc_stream);
   if (c->up_stream) (void)hipStreamSynchronize(c->up_stream);
@@ -531,6 +573,10 @@ static int heap_prepare(fi_ctx *c, Exec &E) {
     size_t cap, esz;
   } hs[3] = {{&c->heap_i, kHeapI, 4}, {&c->heap_f, kHeapF, 4}, {&c->heap_d, kHeapD, 8}};
   for (auto &x : hs) {
+    if (c->host_only) {  // planner timing: offsets only, nothing is written through the heaps
+      x.h->cap = x.cap;
+      continue;
+    }
     if (!x.h->p) {
       if (hipMalloc(&x.h->p, x.cap * x.esz) != hipSuccess) {
         x.h->p = nullptr;
@@ -579,7 +625,7 @@ static int heap_commit(fi_ctx *c, Exec &E, const uint8_t *ab, size_t ai_off, siz
 
 static const AxisTable *add_axis(fi_ctx *c, Exec &E, int filter, double factor, int in_sampled, int out_size,
                                  int o0, int o1, bool sample, int in_src, DevAxis *out,
-                                 std::map<const AxisTable *, DevAxis> &placed) {
+                                 HashMap<const AxisTable *, DevAxis> &placed) {
   auto key = std::make_tuple(filter, dbits(factor), in_sampled, out_size, o0, o1, (int)sample, in_src);
   auto it = c->axis_cache.find(key);
   if (it == c->axis_cache.end()) {
@@ -1221,7 +1267,7 @@ struct BatchPlan {
   std::vector<int> rd_of;      // image -> rd index (-1: the image failed)
   std::vector<ScItem> sitems;  // smartcrop jobs
   std::vector<int> sc_of;      // image -> sitems index (-1: none)
-  std::map<const AxisTable *, DevAxis> placed;
+  HashMap<const AxisTable *, DevAxis> placed;
   // resample path members (indices into rd) and their tables
   std::vector<int> vm_img;
   std::vector<const VmV *> vm_v;
@@ -1731,7 +1777,7 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
   struct Span {
     int32_t glen, inner, head, tail;
   };
-  std::map<std::tuple<const VrV *, int, int>, Span> spans;
+  HashMap<std::tuple<const VrV *, int, int>, Span> spans;
   std::tuple<const VrV *, int, int> last_key{nullptr, -1, -1};
   const Span *last_sp = nullptr;
   auto span_of = [&](const VrV &V, int b0, int b1) -> const Span & {
@@ -1759,6 +1805,14 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     const Span *sp;
   };
   std::vector<TC> all;
+  all.reserve((size_t)nst);
+  // tiles of one (image, band) share a cost: groups [first, first + n) of `all`
+  struct Grp {
+    int64_t cost;
+    int32_t first, n;
+  };
+  std::vector<Grp> grps;
+  grps.reserve(work.size());
   std::vector<int64_t> img_cost(work.size(), 0);
   for (size_t k = 0; k < work.size(); k++) {
     const VrWork &w = work[k];
@@ -1771,10 +1825,10 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
       const Span &sp = span_of(*w.V, b0, b1);
       if (sp.inner > L.R) return false;
       const int64_t cost = sp.glen + 16 * (b1 - b0);
-      for (int st = 0; st < w.nstrips; st++) {
+      grps.push_back(Grp{cost, (int32_t)all.size(), w.nstrips});
+      for (int st = 0; st < w.nstrips; st++)
         all.push_back(TC{VrTile{desc_of[k], w.first_strip + st, b0, b1, 0, 0, 0, (int32_t)k}, cost, &sp});
-        img_cost[k] += cost;
-      }
+      img_cost[k] += cost * w.nstrips;
     }
   }
   const int ntiles = (int)all.size();
@@ -1819,32 +1873,41 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
       load[x] += img_cost[k];
     }
   }
-  // equal costs (a uniform batch) keep the list order: no sort needed
+  // equal costs (a uniform batch) keep the list order: no sort needed; else
+  // LPT over the tiles longest first, sorting the (image, band) groups (the
+  // tiles of a group cost the same) rather than the tiles
   bool uniform = true;
-  for (const TC &tc : all) uniform = uniform && tc.cost == all[0].cost;
-  if (!uniform) std::stable_sort(all.begin(), all.end(), [](const TC &x, const TC &y) { return x.cost > y.cost; });
+  for (const Grp &gp : grps) uniform = uniform && gp.cost == grps[0].cost;
+  std::vector<const TC *> order_t;
+  order_t.reserve(all.size());
+  if (uniform) {
+    for (const TC &tc : all) order_t.push_back(&tc);
+  } else {
+    std::stable_sort(grps.begin(), grps.end(), [](const Grp &x, const Grp &y) { return x.cost > y.cost; });
+    for (const Grp &gp : grps)
+      for (int i = 0; i < gp.n; i++) order_t.push_back(&all[gp.first + i]);
+  }
   std::vector<std::vector<const TC *>> per(G);
+  for (auto &v : per) v.reserve(ntiles / G + 8);
   if (uniform) {
     // equal costs: LPT is a round robin over each XCD's workgroups
     std::vector<int> next(nx, 0);
     const int per_x = G / nx;
-    for (const TC &tc : all) {
-      const int x = xcd_of[tc.t.pad];
-      per[x + nx * (next[x]++ % per_x)].push_back(&tc);
+    for (const TC *tc : order_t) {
+      const int x = xcd_of[tc->t.pad];
+      per[x + nx * (next[x]++ % per_x)].push_back(tc);
     }
   } else {
-    // per XCD: a min-heap of (load, workgroup)
-    std::vector<std::priority_queue<std::pair<int64_t, int>, std::vector<std::pair<int64_t, int>>,
-                                    std::greater<std::pair<int64_t, int>>>>
-        heap(nx);
-    for (int g = 0; g < G; g++) heap[g % nx].push({0, g});
-    for (const TC &tc : all) {
-      auto &h = heap[xcd_of[tc.t.pad]];
-      auto top = h.top();
-      h.pop();
-      per[top.second].push_back(&tc);
-      top.first += tc.cost;
-      h.push(top);
+    // longest first, dealt boustrophedon over each XCD's workgroups (0 .. n-1,
+    // n-1 .. 0, ...): O(1) per tile and, over ~80 sorted tiles per
+    // workgroup, within a tile of LPT's balance (an LPT heap per tile cost
+    // ~1 ms of host planning per cfg4 batch)
+    std::vector<int> next(nx, 0);
+    const int per_x = G / nx;
+    for (const TC *tc : order_t) {
+      const int x = xcd_of[tc->t.pad];
+      const int i = next[x]++, r = i % per_x;
+      per[x + nx * (((i / per_x) & 1) ? per_x - 1 - r : r)].push_back(tc);
     }
   }
   // the streams: workgroup g walks tiles [t0(g), t1(g)); every phase's rows
@@ -1917,7 +1980,7 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     E.ai.insert(E.ai.end(), v.begin(), v.end());
     return o;
   };
-  std::map<const MfmaH *, std::array<int32_t, 3>> hplaced;  // first strip, hwsum, hwsum2
+  HashMap<const MfmaH *, std::array<int32_t, 5>> hplaced;  // first strip, hwsum, hwsum2, LDS (8-bit / Q16 tile)
   struct Work1 {
     int32_t img, first_strip, nstrips;
     const VmV *V;
@@ -1926,6 +1989,8 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   };
   std::vector<Work1> work;
   const int nv = (int)Bp.vm_img.size();
+  work.reserve(nv);
+  Bp.vdescs.reserve(2 * (size_t)nv);  // + the k_rs_vr descriptors
   for (int q = 0; q < nv; q++) {
     const ResizeDesc &d = Bp.rd[Bp.vm_img[q]];
     const VmV &V = *Bp.vm_v[q];
@@ -1958,44 +2023,48 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
       const int32_t first = (int32_t)Bp.vstrips.size();
       auto ht = c->mh_at.find(&H);
       if (ht == c->mh_at.end()) {
-        std::array<int32_t, 6> o;
-        o[0] = put(H.wsum);
+        fi_ctx::MhPlaced pl;
+        pl.hwsum = put(H.wsum);
         align4();
-        o[1] = put(H.frag);
-        o[2] = put(H.s0);
+        const int32_t frag = put(H.frag);
+        const int32_t s0 = put(H.s0);
         align4();  // 16-byte aligned LUT rows (k_rs_vr's LDS-DMA)
-        o[3] = put(H.lut);
+        const int32_t lut = put(H.lut);
         align4();
-        o[4] = put(H.frag2);
-        o[5] = put(H.wsum2);
-        ht = c->mh_at.emplace(&H, o).first;
+        const int32_t frag2 = put(H.frag2);
+        pl.hwsum2 = put(H.wsum2);
+        pl.strips.reserve(H.strips.size());
+        for (const MfmaStrip &st : H.strips) {
+          MStrip m{};
+          m.x0 = st.x0;
+          m.x1 = st.x1;
+          m.b0 = st.b0;
+          m.nbytes = st.nbytes;
+          m.c_lo = st.c_lo;
+          m.ncols = st.ncols;
+          m.pitch = st.pitch;
+          m.nocb = st.nocb;
+          m.ks = st.ks;
+          m.lut_px0 = st.lut_px0;
+          m.lut_n = st.lut_n;
+          m.frag = frag + (int32_t)st.frag;
+          m.s0 = s0 + (int32_t)st.s0;
+          m.lut = lut + (int32_t)st.lut;
+          m.vpitch = st.vpitch;
+          m.frag2 = frag2 + (int32_t)st.frag2;
+          pl.strips.push_back(m);
+          // the workgroup's LDS layout follows its strip and tile kind
+          pl.lds8 = std::max(pl.lds8, vm_lds_bytes(st.vpitch, st.nocb, st.ks, false));
+          pl.lds16 = std::max(pl.lds16, vm_lds_bytes(st.vpitch, st.nocb, st.ks, true));
+        }
+        ht = c->mh_at.emplace(&H, std::move(pl)).first;
       }
-      const int32_t hw = ht->second[0], frag = ht->second[1], s0 = ht->second[2], lut = ht->second[3];
-      const int32_t frag2 = ht->second[4], hw2 = ht->second[5];
-      for (const MfmaStrip &st : H.strips) {
-        MStrip m{};
-        m.x0 = st.x0;
-        m.x1 = st.x1;
-        m.b0 = st.b0;
-        m.nbytes = st.nbytes;
-        m.c_lo = st.c_lo;
-        m.ncols = st.ncols;
-        m.pitch = st.pitch;
-        m.nocb = st.nocb;
-        m.ks = st.ks;
-        m.lut_px0 = st.lut_px0;
-        m.lut_n = st.lut_n;
-        m.frag = frag + (int32_t)st.frag;
-        m.s0 = s0 + (int32_t)st.s0;
-        m.lut = lut + (int32_t)st.lut;
-        m.vpitch = st.vpitch;
-        m.frag2 = frag2 + (int32_t)st.frag2;
-        Bp.vstrips.push_back(m);
-      }
-      hp = hplaced.emplace(&H, std::array<int32_t, 3>{first, hw, hw2}).first;
+      const fi_ctx::MhPlaced &pl = ht->second;
+      Bp.vstrips.insert(Bp.vstrips.end(), pl.strips.begin(), pl.strips.end());
+      hp = hplaced.emplace(&H, std::array<int32_t, 5>{first, pl.hwsum, pl.hwsum2, (int32_t)pl.lds8, (int32_t)pl.lds16})
+               .first;
     }
-    for (const MfmaStrip &st : H.strips)  // the workgroup's LDS layout follows its strip and tile kind
-      Bp.vm_lds = std::max(Bp.vm_lds, vm_lds_bytes(st.vpitch, st.nocb, st.ks, d.gray || d.rot != 0));
+    Bp.vm_lds = std::max(Bp.vm_lds, (size_t)hp->second[(d.gray || d.rot != 0) ? 4 : 3]);
     VDesc m{};
     m.src = d.src;
     m.src_stride = d.src_stride;
@@ -2027,6 +2096,7 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
   Bp.vrl.clear();
   Bp.vrtiles.clear();
   Bp.vr_info.clear();
+  const double t_vr0 = now_ms();
   if (c->vr_rs) {
     std::vector<Work1> rest;
     std::vector<VrWork> vr;
@@ -2053,9 +2123,12 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     // k_rs_vr than on k_rs_vm in round 4 (432 vs 385 ms), hence a class cap
     // (FI_VR_MAX_CLASSES); since round 5 (4 loader waves for one-block strips,
     // their own launch) k_rs_vr takes them: cfg4 resize 363 -> 329 ms per step
-    std::set<const VrV *> classes;
-    for (const VrWork &w : vr) classes.insert(w.V);
-    if (!vr.empty() && (int)classes.size() <= c->vr_max_classes) {
+    std::vector<const VrV *> classes;
+    classes.reserve(vr.size());
+    for (const VrWork &w : vr) classes.push_back(w.V);
+    std::sort(classes.begin(), classes.end());
+    const int nclasses = (int)(std::unique(classes.begin(), classes.end()) - classes.begin());
+    if (!vr.empty() && nclasses <= c->vr_max_classes) {
       // two launches when the batch mixes strips of one 16-px output block
       // (4 loader waves) with wider ones (2) and both halves fill the chip
       std::vector<int> grp(vr.size(), 0);
@@ -2080,6 +2153,7 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
       work.swap(rest);
     }
   }
+  host_stat(c, "host_plan_vr", now_ms() - t_vr0);
   // bands of blocks only when the batch is too small to fill the chip
   int64_t nst = 0;
   for (const Work1 &w : work) nst += w.nstrips;
@@ -2143,7 +2217,7 @@ static void build_hv_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     E.ai.insert(E.ai.end(), v.begin(), v.end());
     return o;
   };
-  std::map<const HvH *, int32_t> splaced;  // first strip in Bp.hstrips
+  HashMap<const HvH *, int32_t> splaced;  // first strip in Bp.hstrips
   struct Work1 {
     int32_t img, first_strip, nstrips, nblk, nrows;
   };
@@ -2545,8 +2619,10 @@ static int run_batch(fi_ctx *c, fi_image *imgs, int32_t n, bool async, std::shar
   const double t_sc = now_ms();
   const double t_tiles0 = now_ms();
   build_vm_tiles(c, E, Bp);
+  const double t_tiles1 = now_ms();
   build_hv_tiles(c, E, Bp);
   const double t_tiles = now_ms();
+  host_stat(c, "host_plan_hv", t_tiles - t_tiles1);
   Packed K;
   pack_batch(c, E, Bp, K);
   if (!heap_fits(c, E)) {
@@ -3268,6 +3344,85 @@ int fi_plan_bytes(const fi_image *imgs, int32_t n, int64_t *bytes) {
                ((imgs[i].flags & FI_OP_SMARTCROP) ? 16 : 0);
   }
   return first;
+}
+
+// Test hook (host only, needs no GPU): run_batch's planner -- plan_image,
+// plan_batch_sc, resolve_workspace, build_vm_tiles (with the k_rs_vr tiles),
+// build_hv_tiles, pack_batch -- over `imgs` `iters` times on one host-only
+// context (device pointers are planned, never dereferenced; caches and heap
+// offsets persist across iterations as across a serving run's batches).
+// ms[0..6] += images, smartcrop, workspace, vm + vr tiles, of which vr, hv
+// tiles, blob (milliseconds, summed over the iterations).
+int fi_debug_host_plan(const fi_image *imgs, int32_t n, int32_t iters, double *ms) {
+  static fi_ctx *c = nullptr;  // one host-only context across calls (its caches, as a serving context's)
+  if (!imgs && n == 0) {       // (NULL, 0, ...): drop it
+    if (c && getenv("FI_PLAN_PROF"))
+      for (const auto &kv : c->stats) fprintf(stderr, "%s %.1f ms (%lld)\n", kv.first.c_str(), kv.second.ms, (long long)kv.second.launches);
+    delete c;
+    c = nullptr;
+    return FI_OK;
+  }
+  if (!imgs && n == 1) {  // (NULL, 1, ...): reset the stage stats (after a warm-up pass)
+    if (c) c->stats.clear();
+    return FI_OK;
+  }
+  if (!imgs || n <= 0 || iters <= 0 || !ms) return set_err(FI_EINVAL, "bad arguments");
+  if (!c) {
+    c = new fi_ctx();
+    c->host_only = true;
+    c->timing = true;
+    if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
+  }
+  std::vector<fi_image> v(imgs, imgs + n);
+  uint8_t *wb = reinterpret_cast<uint8_t *>((uintptr_t)1 << 40);  // a stand-in workspace base
+  int rc = FI_OK;
+  for (int it = 0; it < iters && rc == FI_OK; it++) {
+    const double t0 = now_ms();
+    Exec E;
+    E.c = c;
+    fi_smartcrop_default_params(&E.params);
+    rc = heap_prepare(c, E);
+    if (rc) break;
+    BatchPlan Bp;
+    Bp.imgs = v.data();
+    Bp.n = n;
+    Bp.plans.resize(n);
+    Bp.status.assign(n, FI_OK);
+    Bp.errs.resize(n);
+    Bp.rd_of.assign(n, -1);
+    Bp.sc_of.assign(n, -1);
+    Bp.res_off.assign(n, 0);
+    Bp.res_stride.assign(n, 0);
+    Bp.out_of.assign(n, nullptr);
+    for (int i = 0; i < n; i++) plan_image(c, E, Bp, i);
+    const double t1 = now_ms();
+    plan_batch_sc(c, E, Bp);
+    const double t2 = now_ms();
+    resolve_workspace(E, Bp, wb);
+    const double t3 = now_ms();
+    const double vr0 = c->stats["host_plan_vr"].ms;
+    build_vm_tiles(c, E, Bp);
+    const double t4 = now_ms();
+    build_hv_tiles(c, E, Bp);
+    const double t5 = now_ms();
+    Packed K;
+    pack_batch(c, E, Bp, K);
+    const double t6 = now_ms();
+    if (!heap_fits(c, E)) heap_reset(c);
+    else {
+      c->heap_i.used = (size_t)E.bi + (E.ai.size() + 15) / 16 * 16;
+      c->heap_f.used = (size_t)E.bf + (E.af.size() + 15) / 16 * 16;
+      c->heap_d.used = (size_t)E.bd + (E.ad.size() + 15) / 16 * 16;
+    }
+    ms[0] += t1 - t0;
+    ms[1] += t2 - t1;
+    ms[2] += t3 - t2;
+    ms[3] += t4 - t3;
+    ms[4] += c->stats["host_plan_vr"].ms - vr0;
+    ms[5] += t5 - t4;
+    ms[6] += t6 - t5;
+  }
+  return rc;
 }
 
 int fi_process_batch_device(fi_ctx *c, fi_image *imgs, int32_t n) {

@@ -10,6 +10,12 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/r06; mkdir -p "$OUT"
 for s in ${STEP:-tests bench trace}; do
   case $s in
+  full)
+    rm -f "$OUT/exact.tsv"
+    FI_EXACT_LOG="$OUT/exact.tsv" timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --durations=25 \
+      --timeout 300 --timeout-method thread > "$OUT/pytest_full.log" 2>&1; rc=$?
+    echo "pytest full rc=$rc"; tail -30 "$OUT/pytest_full.log" | grep -E "passed|failed|s call" | head -30
+    [ $rc -eq 0 ] || exit $rc ;;
   tests)
     timeout -k 10 500 python -u -m pytest tests/test_gpu_streams.py tests/test_gpu_parity.py -m gpu -x -q -rf \
       -k "${TESTK:-streams or smartcrop or score3 or pipelined or baseline_geometries}" \
@@ -22,6 +28,11 @@ for s in ${STEP:-tests bench trace}; do
       [ $rc -eq 0 ] || { echo "bench ft=$ft rc=$rc"; tail -5 "$OUT/bench_ft$ft.err"; exit $rc; }
       python3 -c "import json;d=json.load(open('$OUT/bench_ft$ft.json'));print('ft=$ft', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['stages_ms_per_step'], d['smartcrop_kernels'], d['verified'][:5])"
     done ;;
+  cfg4)
+    timeout -k 10 600 python bench.py --workload cfg4 --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/cfg4.json" \
+      2> "$OUT/cfg4.err"; rc=$?
+    [ $rc -eq 0 ] || { echo "cfg4 rc=$rc"; tail -5 "$OUT/cfg4.err"; exit $rc; }
+    python3 -c "import json;d=json.load(open('$OUT/cfg4.json'));print('cfg4', d['value'], d['ms_per_step'], d['roofline']['frac'], d['verified'][:5]); print({k: v for k, v in d['stages_ms_per_step'].items() if k.startswith('host') or k in ('resize','sc_prep','sc_score','batch')})" ;;
   trace)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
