@@ -283,7 +283,9 @@ struct fi_ctx {
   int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   bool sc_fd = true;        // FI_SC_FD=0: k_sc_fz instead of its LDS-DMA form k_sc_fd
-  bool sc_ft = true;        // FI_SC_FT=0: k_sc_fd (per image) instead of the chunk-tiled k_sc_ft
+  // k_sc_ft (chunk tiles) for the images k_sc_fd cannot stream (analysed widths
+  // over 224 px, LDS): FI_SC_FT=0 never, 1 there (default), 2 in place of k_sc_fd too
+  int sc_ft = 1;
   bool sc_mf = true;        // FI_SC_MFMA=0: k_sc_score2 (f64 VALU fast pass) instead of k_sc_score3
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
   DevBuf jpeg[3];           // GPU JPEG decode: upload (compressed data + tables), -, coefficients + planes
@@ -989,7 +991,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     // k_sc_ft: the vertical tables (one 64-row window per chunk), the
     // horizontal ones at <= 2 k-steps, 16-B aligned 3-channel rows readable to
     // fd_rp(W) (the source's own alignment is checked at launch)
-    d.ft = d.vq && c->sc_ft && c->sc_fz && c->sc_fd && P.fx == 1 && P.fy == 1 && it.C == 3 && it.stride % 16 == 0 &&
+    d.ft = d.vq && c->sc_ft > 0 && c->sc_fz && c->sc_fd && P.fx == 1 && P.fy == 1 && it.C == 3 && it.stride % 16 == 0 &&
                    (it.padded || (it.W * 3) % 16 == 0) && P.hm_ks <= 2 && T.ftB >= 0 && P.ft_lds > 0 &&
                    P.ft_lds <= kFtMaxLds
                ? 1
@@ -1078,11 +1080,15 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
     const ScDesc &d = SL.descs[k];
     const ScPlan &P = *SL.plans[k];
     if (d.red) sred.push_back((int)k);
-    if (d.ft && ((uintptr_t)d.img & 15) == 0) {
+    const bool aligned = ((uintptr_t)d.img & 15) == 0;
+    const bool fd_ok = d.fz && d.fd && aligned;
+    // k_sc_fd where it streams the image (cfg2: 0.353 vs k_sc_ft's 0.363 ms per
+    // 1024 images), k_sc_ft where it does not (FI_SC_FT=2: k_sc_ft first)
+    if (d.ft && aligned && (!fd_ok || c->sc_ft == 2)) {
       ft.push_back(d);
       ft_chunks.push_back(P.vq_chunks);
       X->ft_lds = std::max(X->ft_lds, P.ft_lds);
-    } else if (d.fz && d.fd && ((uintptr_t)d.img & 15) == 0) {
+    } else if (fd_ok) {
       fd.push_back(d);
       X->fd_lds = std::max(X->fd_lds, fd_lds(d.W, d.hm_pitch, d.aw, d.ah));
     } else if (d.fz) {
@@ -3210,7 +3216,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_VR_PBUF")) c->vr_pbuf = atoi(e);
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';
-  if (const char *e = getenv("FI_SC_FT")) c->sc_ft = e[0] == '1';
+  if (const char *e = getenv("FI_SC_FT")) c->sc_ft = atoi(e);
   if (const char *e = getenv("FI_SC_MFMA")) c->sc_mf = e[0] == '1';
   if (const char *e = getenv("FI_VR_MAX_CLASSES")) c->vr_max_classes = atoi(e);
   if (const char *e = getenv("FI_VM_LPT")) c->vm_lpt = e[0] == '1';

@@ -58,8 +58,9 @@ def _context_with(env):
 _ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_SC_FD": "1", "FI_SC_FT": "1"}
 PATHS = {
     # default kernels: k_rs_vr (block-major persistent MFMA resample; k_rs_vm
-    # where its tables do not fit) / k_rs_hv; k_sc_ft chunk-tiled prescale +
-    # maps; k_sc_score3 (exact-integer MFMA score fast pass)
+    # where its tables do not fit) / k_rs_hv; k_sc_fd streamed prescale + maps
+    # (k_sc_ft chunk tiles where it cannot stream); k_sc_score3 (exact-integer
+    # MFMA score fast pass)
     "vr": dict(_ENV),
     # the same with k_sc_fz (register-staged source rows, two workgroups per CU)
     "fz": dict(_ENV, FI_SC_FD="0"),
@@ -82,9 +83,9 @@ def rctx(request):
 
 EXPECTED_PATH = {"vr": "path_vr", "fz": "path_vr", "vm": "path_vm", "generic": "path_generic_v"}
 # smartcrop prescale kernel of each path (images counted by fi_kernel_stats)
-EXPECTED_SC = {"vr": "sc_path_ft", "fd": "sc_path_fd", "fz": "sc_path_fz", "vm": None, "generic": None}
-# the smartcrop tests also run k_sc_fd (per-image streamed prescale, FI_SC_FT=0)
-SC_PATHS = dict(PATHS, fd=dict(_ENV, FI_SC_FT="0"))
+EXPECTED_SC = {"vr": "sc_path_fd", "ft": "sc_path_ft", "fz": "sc_path_fz", "vm": None, "generic": None}
+# the smartcrop tests also run k_sc_ft (chunk-tiled prescale) on every image
+SC_PATHS = dict(PATHS, ft=dict(_ENV, FI_SC_FT="2"))
 
 
 @pytest.mark.parametrize("W,H,opts,even_rows", [
@@ -231,8 +232,8 @@ def test_score3_runs_and_agrees_with_score2(ctx, s2ctx, w, h):
 @pytest.mark.parametrize("w,h", [(500, 281), (333, 500), (450, 300), (301, 201)])
 def test_smartcrop_prescale_kernel_of_path(sctx, w, h):
     """fi_smartcrop runs its prescale + maps on the kernel the path names
-    (k_sc_ft on the default path for 3-channel images at the staged 16-B
-    rounded pitch, k_sc_fd with FI_SC_FT=0, k_sc_fz with FI_SC_FD=0; no
+    (k_sc_fd on the default path for 3-channel images at the staged 16-B
+    rounded pitch, k_sc_ft with FI_SC_FT=2, k_sc_fz with FI_SC_FD=0; no
     silent fallback), and the result is the oracle's: every crop's scores
     bit-exact (exact_all).  The sizes prescale by 1.8-3 (a 14-row chunk's
     window within 64 H-stage rows)."""
@@ -306,7 +307,14 @@ def test_smartcrop_dropin_module(ctx):
     assert len(res["crops"]) == len(g["crops"])
 
 
-def _cmp(gpu, ref, name, min_exact=0.98):
+# exact-match floors: the BASELINE geometries measure
+# 0.9996-0.9999 exact against the oracle, everything else >= 0.9986
+# (profiles/r06/exact_fractions.tsv) -- a regression to 0.98 no longer passes
+MIN_EXACT_BASELINE = 0.999
+MIN_EXACT = 0.995
+
+
+def _cmp(gpu, ref, name, min_exact=MIN_EXACT):
     assert gpu.shape == ref.shape, (name, gpu.shape, ref.shape)
     d = np.abs(gpu.astype(np.int16) - ref.astype(np.int16))
     exact = float((d == 0).mean())
@@ -358,7 +366,8 @@ def test_resize_within_one_lsb_of_oracle(rctx, case):
     outs, recs, rc = ctx.process([src], [Op(tw, th, flags, grav, rot)])
     assert rc == 0 and recs[0].status == 0, L.lib().fi_last_error()
     ref = orc.im_convert(src, tw, th, _oracle_flags(flags), gravity=grav, rotate=rot)
-    _cmp(outs[0], ref, name)
+    # w_500_shrink is cfg2's geometry (1920x1080 -> w_500), c1_300x250 cfg1's
+    _cmp(outs[0], ref, name, MIN_EXACT_BASELINE if name in ("w_500_shrink", "c1_300x250") else MIN_EXACT)
 
 
 EDGE_CASES = [
@@ -419,7 +428,7 @@ HV_CASES = [
 def test_horizontal_first_within_one_lsb_of_oracle(rctx, case):
     """Horizontal-first geometries (IM runs HorizontalFilter first): the
     streaming k_rs_hv on the default path, the two-pass kernels on the others
-    -- +-1 LSB of the oracle, exact-match fraction >= 0.98 -- and the path
+    -- +-1 LSB of the oracle, exact-match fraction >= 0.995 -- and the path
     actually taken is the one named."""
     name, W, H, tw, th, flags, rot, grav, hv = case
     src = synth_rgb(W, H, 31 + W + H)
@@ -495,7 +504,7 @@ def test_full_size_pipeline_smartcrop_box_bit_exact(rctx, W, H, opts):
     # and the resample itself within +-1 of the oracle
     flags = op.flags
     ref_img = orc.im_convert(src, op.target_w, op.target_h, _oracle_flags(flags), rotate=op.rotate)
-    _cmp(resized, ref_img, opts)
+    _cmp(resized, ref_img, opts, MIN_EXACT_BASELINE)
 
 
 def _fast_rgb(W, H, seed):
@@ -563,7 +572,7 @@ def test_cfg4_slice_one_batch(ctx):
 
     with ThreadPoolExecutor(8) as ex:
         exact = list(ex.map(check, range(len(picks))))
-    assert len(exact) == len(picks) >= 55 and min(exact) >= 0.98
+    assert len(exact) == len(picks) >= 55 and min(exact) >= MIN_EXACT
 
 
 @pytest.fixture(scope="module", params=["1", "0"], ids=["apply_overlap", "apply_serial"])

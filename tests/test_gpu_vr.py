@@ -2,19 +2,30 @@
 class it takes: the path actually ran (its image counter rose by the batch),
 the output is bit-identical to k_rs_vm's (which carries k_rs_vr's two-limb
 weights scaled to 2^22, fi_plan.cpp axis_q22 -- so an image's pixels do not
-depend on which kernel its batch took), and within +-1 LSB / >= 98 % exact of
+depend on which kernel its batch took), and within +-1 LSB / >= 99.5 % exact (99.9 % on the BASELINE geometries) of
 the oracle (ImageProcessor.php:86 -thumbnail / -resize, IM's VerticalFilter
 then HorizontalFilter)."""
+import functools
+
 import numpy as np
 import pytest
 
 from flyimg_amd import _lib as L
 from flyimg_amd.processor import ImageProcessor, OptionsBag
-from flyimg_amd.synth import synth_rgb
+from flyimg_amd.synth import synth_rgb as _synth_rgb
 from oracle import oracle as orc
-from tests.test_gpu_parity import _context_with, _log_exact, _oracle_flags
+from tests.test_gpu_parity import MIN_EXACT, MIN_EXACT_BASELINE, _context_with, _log_exact, _oracle_flags
 
 pytestmark = pytest.mark.gpu
+
+
+@functools.lru_cache(maxsize=24)
+def synth_rgb(W, H, seed):
+    """the seeded synthetic source, generated once per module (the role-split
+    parametrizations reuse the 24 MP inputs; the kernels only read them)"""
+    a = _synth_rgb(W, H, seed)
+    a.flags.writeable = False
+    return a
 
 CASES = [
     # (W, H, options, images)
@@ -81,7 +92,8 @@ def test_vr_takes_the_class_and_matches(pair, W, H, opts, n):
         for j in range(k, n, len(base)):  # repeated sources give identical outputs
             assert np.array_equal(ob[j], ob[k])
     if W * H <= 4_000_000:
-        _close(ob[0], _oracle(base[0], op), f"{opts} vs oracle", 0.98)
+        baseline = (W, H, opts) in {(1920, 1080, "w_500"), (3000, 2000, "w_300,h_250,c_1")}
+        _close(ob[0], _oracle(base[0], op), f"{opts} vs oracle", MIN_EXACT_BASELINE if baseline else MIN_EXACT)
 
 
 def test_vr_mixed_batch(pair):
@@ -105,7 +117,7 @@ def test_vr_mixed_batch(pair):
     for k in range(len(srcs)):
         assert np.array_equal(ob[k], oa[k]), f"mixed {k}: k_rs_vr != k_rs_vm"
         if srcs[k].shape[0] * srcs[k].shape[1] <= 4_000_000:
-            _close(ob[k], _oracle(srcs[k], ops[k]), f"mixed {k} vs oracle", 0.98)
+            _close(ob[k], _oracle(srcs[k], ops[k]), f"mixed {k} vs oracle", MIN_EXACT)
 
 
 def test_output_independent_of_cobatched_images(pair):

@@ -22,7 +22,7 @@ for s in ${STEP:-tests bench trace}; do
       --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
     echo "pytest rc=$rc"; tail -4 "$OUT/pytest.log"; [ $rc -eq 0 ] || exit $rc ;;
   bench)
-    for ft in 1 0; do
+    for ft in ${FTS:-1 2}; do
       FI_SC_FT=$ft timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-20} > "$OUT/bench_ft$ft.json" \
         2> "$OUT/bench_ft$ft.err"; rc=$?
       [ $rc -eq 0 ] || { echo "bench ft=$ft rc=$rc"; tail -5 "$OUT/bench_ft$ft.err"; exit $rc; }
