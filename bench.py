@@ -79,6 +79,7 @@ KERNEL_OF_PATH = {
 }
 # smartcrop prescale + maps kernel per image (counts kept by the library)
 SC_KERNEL_OF_PATH = {
+    "sc_path_cx": "k_sc_hx + k_sc_vx (prescale + maps, co-resident beside the next batch's resample)",
     "sc_path_ft": "k_sc_ft (prescale + maps, one workgroup per analysed-row chunk)",
     "sc_path_fd": "k_sc_fd (prescale + maps, source rows by LDS-DMA)",
     "sc_path_fz": "k_sc_fz (prescale + maps, register-staged source rows)",
@@ -241,10 +242,17 @@ def launch_ranks(n: int) -> int:
     return 0
 
 
+# batches in flight per context: the library's slots (fi_api.cpp kSlots)
+PIPE_DEPTH = 3
+
+
 def run_batches(ctx, arrs, nimg, k0, count, on_done):
-    """Batches k0 .. k0+count-1 of one rank, pipelined: submit batch k
-    (fi_submit_batch_device: planned and uploaded while batch k-1 runs), then
-    finalize batch k-1 (fi_wait(1)) and hand its records to on_done(k-1, arr).
+    """Batches k0 .. k0+count-1 of one rank, pipelined len(arrs) deep (the
+    library's slots): submit batch k (fi_submit_batch_device: planned and
+    uploaded while earlier batches run), then finalize batch k-D+1
+    (fi_wait(D-1)) and hand its records to on_done.  With the smartcrop stage
+    beside the next resample, batch k's stage ends after batch k+1's resample,
+    so batch k+2 must be queued before batch k is waited for (D = 3).
     Nothing here waits on another rank: the result gather is the caller's, once
     after the last batch (RCCL on the library's gather stream), so no rank
     blocks its next batch on a collective.  Returns after every batch is
@@ -253,13 +261,17 @@ def run_batches(ctx, arrs, nimg, k0, count, on_done):
 
     if count <= 0:
         return
+    D = len(arrs)
+    done = k0
     for k in range(k0, k0 + count):
-        L.check(ctx.submit_device(arrs[k % 2], nimg))
-        if k > k0:
-            L.check(ctx.wait(1))  # batch k-1 done (batch k still queued)
-            on_done(k - 1, arrs[(k - 1) % 2])
+        L.check(ctx.submit_device(arrs[k % D], nimg))
+        if k - done >= D - 1:
+            L.check(ctx.wait(D - 1))  # batch `done` finished (later ones still queued)
+            on_done(done, arrs[done % D])
+            done += 1
     L.check(ctx.wait(0))
-    on_done(k0 + count - 1, arrs[(k0 + count - 1) % 2])
+    for k in range(done, k0 + count):
+        on_done(k, arrs[k % D])
 
 
 def dry_run(args, rank, world, local_rank, comm):
@@ -333,17 +345,17 @@ def main():
     ow, oh, oc = fi_plan(W, H, op)
     dst_cap = ow * oh * oc
     pool = ctx.malloc(src_bytes * nimg)
-    # one output set per in-flight batch: batch k+1 resamples while batch k's
-    # smart-crop stage still reads its resized outputs
-    dsts = [ctx.malloc(dst_cap * nimg) for _ in range(2)]
+    # one output set per in-flight batch (PIPE_DEPTH, the library's slots):
+    # batch k+1 resamples while batch k's smart-crop stage still runs
+    dsts = [ctx.malloc(dst_cap * nimg) for _ in range(PIPE_DEPTH)]
     t0 = time.perf_counter()
     for i in range(nimg):
         ctx.fill_synthetic(pool + i * src_bytes, W, H, src_stride, 0x5EED + rank * nimg + i)
     log(f"rank {rank}: pool {nimg} x {W}x{H} ({src_bytes * nimg / 1e9:.2f} GB) filled in {time.perf_counter() - t0:.1f} s")
-    # two descriptor arrays: batch k+1 is planned and launched while batch k
-    # runs (fi_submit_batch_device); batch k's records are finalized and
-    # gathered once k+1 is queued.
-    arrs = [(L.FiImage * nimg)() for _ in range(2)]
+    # one descriptor array per in-flight batch: batch k+2 is planned and
+    # launched while batches k, k+1 run (fi_submit_batch_device); batch k's
+    # records are finalized once k+2 is queued.
+    arrs = [(L.FiImage * nimg)() for _ in range(PIPE_DEPTH)]
     for arr, dst in zip(arrs, dsts):
         for i in range(nimg):
             a = arr[i]
@@ -389,13 +401,13 @@ def main():
     paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in KERNEL_OF_PATH}
     sc_paths = {p: ctx.stats(p)[1] // max(args.steps, 1) for p in SC_KERNEL_OF_PATH}
     ablation = ctx.stats("vr_ablation")[1]  # FI_VR_VARIANT profiling launches (wrong pixels)
-    last = arrs[(args.warmup + args.steps - 1) % 2]
+    last = arrs[(args.warmup + args.steps - 1) % PIPE_DEPTH]
     allv = comm.allgather_obj({"elapsed": el, "stats": stats,
                                "ncand": sum(last[i].n_candidates for i in range(nimg)),
                                "bad": bad[0]})
     # correctness of the headline batch itself (untimed): the last timed batch's
     # records and outputs against the oracle, including images past 2^32 of pool
-    vlast = (args.warmup + args.steps - 1) % 2
+    vlast = (args.warmup + args.steps - 1) % PIPE_DEPTH
     vok, vtot, verr = (0, 0, None)
     if not args.no_verify:
         from oracle.verify import verify_batch, verify_sample  # the checker (test infrastructure)
@@ -572,8 +584,8 @@ def run_cfg4(args, rank, world, local_rank, comm):
             op = ImageProcessor(OptionsBag(CFG4_OPS[k]), W, H).to_op()
             ops[(W, H, k)] = (op, fi_plan(W, H, op))
     cap = max(sum(int(np.prod(ops[items[i]][1])) for i in b) for b in batches) if batches else 1
-    dst = [ctx.malloc(cap), ctx.malloc(cap)]
-    arrs = [(L.FiImage * B)() for _ in range(2)]
+    dst = [ctx.malloc(cap) for _ in range(PIPE_DEPTH)]
+    arrs = [(L.FiImage * B)() for _ in range(PIPE_DEPTH)]
 
     def fill(arr, b, slot):
         o = 0
@@ -592,21 +604,24 @@ def run_cfg4(args, rank, world, local_rank, comm):
 
     def step():
         recs = []
-        for k, b in enumerate(batches):
-            fill(arrs[k % 2], b, k % 2)
-            L.check(ctx.submit_device(arrs[k % 2], len(b)))
-            if k > 0:
-                L.check(ctx.wait(1))
-                pb, pa = batches[k - 1], arrs[(k - 1) % 2]
-                bad[0] += sum(1 for j in range(len(pb)) if pa[j].status != 0)
-                recs += [(pb[j], pa[j].status, pa[j].out_w, pa[j].out_h, pa[j].crop_x, pa[j].crop_y,
-                          pa[j].crop_w, pa[j].crop_h) for j in range(len(pb))]
-        L.check(ctx.wait(0))
-        if batches:
-            pb, pa = batches[-1], arrs[(len(batches) - 1) % 2]
+        def on_done(k, pa):
+            pb = batches[k]
             bad[0] += sum(1 for j in range(len(pb)) if pa[j].status != 0)
-            recs += [(pb[j], pa[j].status, pa[j].out_w, pa[j].out_h, pa[j].crop_x, pa[j].crop_y,
-                      pa[j].crop_w, pa[j].crop_h) for j in range(len(pb))]
+            recs.extend((pb[j], pa[j].status, pa[j].out_w, pa[j].out_h, pa[j].crop_x, pa[j].crop_y,
+                         pa[j].crop_w, pa[j].crop_h) for j in range(len(pb)))
+
+        D = PIPE_DEPTH
+        done = 0
+        for k, b in enumerate(batches):
+            fill(arrs[k % D], b, k % D)
+            L.check(ctx.submit_device(arrs[k % D], len(b)))
+            if k - done >= D - 1:
+                L.check(ctx.wait(D - 1))
+                on_done(done, arrs[done % D])
+                done += 1
+        L.check(ctx.wait(0))
+        for k in range(done, len(batches)):
+            on_done(k, arrs[k % D])
         if world > 1:
             # uneven shards: pad to the longest so every rank sends the same count
             n_max = max(comm.allgather_obj(len(recs)))
@@ -639,8 +654,8 @@ def run_cfg4(args, rank, world, local_rank, comm):
     if batches and not args.no_verify:
         from oracle.verify import verify_mixed_batch  # the checker (test infrastructure)
 
-        lb, la = batches[-1], arrs[(len(batches) - 1) % 2]
-        slot = (len(batches) - 1) % 2
+        lb, la = batches[-1], arrs[(len(batches) - 1) % PIPE_DEPTH]
+        slot = (len(batches) - 1) % PIPE_DEPTH
         views, vops, seeds, offs, o = [], [], [], [], 0
         for i in lb:
             W, H, k = items[i]

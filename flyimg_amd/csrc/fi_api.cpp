@@ -56,6 +56,10 @@ int launch_sc_fd(hipStream_t s, const ScDesc *descs, int n, int lds, const int32
                  const uint16_t *skinsat);
 int launch_sc_ft(hipStream_t s, int ks, const ScDesc *descs, const int32_t *tiles, int ntiles, int lds,
                  const int32_t *ai, const ScParamsDev &P, const uint16_t *skinsat);
+int launch_sc_hx(hipStream_t s, int ks, int nch, const ScDesc *descs, const int32_t *tiles, int ntiles,
+                 const int32_t *ai);
+int launch_sc_vx(hipStream_t s, int kv, int nch, const ScDesc *descs, const int32_t *tiles, int ntiles,
+                 const int32_t *ai, const ScParamsDev &P, const uint16_t *skinsat);
 int launch_sc_skinsat(hipStream_t s, uint16_t *table, const ScParamsDev &P);
 int jpeg_info(const uint8_t *data, size_t len, int *w, int *h, int *c);
 int jpeg_decode_batch(hipStream_t st, const uint8_t *const *data, const size_t *len, int n, uint8_t *const *dst,
@@ -193,7 +197,10 @@ struct Slot {
   void *hpin = nullptr;
   size_t hpin_cap = 0;
 };
-constexpr int kSlots = 2;
+// three batches in flight: with the smartcrop stage beside the next resample,
+// batch k's stage finishes after batch k+1's resample, and batch k+2's must
+// already be queued behind it (two slots serialise the host on batch k)
+constexpr int kSlots = 3;
 // hash of the planner's cache keys (tuples / pairs of ints, doubles' bits and
 // pointers): the per-image lookups of a mixed batch run in O(1) (a std::map
 // over thousands of tables cost ~1 us per lookup in cache misses)
@@ -286,6 +293,13 @@ struct fi_ctx {
   // k_sc_ft (chunk tiles) for the images k_sc_fd cannot stream (analysed widths
   // over 224 px, LDS): FI_SC_FT=0 never, 1 there (default), 2 in place of k_sc_fd too
   int sc_ft = 1;
+  // k_sc_hx + k_sc_vx (no LDS, <= 64 VGPRs; gray sources, two-k-step
+  // vertical windows): FI_SC_CX=0 never; 1 (default) for the images neither
+  // k_sc_fd nor k_sc_ft takes (cfg5's gray 400 -> 111, which otherwise runs
+  // k_sc_hmfma + k_sc_vmaps); 2 for every image it fits; 3 the same, and a
+  // batch whose smartcrop images all take them runs the stage on ap_stream
+  // beside the next batch's resample (measured a loss on cfg2: DESIGN.md §3.2)
+  int sc_cx = 1;
   bool sc_mf = true;        // FI_SC_MFMA=0: k_sc_score2 (f64 VALU fast pass) instead of k_sc_score3
   DevBuf skinsat;           // k_sc_skinsat table: 2^24 colours x u16, built for skinsat_key's parameters
   DevBuf jpeg[3];           // GPU JPEG decode: upload (compressed data + tables), -, coefficients + planes
@@ -314,6 +328,7 @@ struct fi_ctx {
     int32_t hb = 0, hk = 0, hkT = 0, vb = 0, vk = 0;
     int32_t hmB = 0, hmC = 0, hmS0 = 0, vqA = 0, vqC = 0, vqK0 = 0;
     int32_t ftB = -1;
+    int32_t cxA = -1, cxK0 = -1;
   };
   HashMap<const AxisTable *, DevAxis> axis_at;
   HashMap<const AxisTable *, int32_t> axis_wd_at;  // f64 weights (RGBA path) in heap_d
@@ -851,10 +866,19 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
             while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
             t.vqA = E.oi();
             E.ai.insert(E.ai.end(), P.vqA.begin(), P.vqA.end());
-            t.vqC = E.oi();
-            E.ai.insert(E.ai.end(), P.vqC.begin(), P.vqC.end());
             t.vqK0 = E.oi();
             E.ai.insert(E.ai.end(), P.vqK0.begin(), P.vqK0.end());
+          }
+          if (P.vq_ok || P.cx_ok) {
+            t.vqC = E.oi();
+            E.ai.insert(E.ai.end(), P.vqC.begin(), P.vqC.end());
+          }
+          if (P.cx_ok) {
+            while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
+            t.cxA = E.oi();
+            E.ai.insert(E.ai.end(), P.cxA.begin(), P.cxA.end());
+            t.cxK0 = E.oi();
+            E.ai.insert(E.ai.end(), P.cxK0.begin(), P.cxK0.end());
           }
           if (!P.ftB.empty()) {
             while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
@@ -1001,6 +1025,19 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     d.vqA = T.vqA;
     d.vqC = T.vqC;
     d.vqK0 = T.vqK0;
+    // k_sc_hx + k_sc_vx: their tables, the horizontal ones at <= 2 k-steps, rows
+    // readable to the 16-B rounded row bytes (3 or 1 channels; the source's own
+    // alignment is checked at launch)
+    const int rowb = it.C == 3 ? fd_rp(it.W) : (it.W + 15) / 16 * 16;
+    d.cx = prep && c->sc_cx > 0 && P.cx_ok && T.cxA >= 0 && P.fx == 1 && P.fy == 1 &&
+                   (it.C == 3 || it.C == 1) && P.hm_ks <= 2 && it.stride % 16 == 0 &&
+                   (it.padded || it.W * it.C == rowb)
+               ? 1
+               : 0;
+    d.cx_kv = P.cx_kv;
+    d.cx_tp = P.cx_tp;
+    d.cxA = T.cxA;
+    d.cxK0 = T.cxK0;
     d.prescale = P.prescale;
     d.exact_all = o.exact_all || !fast_ok;
     // workspace (offsets; converted to pointers after allocation)
@@ -1011,6 +1048,7 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     if (P.thumb && P.need_h && !d.fz)  // generic kernels: pitch aw*3; k_sc_hmfma: pitch apitch
       d.hbuf = take((size_t)(prep ? (P.aw * 3 + 15) / 16 * 16 : P.aw * 3) * std::max(P.hrows, 1));
     if (P.thumb && (!prep || want_pre)) d.pre = take((size_t)P.aw * P.ah * 3);
+    if (d.cx) d.tbuf = take((size_t)P.hm_nb * it.C * 16 * P.cx_tp);
     d.maps = (uint32_t *)take((size_t)P.aw * P.ah * 4);
     d.crop0 = q.crop0;
     d.ncrops = q.ncrops;
@@ -1063,6 +1101,10 @@ struct ScLaunches {
   int nfz = 0, fz_lds = 0, nfd = 0, fd_lds = 0;
   size_t ft_off = 0, ftt_off[2] = {0, 0};  // k_sc_ft: descriptors, tile lists per k-step count
   int nft = 0, ft_tiles[2] = {0, 0}, ft_lds = 0;
+  // k_sc_hx / k_sc_vx: descriptors, tile lists per variant v = 2 (k-steps - 1) + (channels == 3)
+  size_t cx_off = 0, hxt_off[4] = {0, 0, 0, 0}, vxt_off[4] = {0, 0, 0, 0};
+  int ncx = 0, hx_tiles[4] = {0, 0, 0, 0}, vx_tiles[4] = {0, 0, 0, 0};
+  int nok = 0;  // descriptors planned OK (ncx == nok: the whole stage is co-resident work)
   int nvq = 0, vq_chunks = 0, vq_lds = 0;
   size_t sl_off = 0, sg_off = 0;   // k_sc_score2 with maps in LDS / global
   int nsl = 0, nsg = 0, sl_px = 0;
@@ -1073,18 +1115,24 @@ struct ScLaunches {
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> hm, sl, sg, vq, vm, fz, fd, s3, ft;
+  std::vector<ScDesc> hm, sl, sg, vq, vm, fz, fd, s3, ft, cx;
   std::vector<int> ft_chunks;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
+    X->nok++;
     const ScDesc &d = SL.descs[k];
     const ScPlan &P = *SL.plans[k];
     if (d.red) sred.push_back((int)k);
     const bool aligned = ((uintptr_t)d.img & 15) == 0;
     const bool fd_ok = d.fz && d.fd && aligned;
-    // k_sc_fd where it streams the image (cfg2: 0.353 vs k_sc_ft's 0.363 ms per
-    // 1024 images), k_sc_ft where it does not (FI_SC_FT=2: k_sc_ft first)
-    if (d.ft && aligned && (!fd_ok || c->sc_ft == 2)) {
+    // k_sc_fd where it streams the image (cfg2: 0.353 vs k_sc_ft's 0.363 and
+    // k_sc_hx + k_sc_vx's 0.44 ms per 1024 images), k_sc_ft where it does not
+    // (FI_SC_FT=2: k_sc_ft first), k_sc_hx + k_sc_vx where neither fits
+    // (FI_SC_CX=2, 3: first)
+    const bool ft_ok = d.ft && aligned;
+    if (d.cx && aligned && (c->sc_cx >= 2 || !(fd_ok || ft_ok))) {
+      cx.push_back(d);
+    } else if (ft_ok && (!fd_ok || c->sc_ft == 2)) {
       ft.push_back(d);
       ft_chunks.push_back(P.vq_chunks);
       X->ft_lds = std::max(X->ft_lds, P.ft_lds);
@@ -1166,6 +1214,37 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
     X->ftt_off[ks - 1] = B.addv(tl);
     X->ft_tiles[ks - 1] = (int)(tl.size() / 2);
   }
+  // k_sc_hx tiles (descriptor, first of 4 column blocks), k_sc_vx tiles
+  // (descriptor, chunk) four to a workgroup, one list per variant
+  X->cx_off = B.addv(cx);
+  X->ncx = (int)cx.size();
+  for (int v = 0; v < 4; v++) {
+    const int ks = v / 2 + 1, nch = (v & 1) ? 3 : 1;
+    std::vector<int32_t> ht, vt;
+    for (size_t k = 0; k < cx.size(); k++) {
+      const ScDesc &d = cx[k];
+      if (d.C != nch) continue;
+      if (d.hm_ks == ks)
+        for (int b = 0; b < d.hm_nb; b += 4) {
+          ht.push_back((int32_t)k);
+          ht.push_back(b);
+        }
+      if (d.cx_kv == ks)
+        for (int ch = 0; ch < (d.ah + kVqRows - 1) / kVqRows; ch++) {
+          vt.push_back((int32_t)k);
+          vt.push_back(ch);
+        }
+    }
+    while (vt.size() % 8) {
+      vt.push_back(-1);
+      vt.push_back(0);
+    }
+    X->hxt_off[v] = B.addv(ht);
+    X->hx_tiles[v] = (int)(ht.size() / 2);
+    X->vxt_off[v] = B.addv(vt);
+    X->vx_tiles[v] = (int)(vt.size() / 2);
+  }
+  c->stats["sc_path_cx"].launches += X->ncx;
   c->stats["sc_path_ft"].launches += X->nft;  // images per smartcrop prescale kernel (fi_kernel_stats)
   c->stats["sc_path_fd"].launches += X->nfd;
   c->stats["sc_path_fz"].launches += X->nfz;
@@ -1188,11 +1267,13 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
   // on the stream that reads it, so batches queued before a parameter change
   // have read the old table first
   const uint16_t *skinsat = nullptr;
-  if (X.nfz > 0 || X.nfd > 0 || X.nft > 0) {
+  if (X.nfz > 0 || X.nfd > 0 || X.nft > 0 || X.ncx > 0) {
     const std::string key(reinterpret_cast<const char *>(&PD), offsetof(ScParamsDev, pad));
     if (!c->skinsat.p || c->skinsat_key != key) {
       const int rc = ensure(c, &c->skinsat, (size_t)2 << 24);
       if (rc != FI_OK) return rc;
+      // readers of the old table may still run on the other stream
+      if (c->ap_pending && st == c->stream && order_after_apply(c) != FI_OK) return FI_EDEVICE;
       launch_sc_skinsat(st, (uint16_t *)c->skinsat.p, PD);
       c->skinsat_key = key;
     }
@@ -1213,6 +1294,18 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
                      X.ft_lds, ai, PD, skinsat) != 0)
       return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d/%d/%d)", X.hm_lds, X.vq_lds,
                      X.fz_lds, X.fd_lds, X.ft_lds);
+    for (int v = 0; v < 4; v++) {
+      const ScDesc *cd = (const ScDesc *)(ab + X.cx_off);
+      if (launch_sc_hx(st, v / 2 + 1, (v & 1) ? 3 : 1, cd, (const int32_t *)(ab + X.hxt_off[v]), X.hx_tiles[v],
+                       ai) != 0)
+        return set_err(FI_EDEVICE, "k_sc_hx launch rejected");
+    }
+    for (int v = 0; v < 4; v++) {
+      const ScDesc *cd = (const ScDesc *)(ab + X.cx_off);
+      if (launch_sc_vx(st, v / 2 + 1, (v & 1) ? 3 : 1, cd, (const int32_t *)(ab + X.vxt_off[v]), X.vx_tiles[v],
+                       ai, PD, skinsat) != 0)
+        return set_err(FI_EDEVICE, "k_sc_vx launch rejected");
+    }
     if (X.hp.tiles)
       hipLaunchKernelGGL(k_sc_hpass, dim3(X.hp.tiles), dim3(256), 0, st, desc(X.hp), pre(X.hp), X.hp.n, ai);
     if (X.vp.tiles)
@@ -1663,6 +1756,7 @@ static void resolve_workspace(Exec &E, BatchPlan &Bp, uint8_t *wb) {
   for (ScDesc &d : Bp.SL.descs) {
     fix_ptr(d.red, wb);
     fix_ptr(d.hbuf, wb);
+    fix_ptr(d.tbuf, wb);
     fix_ptr(d.pre, wb);
     fix_ptr(d.maps, wb);
   }
@@ -2481,19 +2575,31 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
     (void)launch_mono(c->stream, (const MonoDesc *)(ab + K.mono_off), (int)Bp.mono.size(), ad + K.mono_wts);
   }
   HIP_TRY(hipGetLastError());
-  if (c->sc_stream != c->stream) {  // (one stream today: stream order is the dependency)
+  // a smartcrop stage made only of co-resident kernels (k_sc_hx / k_sc_vx, the
+  // score, the apply) runs on ap_stream behind this batch's resample, beside
+  // the next batch's
+  const bool beside = c->sc_cx == 3 && c->apply_overlap && c->ap_stream && K.SX.ncx > 0 && K.SX.ncx == K.SX.nok;
+  hipStream_t scs = c->sc_stream;
+  if (c->sc_stream != c->stream || beside) {
+    if (beside) scs = c->ap_stream;
     if (!S.rs_done) HIP_TRY(hipEventCreateWithFlags(&S.rs_done, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(S.rs_done, c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->sc_stream, S.rs_done, 0));
+    HIP_TRY(hipStreamWaitEvent(scs, S.rs_done, 0));
   }
   if (K.SX.nsl + K.SX.nsg + K.SX.ns3 > 0) {
-    const int rc = enqueue_sc(c, c->sc_stream, ab, K.SX, ai, ad, (CropScore *)(wb + Bp.scores_off),
+    const int rc = enqueue_sc(c, scs, ab, K.SX, ai, ad, (CropScore *)(wb + Bp.scores_off),
                               (ScResult *)(wb + Bp.results_off), PD);
     if (rc) return rc;
+    if (beside) {
+      S.tail = scs;
+      tb.sb = scs;
+    }
     if (!Bp.apply.empty()) {
-      hipStream_t as = c->sc_stream;
+      hipStream_t as = scs;
       int pw = 0;
-      if (c->apply_overlap && c->ap_stream) {
+      if (beside) {
+        pw = c->n_cu;
+      } else if (c->apply_overlap && c->ap_stream) {
         if (!S.sc_done) HIP_TRY(hipEventCreateWithFlags(&S.sc_done, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(S.sc_done, c->sc_stream));
         HIP_TRY(hipStreamWaitEvent(c->ap_stream, S.sc_done, 0));
@@ -2509,6 +2615,7 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
       }
       if (as == c->ap_stream) {
         if (!c->ap_tail) HIP_TRY(hipEventCreateWithFlags(&c->ap_tail, hipEventDisableTiming));
+        // (as in the overlapped apply; the smartcrop kernels beside it write only the slot's workspace)
         HIP_TRY(hipEventRecord(c->ap_tail, as));
         c->ap_pending = true;
         // the bytes this apply writes (a crop is at most the resized image)
@@ -2519,6 +2626,10 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
           S.ap_hi = std::max(S.ap_hi, (uintptr_t)a.dst + (uintptr_t)a.W * a.H * a.C);
         }
       }
+    } else if (beside) {
+      if (!c->ap_tail) HIP_TRY(hipEventCreateWithFlags(&c->ap_tail, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(c->ap_tail, scs));
+      c->ap_pending = true;
     }
     HIP_TRY(hipGetLastError());
   }
@@ -2817,6 +2928,7 @@ static int run_smartcrop(fi_ctx *c, const uint8_t *d_img, int W, int H, int64_t 
   ScDesc &d = SL.descs[0];
   fix_ptr(d.red, wb);
   fix_ptr(d.hbuf, wb);
+  fix_ptr(d.tbuf, wb);
   fix_ptr(d.pre, wb);
   fix_ptr(d.maps, wb);
   Blob &B = E.blob;
@@ -3217,6 +3329,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';
   if (const char *e = getenv("FI_SC_FT")) c->sc_ft = atoi(e);
+  if (const char *e = getenv("FI_SC_CX")) c->sc_cx = atoi(e);
   if (const char *e = getenv("FI_SC_MFMA")) c->sc_mf = e[0] == '1';
   if (const char *e = getenv("FI_VR_MAX_CLASSES")) c->vr_max_classes = atoi(e);
   if (const char *e = getenv("FI_VM_LPT")) c->vm_lpt = e[0] == '1';
@@ -3231,9 +3344,13 @@ int fi_create(fi_ctx **out, int32_t device) {
   }
   c->sc_stream = c->stream;
   if (const char *e = getenv("FI_APPLY_OVERLAP")) c->apply_overlap = e[0] == '1';
+  // ap_stream at the higher priority: its score / apply take the CUs the
+  // resample frees before the next resample's workgroups do
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->ap_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->ap_stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipStreamCreateWithFlags(&c->gx_stream, hipStreamNonBlocking) != hipSuccess) {
     fi_destroy(c);
     return set_err(FI_EDEVICE, "hipStreamCreate failed");

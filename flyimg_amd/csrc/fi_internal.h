@@ -112,6 +112,11 @@ struct ScDesc {
   int32_t ftB;             // arena offset (int32 units, 16-B aligned) of k_sc_ft's B fragments (ScPlan::ftB)
   int32_t ft_rows;         // k_sc_ft's H-stage window rows in LDS (ScPlan::ft_rows)
   int32_t vqA, vqC, vqK0;  // arena offsets (int32 units; vqA 16-B aligned)
+  int32_t cx;              // 1: k_sc_hx + k_sc_vx take it (tables below, tbuf)
+  int32_t cx_kv, cx_tp;    // their vertical k-steps, transposed H-stage row pitch (ScPlan::cx_*)
+  int32_t cxA, cxK0;       // arena offsets (int32 units; cxA 16-B aligned)
+  int32_t cx_pad;
+  uint8_t *tbuf;       // k_sc_hx's transposed H-stage: [hm_nb][C][16][cx_tp] bytes
   uint8_t *red;        // reduce scratch rw*rh*3
   uint8_t *hbuf;       // H-pass scratch aw*hrows*3
   uint8_t *pre;        // prescaled image aw*ah*3

@@ -1122,6 +1122,12 @@ static void plan_sc_vq(ScPlan *p) {
   p->vq_ok = false;
   if (!(p->thumb && p->need_h && p->need_v)) return;
   const int ah = p->ah, chunks = (ah + kVqRows - 1) / kVqRows;
+  p->vqC.assign(ah, 0);  // (k_sc_vx's bias too, whether or not k_sc_vq's windows fit)
+  for (int y = 0; y < ah; y++) {
+    int64_t sum = 0;
+    for (int j = 0; j < p->vb[2 * y + 1]; j++) sum += p->vk[(size_t)y * p->ksv + j];
+    p->vqC[y] = (int32_t)((1 << 21) + 128 * sum);
+  }
   p->vqK0.assign(chunks, 0);
   p->vqA.assign((size_t)chunks * 3 * 256, 0);
   for (int c = 0; c < chunks; c++) {
@@ -1141,12 +1147,6 @@ static void plan_sc_vq(ScPlan *p) {
         for (int q = 0; q < 3; q++)
           reinterpret_cast<uint8_t *>(&p->vqA[((size_t)c * 3 + q) * 256])[l * 16 + j] = (uint8_t)(int8_t)limb[q];
       }
-  }
-  p->vqC.assign(ah, 0);
-  for (int y = 0; y < ah; y++) {
-    int64_t sum = 0;
-    for (int j = 0; j < p->vb[2 * y + 1]; j++) sum += p->vk[(size_t)y * p->ksv + j];
-    p->vqC[y] = (int32_t)((1 << 21) + 128 * sum);
   }
   const int apitch = (p->aw * 3 + 15) / 16 * 16;
   p->vq_lds = 64 * apitch + 16 * apitch + 16 * ((p->aw + 3) / 4 * 4);
@@ -1217,6 +1217,53 @@ static void plan_sc_ft(ScPlan *p) {
   p->ft_lds = rows * apitch + 16 * apitch + 16 * lpitch;
 }
 
+// k_sc_hx / k_sc_vx tables (fi_plan.h ScPlan::cx_*): per chunk of kVqRows
+// analysed rows, the 16 prescaled rows [pa, pa + 16) over the H-stage rows
+// [K0, K0 + 64 kv), K0 = the chunk's first tap rounded down to a multiple of 4,
+// coefficients as three signed-byte limbs in A-fragment order (row pa + (l & 15),
+// K slot mfma_i8_k(l, j) of k-step t).  Needs k_sc_hmfma's horizontal tables.
+static void plan_sc_cx(ScPlan *p) {
+  p->cx_ok = false;
+  p->cxA.clear();
+  p->cxK0.clear();
+  if (!p->hm_ok || !(p->thumb && p->need_h && p->need_v) || (int)p->vqC.size() != p->ah) return;
+  const int ah = p->ah, chunks = (ah + kVqRows - 1) / kVqRows;
+  int kv = 1, tp = p->hrows;
+  p->cxK0.assign(chunks, 0);
+  for (int c = 0; c < chunks; c++) {
+    const int y0 = kVqRows * c, pa = std::max(0, y0 - 1), pe = std::min(ah, pa + 16);
+    int lo = 1 << 30, hi = 0;
+    for (int y = pa; y < pe; y++) {
+      lo = std::min(lo, p->vb[2 * y]);
+      hi = std::max(hi, p->vb[2 * y] + p->vb[2 * y + 1]);
+    }
+    p->cxK0[c] = lo & ~3;
+    kv = std::max(kv, (hi - p->cxK0[c] + 63) / 64);
+  }
+  if (kv > 2) return;
+  for (int c = 0; c < chunks; c++) tp = std::max(tp, p->cxK0[c] + 64 * kv);
+  p->cx_tp = (tp + 15) / 16 * 16 + 16;  // + one row block: the V pass's 16-B reads straddle two
+  p->cx_kv = kv;
+  p->cxA.assign((size_t)chunks * kv * 3 * 256, 0);
+  for (int c = 0; c < chunks; c++) {
+    const int y0 = kVqRows * c, pa = std::max(0, y0 - 1), pe = std::min(ah, pa + 16);
+    for (int t = 0; t < kv; t++)
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int y = pa + (l & 15), k = p->cxK0[c] + 64 * t + mfma_i8_k(l, j);
+          int32_t w = 0;
+          if (y < pe && k >= p->vb[2 * y] && k < p->vb[2 * y] + p->vb[2 * y + 1])
+            w = p->vk[(size_t)y * p->ksv + (k - p->vb[2 * y])];
+          int32_t limb[3];
+          limbs3(w, limb);
+          for (int q = 0; q < 3; q++)
+            reinterpret_cast<uint8_t *>(&p->cxA[(((size_t)c * kv + t) * 3 + q) * 256])[l * 16 + j] =
+                (uint8_t)(int8_t)limb[q];
+        }
+  }
+  p->cx_ok = true;
+}
+
 void plan_sc_prep(ScPlan *p) {
   p->prep_ok = false;
   p->hkT.clear();
@@ -1267,7 +1314,10 @@ void plan_sc_prep(ScPlan *p) {
       p->fz_ok = true;
     }
   }
-  if (!reduced) plan_sc_ft(p);
+  if (!reduced) {
+    plan_sc_ft(p);
+    plan_sc_cx(p);
+  }
 }
 
 static double thirds(double x) {

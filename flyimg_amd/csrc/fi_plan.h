@@ -220,6 +220,16 @@ struct ScPlan {
   // tile of kFtChunks chunks needs (16-row blocks), ft_lds its LDS
   std::vector<int32_t> ftB;
   int ft_rows = 0, ft_lds = 0;
+  // k_sc_hx + k_sc_vx (co-resident with the next batch's resample: no LDS,
+  // <= 64 VGPRs): the H-stage goes to HBM as 256-B tiles [block][channel][row
+  // block][16 columns][16 rows] of p - 128 bytes, cx_tp / 16 row blocks, of
+  // which k_sc_hx writes all but the last (source rows clamped to the last;
+  // the last block is read only as zero-weight straddle).  Per chunk the vertical window
+  // starts at cxK0 (vqK0 rounded down to 4: dword loads) and spans cx_kv
+  // 64-row k-steps; cxA = [chunk][kv][3 limbs] fragments (256 int32 each).
+  bool cx_ok = false;
+  int cx_kv = 0, cx_tp = 0;
+  std::vector<int32_t> cxA, cxK0;
   bool fz_ok = false;  // k_sc_fz (fused per-image prescale + maps)
   int fz_lds = 0;
   std::vector<int32_t> vqA;   // [chunk][3 limbs] fragments of 64 lanes x 16 B (256 int32)

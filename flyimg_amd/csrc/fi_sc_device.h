@@ -90,13 +90,13 @@ struct ScFast {
   int32_t slo, shi, tlo, thi;  // brightness bounds (inclusive) on the integer luma
   int32_t skin_est, sat_est;   // the estimates apply to these parameters
 };
-__device__ __forceinline__ int32_t sc_lbound(double a) {  // L >= a <=> L >= ceil(a)
+__host__ __device__ __forceinline__ int32_t sc_lbound(double a) {  // L >= a <=> L >= ceil(a)
   return a <= 0 ? 0 : a > 256 ? 256 : (int32_t)ceil(a);
 }
-__device__ __forceinline__ int32_t sc_ubound(double b) {  // L <= b <=> L <= floor(b)
+__host__ __device__ __forceinline__ int32_t sc_ubound(double b) {  // L <= b <=> L <= floor(b)
   return b < 0 ? -1 : b >= 255 ? 255 : (int32_t)floor(b);
 }
-__device__ __forceinline__ ScFast sc_fast_params(const ScParamsDev &P) {
+__host__ __device__ __forceinline__ ScFast sc_fast_params(const ScParamsDev &P) {
   ScFast F;
   F.c0 = (float)P.skin_color[0];
   F.c1 = (float)P.skin_color[1];

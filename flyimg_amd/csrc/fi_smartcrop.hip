@@ -1437,6 +1437,267 @@ __global__ __launch_bounds__(kFtThreads, KS == 1 ? 4 : 2) void k_sc_ft(const ScD
   }
 }
 
+// ---- k_sc_hx + k_sc_vx: the same prescale + maps (same integer arithmetic,
+// bit-identical maps) shaped to run BESIDE the next batch's k_rs_vr: no LDS,
+// <= 64 VGPRs (launch_bounds(256, 8)), so their waves take the one wave slot
+// per SIMD that k_rs_vr's workgroup leaves free (as k_crop_apply3p does),
+// instead of a serial stage between two resamples.
+//  * k_sc_hx: one wave per (image, 16-column block b), looping over 16-row
+//    blocks of the H stage (k_sc_hmfma's B fragments stay in registers).  A
+//    lane's A operand is 16 consecutive source pixels (48 contiguous bytes);
+//    limbs fold through the accumulator as in k_sc_ft.  The MFMA result lane
+//    (g, n) holds rows 4g .. 4g + 3 of column n: one dword store per channel
+//    into the TRANSPOSED H stage tbuf[b][ch][n][row] (p - 128 bytes).
+//  * k_sc_vx: one wave per (image, chunk of kVqRows analysed rows): per
+//    column block, the chunk's 16 prescaled rows = one MFMA block whose B
+//    operand is 16 contiguous bytes of a tbuf column (rows K0 + 16 g ..); the
+//    lane then holds R, G, B of 4 vertically adjacent pixels.  Luma is packed
+//    4 bytes a dword; the Laplacian's row neighbours come from lanes -+16
+//    (ds_bpermute), its column neighbours by DPP within the 16-lane row, the
+//    previous / next block's edge column through the rotate's `old` operand, so
+//    a block's maps are written one block late.  Skin / saturation: k_sc_fd's
+//    estimator, k_sc_skinsat's table for what it leaves open.
+// The host runs both on the apply stream behind the batch's resample, so they
+// overlap the next batch's k_rs_vr (fi_api.cpp launch_batch).
+template <int KS, int NCH>
+__global__ __launch_bounds__(256, 8) void k_sc_hx(const ScDesc *__restrict__ descs, const int32_t *__restrict__ tiles,
+                                                  const int32_t *__restrict__ ai) {
+  typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int di = tiles[2 * blockIdx.x];
+  if (di < 0) return;
+  const ScDesc &D = descs[di];
+  const int b = tiles[2 * blockIdx.x + 1] + wave;
+  if (b >= D.hm_nb) return;
+  const int g = lane >> 4, r = lane & 15;
+  const int aw = D.aw, hrows = D.hrows, yoff = D.ybox_first, tp = D.cx_tp;
+  const int rp = NCH == 3 ? fd_rp(D.W) : (D.W + 15) & ~15;  // readable bytes of a row
+  const int s0 = ai[D.hmS0 + b];
+  const i32x4 *hmB = reinterpret_cast<const i32x4 *>(ai + D.hmB) + (size_t)b * KS * 3 * 64 + lane;
+  // B fragments in registers, except at two k-steps of RGB (64 VGPRs: from L1 per item)
+  constexpr bool kKeepB = !(KS == 2 && NCH == 3);
+  i32x4 Bf[kKeepB ? KS : 1][3];
+  if (kKeepB)
+#pragma unroll
+    for (int t = 0; t < KS; t++)
+#pragma unroll
+      for (int q = 0; q < 3; q++) Bf[kKeepB ? t : 0][q] = hmB[(t * 3 + q) * 64];
+  auto bfrag = [&](int t, int q) {
+    const i32x4 *hb = hmB;
+    if (!kKeepB) asm volatile("" : "+v"(hb));  // re-read per use: not hoisted out of the row loop
+    return kKeepB ? Bf[kKeepB ? t : 0][q] : hb[(t * 3 + q) * 64];
+  };
+  const int x = 16 * b + r;
+  const int32_t cxp = x < aw ? ai[D.hmC + x] - (1 << 29) : 0;
+  constexpr int NQ = NCH == 3 ? 3 : 1;  // 16-B loads per k-step
+  const int64_t sstride = D.stride;
+  // tbuf tiles [b][ch][row block][16 columns][16 rows]: a store instruction
+  // writes one whole 256-B tile (lane (g, n): column n, rows 4g .. 4g + 3)
+  const int nrbt = tp >> 4;
+  uint8_t *tcol = D.tbuf + (int64_t)b * NCH * nrbt * 256 + 16 * r + 4 * g;
+  auto load = [&](int rb, u32x4a (&q)[KS][NQ]) {
+    const int hr = min(16 * rb + r, hrows - 1);
+    const uint8_t *row = D.img + (int64_t)(hr + yoff) * sstride;
+#pragma unroll
+    for (int t = 0; t < KS; t++)
+#pragma unroll
+      for (int i = 0; i < NQ; i++) {
+        const int off = (NCH == 3 ? 3 : 1) * (s0 + 64 * t + 16 * g) + 16 * i;  // 8-B aligned
+        u32x4a v = *reinterpret_cast<const u32x4a *>(row + min(off, rp - 16));
+        if (off > rp - 16) v = off == rp - 8 ? u32x4a{v.z, v.w, 0u, 0u} : u32x4a{0u, 0u, 0u, 0u};
+        q[t][i] = v;
+      }
+  };
+  const int nrb = nrbt - 1;  // (the last tile row block: the V pass's straddle margin, never read as data)
+  constexpr bool kPre = KS * NQ <= 3;  // the next row block's loads in flight (within 64 VGPRs)
+  u32x4a cur[KS][NQ], nxt[KS][NQ];
+  load(0, cur);
+#pragma unroll 1
+  for (int rb = 0; rb < nrb; rb++) {
+    if (!kPre && rb > 0) load(rb, cur);
+    if (kPre && rb + 1 < nrb) load(rb + 1, nxt);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      i32x4 A[KS];
+#pragma unroll
+      for (int t = 0; t < KS; t++) {
+        if (NCH == 3) {
+          const uint32_t d[12] = {cur[t][0].x, cur[t][0].y, cur[t][0].z, cur[t][0].w, cur[t][1].x, cur[t][1].y,
+                                  cur[t][1].z, cur[t][1].w, cur[t][2].x, cur[t][2].y, cur[t][2].z, cur[t][2].w};
+          A[t] = i32x4{(int32_t)fd_ch(ch, d[0], d[1], d[2]), (int32_t)fd_ch(ch, d[3], d[4], d[5]),
+                       (int32_t)fd_ch(ch, d[6], d[7], d[8]), (int32_t)fd_ch(ch, d[9], d[10], d[11])};
+        } else {
+          A[t] = i32x4{(int32_t)(cur[t][0].x ^ 0x80808080u), (int32_t)(cur[t][0].y ^ 0x80808080u),
+                       (int32_t)(cur[t][0].z ^ 0x80808080u), (int32_t)(cur[t][0].w ^ 0x80808080u)};
+        }
+      }
+      // limbs folded through the accumulator (modular int32; k_sc_ft's C')
+      i32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+      for (int t = 0; t < KS; t++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[t], bfrag(t, 2), acc, 0, 0, 0);
+      acc = acc << 8;
+#pragma unroll
+      for (int t = 0; t < KS; t++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[t], bfrag(t, 1), acc, 0, 0, 0);
+      acc = (acc << 8) + i32x4{cxp, cxp, cxp, cxp};
+#pragma unroll
+      for (int t = 0; t < KS; t++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[t], bfrag(t, 0), acc, 0, 0, 0);
+      uint32_t w = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) w |= ((uint32_t)min(max(acc[i] >> 22, -128), 127) & 255u) << (8 * i);
+      *reinterpret_cast<uint32_t *>(tcol + ((int64_t)ch * nrbt + rb) * 256) = w;
+    }
+    if (kPre)
+#pragma unroll
+      for (int t = 0; t < KS; t++)
+#pragma unroll
+        for (int i = 0; i < NQ; i++) cur[t][i] = nxt[t][i];
+  }
+}
+
+__device__ __forceinline__ uint32_t vx_byte(uint32_t v, int i) { return (v >> (8 * i)) & 255u; }
+
+template <int KV, int NCH>
+__global__ __launch_bounds__(256, 8) void k_sc_vx(const ScDesc *__restrict__ descs, const int32_t *__restrict__ tiles,
+                                                  const int32_t *__restrict__ ai, const ScFast F,
+                                                  const uint16_t *__restrict__ skinsat) {
+  typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tix = 4 * blockIdx.x + wave;
+  const int di = tiles[2 * tix], c = tiles[2 * tix + 1];
+  if (di < 0) return;
+  const ScDesc &D = descs[di];
+  const int g = lane >> 4, n = lane & 15;
+  const int aw = D.aw, ah = D.ah, tp = D.cx_tp, nb = D.hm_nb;
+  const int y0 = kVqRows * c, y1 = min(y0 + kVqRows, ah), pa = max(0, y0 - 1);
+  // the chunk's A fragments, read per block (L1 hits): registers are the budget
+  const i32x4 *af = reinterpret_cast<const i32x4 *>(ai + D.cxA) + (size_t)c * KV * 3 * 64 + lane;
+  int32_t cy[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) cy[i] = ai[D.vqC + min(pa + 4 * g + i, ah - 1)];
+  // the window's rows K0 + 64 t + 16 g .. + 15 of column n straddle row blocks
+  // rb0 + 4 t + g and the next at dword offset m = (K0 & 15) / 4 (uniform)
+  const int K0 = ai[D.cxK0 + c], nrbt = tp >> 4, m4 = (K0 & 15) >> 2;
+  const uint8_t *tb = D.tbuf + ((int64_t)(K0 >> 4) + g) * 256 + 16 * n;
+  const bool edges = aw >= 3 && ah >= 3;
+  // block b's prescaled bytes of the lane's 4 rows, one dword per channel
+  auto vpass = [&](int b, uint32_t (&rgb)[3]) {
+    const i32x4 *afb = af;
+    asm volatile("" : "+v"(afb));  // re-read per block: not hoisted into 12-24 live VGPRs
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      const uint8_t *col = tb + (int64_t)(b * NCH + ch) * nrbt * 256;
+      i32x4 B[KV];
+#pragma unroll
+      for (int t = 0; t < KV; t++) {
+        const i32x4 lo = *reinterpret_cast<const i32x4 *>(col + 1024 * t);
+        if (m4 == 0) {
+          B[t] = lo;
+        } else {
+          const i32x4 hi = *reinterpret_cast<const i32x4 *>(col + 1024 * t + 256);
+          B[t] = m4 == 1 ? i32x4{lo.y, lo.z, lo.w, hi.x} : m4 == 2 ? i32x4{lo.z, lo.w, hi.x, hi.y}
+                                                             : i32x4{lo.w, hi.x, hi.y, hi.z};
+        }
+      }
+      i32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+      for (int t = 0; t < KV; t++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(afb[(t * 3 + 2) * 64], B[t], acc, 0, 0, 0);
+      acc = acc << 8;
+#pragma unroll
+      for (int t = 0; t < KV; t++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(afb[(t * 3 + 1) * 64], B[t], acc, 0, 0, 0);
+      acc = (acc << 8) + i32x4{cy[0], cy[1], cy[2], cy[3]};
+#pragma unroll
+      for (int t = 0; t < KV; t++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(afb[(t * 3 + 0) * 64], B[t], acc, 0, 0, 0);
+      uint32_t w = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) w |= (uint32_t)pil_clip8(acc[i]) << (8 * i);
+      rgb[ch] = w;
+      asm volatile("" ::: "memory");  // one channel's fragments live at a time (64 VGPRs)
+    }
+    if (NCH == 1) rgb[1] = rgb[2] = rgb[0];
+  };
+  auto luma4 = [&](const uint32_t (&rgb)[3]) {
+    uint32_t l4 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) l4 |= sc_luma(vx_byte(rgb[0], i), vx_byte(rgb[1], i), vx_byte(rgb[2], i)) << (8 * i);
+    return l4;
+  };
+  uint32_t cur[3] = {0, 0, 0}, prv[3] = {0, 0, 0};
+  uint32_t Lc = 0, Lp = 0, Lpp = 0;  // luma of blocks b, b - 1, b - 2
+#pragma unroll 1
+  for (int b = 0; b <= nb; b++) {
+    if (b < nb) {
+      vpass(b, cur);
+      Lc = luma4(cur);
+    }
+    if (b > 0) {  // maps of block b - 1
+      const int x = 16 * (b - 1) + n;
+      const uint32_t up = (uint32_t)__shfl((int)Lp, lane - 16, 64), dn = (uint32_t)__shfl((int)Lp, lane + 16, 64);
+      const uint32_t lt = (uint32_t)__builtin_amdgcn_update_dpp(
+          __builtin_amdgcn_update_dpp(0, (int)Lpp, 0x121, 0xF, 0xF, false), (int)Lp, 0x111, 0xF, 0xF, false);
+      const uint32_t rt = (uint32_t)__builtin_amdgcn_update_dpp(
+          __builtin_amdgcn_update_dpp(0, (int)Lc, 0x12F, 0xF, 0xF, false), (int)Lp, 0x101, 0xF, 0xF, false);
+      uint32_t stv[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t rr = vx_byte(prv[0], i), gg = vx_byte(prv[1], i), bb = vx_byte(prv[2], i);
+        if (!sc_skin_sat_est(F, rr, gg, bb, vx_byte(Lp, i), stv[i])) {
+          const uint32_t t = skinsat[sc_colour_key(rr, gg, bb)];
+          stv[i] = (t & 255u) | ((t >> 8) << 16);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int y = pa + 4 * g + i;
+        if (x >= aw || y < y0 || y >= y1) continue;
+        const uint32_t L = vx_byte(Lp, i);
+        uint32_t E = L;
+        if (edges && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
+          const uint32_t u = i > 0 ? vx_byte(Lp, i - 1) : vx_byte(up, 3);
+          const uint32_t d = i < 3 ? vx_byte(Lp, i + 1) : vx_byte(dn, 0);
+          const int v = 4 * (int)L - (int)u - (int)d - (int)vx_byte(lt, i) - (int)vx_byte(rt, i) + 1;
+          E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
+        }
+        D.maps[(int64_t)y * aw + x] = stv[i] | (E << 8);
+        if (D.pre) {  // the prescaled image, when the caller keeps it
+          uint8_t *o = D.pre + ((int64_t)y * aw + x) * 3;
+          o[0] = (uint8_t)vx_byte(prv[0], i);
+          o[1] = (uint8_t)vx_byte(prv[1], i);
+          o[2] = (uint8_t)vx_byte(prv[2], i);
+        }
+      }
+    }
+    Lpp = Lp;
+    Lp = Lc;
+#pragma unroll
+    for (int k = 0; k < 3; k++) prv[k] = cur[k];
+  }
+}
+
+int launch_sc_hx(hipStream_t s, int ks, int nch, const ScDesc *descs, const int32_t *tiles, int ntiles,
+                 const int32_t *ai) {
+  if (ntiles <= 0) return 0;
+  const dim3 grid(ntiles), blk(256);
+  if (ks == 1 && nch == 3) hipLaunchKernelGGL((k_sc_hx<1, 3>), grid, blk, 0, s, descs, tiles, ai);
+  else if (ks == 2 && nch == 3) hipLaunchKernelGGL((k_sc_hx<2, 3>), grid, blk, 0, s, descs, tiles, ai);
+  else if (ks == 1 && nch == 1) hipLaunchKernelGGL((k_sc_hx<1, 1>), grid, blk, 0, s, descs, tiles, ai);
+  else if (ks == 2 && nch == 1) hipLaunchKernelGGL((k_sc_hx<2, 1>), grid, blk, 0, s, descs, tiles, ai);
+  else return -1;
+  return 0;
+}
+int launch_sc_vx(hipStream_t s, int kv, int nch, const ScDesc *descs, const int32_t *tiles, int ntiles,
+                 const int32_t *ai, const ScParamsDev &P, const uint16_t *skinsat) {
+  if (ntiles <= 0) return 0;
+  if (ntiles % 4) return -1;  // four waves (tiles) a workgroup; the host pads
+  const dim3 grid(ntiles / 4), blk(256);
+  const ScFast F = sc_fast_params(P);  // host-side: kernel arguments stay in SGPRs
+  if (kv == 1 && nch == 3) hipLaunchKernelGGL((k_sc_vx<1, 3>), grid, blk, 0, s, descs, tiles, ai, F, skinsat);
+  else if (kv == 2 && nch == 3) hipLaunchKernelGGL((k_sc_vx<2, 3>), grid, blk, 0, s, descs, tiles, ai, F, skinsat);
+  else if (kv == 1 && nch == 1) hipLaunchKernelGGL((k_sc_vx<1, 1>), grid, blk, 0, s, descs, tiles, ai, F, skinsat);
+  else if (kv == 2 && nch == 1) hipLaunchKernelGGL((k_sc_vx<2, 1>), grid, blk, 0, s, descs, tiles, ai, F, skinsat);
+  else return -1;
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 constexpr int kScoreThreads = 1024;
 constexpr int kScoreWaves = kScoreThreads / 64;

@@ -190,8 +190,8 @@ int fi_pixelate_regions_device(fi_ctx *ctx, uint8_t *img, int32_t w, int32_t h, 
 int fi_process_batch(fi_ctx *ctx, fi_image *imgs, int32_t n);
 /* Asynchronous form of fi_process_batch: sources are staged to the device
  * and the batch is queued; outputs and records are final after fi_wait.
- * Two batches can be in flight (the next one's staging and upload overlap the
- * previous one's kernels).  Sources and outputs in pinned memory
+ * Three batches can be in flight (the next one's staging and upload overlap the
+ * earlier ones' kernels).  Sources and outputs in pinned memory
  * (fi_host_alloc) are copied by DMA directly; pageable ones go through the
  * library's pinned staging.  imgs and the buffers must stay valid until
  * fi_wait returns for this batch. */
@@ -205,12 +205,13 @@ int fi_process_batch_device(fi_ctx *ctx, fi_image *imgs, int32_t n);
 /* Asynchronous form of fi_process_batch_device for pipelined serving: plans,
  * uploads and launches the batch, then returns; `imgs` must stay valid until
  * fi_wait().  Batch k+1 is planned and uploaded on the host while batch k runs
- * on the GPU (two pinned staging slots; a third submit waits for the oldest
- * batch).  Streams: the resample, smartcrop and -monochrome / convolution
- * kernels of every batch run on the context's main stream in submission
- * order; the FI_OP_SMARTCROP_APPLY crop of batch k runs on a second stream
- * beside batch k+1's resample (one small workgroup per CU), and batch k's
- * records and outputs are final once that apply is done (fi_wait covers it).
+ * on the GPU (three pinned staging slots; a fourth submit waits for the
+ * oldest batch).  Streams: the resample, smartcrop and -monochrome /
+ * convolution kernels of every batch run on the context's main stream in
+ * submission order; the FI_OP_SMARTCROP_APPLY crop of batch k runs on a
+ * second stream beside batch k+1's resample (one small workgroup per CU; with
+ * FI_SC_CX=3 the whole smartcrop stage of an eligible batch does), and batch
+ * k's records and outputs are final once that apply is done (fi_wait covers it).
  * Ordering across the two streams is kept for the caller: a later batch whose
  * sources overlap an earlier batch's dst, and the device-ordered entry points
  * (fi_pixelate_regions_device, fi_jpeg_decode_device, fi_fill_synthetic) wait

@@ -110,7 +110,7 @@ def test_batch_loop_pipelines_and_gathers_once_without_blocking(tmp_path):
         comm = FileComm(rank, 2, run_id=f"loop_{os.getpid()}", root=str(tmp_path))
         log = []
         ctx = _FakeCtx(gpu_s, log)
-        arrs = [(L.FiImage * nimg)() for _ in range(2)]
+        arrs = [(L.FiImage * nimg)() for _ in range(bench.PIPE_DEPTH)]
         recs = []
 
         def on_done(k, arr):
@@ -131,7 +131,7 @@ def test_batch_loop_pipelines_and_gathers_once_without_blocking(tmp_path):
     log0, got0 = out[0]
     # pipelining: submit k precedes batch k-1's completion and its records
     kinds = [e[0] for e in log0]
-    assert kinds[:2] == ["submit", "submit"] and kinds.count("submit") == steps
+    assert kinds[:bench.PIPE_DEPTH] == ["submit"] * bench.PIPE_DEPTH and kinds.count("submit") == steps
     for k in range(1, steps):
         assert log0.index(("records", k - 1)) > [i for i, e in enumerate(log0) if e[0] == "submit"][k]
     # rank 0's batches are not paced by rank 1's (6 x 50 ms): no per-batch rendezvous

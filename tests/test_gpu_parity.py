@@ -55,18 +55,19 @@ def _context_with(env):
                 os.environ[k] = v
 
 
-_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_SC_FD": "1", "FI_SC_FT": "1"}
+_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_SC_FD": "1", "FI_SC_FT": "1",
+        "FI_SC_CX": "1"}
 PATHS = {
     # default kernels: k_rs_vr (block-major persistent MFMA resample; k_rs_vm
     # where its tables do not fit) / k_rs_hv; k_sc_fd streamed prescale + maps
-    # (k_sc_ft chunk tiles where it cannot stream); k_sc_score3 (exact-integer
-    # MFMA score fast pass)
+    # (k_sc_ft chunk tiles where it cannot stream, k_sc_hx + k_sc_vx where
+    # neither fits); k_sc_score3 (exact-integer MFMA score fast pass)
     "vr": dict(_ENV),
     # the same with k_sc_fz (register-staged source rows, two workgroups per CU)
-    "fz": dict(_ENV, FI_SC_FD="0"),
+    "fz": dict(_ENV, FI_SC_FD="0", FI_SC_CX="0"),
     # the fallbacks: k_rs_vm streaming resample; k_sc_hmfma + k_sc_vq (H-stage rows through HBM);
     # k_sc_score2 (f64 VALU score fast pass)
-    "vm": dict(_ENV, FI_VR_RS="0", FI_DISABLE_SC_FZ="1", FI_SC_MFMA="0"),
+    "vm": dict(_ENV, FI_VR_RS="0", FI_DISABLE_SC_FZ="1", FI_SC_MFMA="0", FI_SC_CX="0"),
     # generic kernels: two-pass resample; per-row prescale/maps kernels
     "generic": dict(_ENV, FI_FORCE_GENERIC="1"),
 }
@@ -83,9 +84,11 @@ def rctx(request):
 
 EXPECTED_PATH = {"vr": "path_vr", "fz": "path_vr", "vm": "path_vm", "generic": "path_generic_v"}
 # smartcrop prescale kernel of each path (images counted by fi_kernel_stats)
-EXPECTED_SC = {"vr": "sc_path_fd", "ft": "sc_path_ft", "fz": "sc_path_fz", "vm": None, "generic": None}
-# the smartcrop tests also run k_sc_ft (chunk-tiled prescale) on every image
-SC_PATHS = dict(PATHS, ft=dict(_ENV, FI_SC_FT="2"))
+EXPECTED_SC = {"vr": "sc_path_fd", "cx": "sc_path_cx", "ft": "sc_path_ft", "fz": "sc_path_fz", "vm": None,
+               "generic": None}
+# the smartcrop tests also run k_sc_ft (chunk tiles) and k_sc_hx + k_sc_vx
+# (H stage through HBM as 256-B tiles, no LDS) on every image
+SC_PATHS = dict(PATHS, ft=dict(_ENV, FI_SC_FT="2", FI_SC_CX="0"), cx=dict(_ENV, FI_SC_CX="2"))
 
 
 @pytest.mark.parametrize("W,H,opts,even_rows", [
@@ -233,12 +236,13 @@ def test_score3_runs_and_agrees_with_score2(ctx, s2ctx, w, h):
 def test_smartcrop_prescale_kernel_of_path(sctx, w, h):
     """fi_smartcrop runs its prescale + maps on the kernel the path names
     (k_sc_fd on the default path for 3-channel images at the staged 16-B
-    rounded pitch, k_sc_ft with FI_SC_FT=2, k_sc_fz with FI_SC_FD=0; no
-    silent fallback), and the result is the oracle's: every crop's scores
+    rounded pitch, k_sc_ft with FI_SC_FT=2, k_sc_hx + k_sc_vx with
+    FI_SC_CX=2, k_sc_fz with FI_SC_FD=0; no silent fallback), and the result
+    is the oracle's: every crop's scores
     bit-exact (exact_all).  The sizes prescale by 1.8-3 (a 14-row chunk's
     window within 64 H-stage rows)."""
     src = synth_rgb(w, h, 0x5C + w)
-    names = ("sc_path_ft", "sc_path_fd", "sc_path_fz")
+    names = ("sc_path_cx", "sc_path_ft", "sc_path_fd", "sc_path_fz")
     before = {k: sctx.stats(k)[1] for k in names}
     r = sctx.smartcrop_ex(src, 100, 100, options=_opts(True), want_images=True)
     ran = {k: sctx.stats(k)[1] - before[k] for k in names}
@@ -575,20 +579,24 @@ def test_cfg4_slice_one_batch(ctx):
     assert len(exact) == len(picks) >= 55 and min(exact) >= MIN_EXACT
 
 
-@pytest.fixture(scope="module", params=["1", "0"], ids=["apply_overlap", "apply_serial"])
+@pytest.fixture(scope="module", params=[("1", "1"), ("0", "1"), ("1", "3")],
+                ids=["apply_overlap", "apply_serial", "smartcrop_beside"])
 def octx(request):
     """FI_APPLY_OVERLAP=1 (default: the crop apply beside the next batch's
-    resample, k_crop_apply3p) and =0 (on the batch stream, k_crop_apply3)."""
-    c = _context_with({"FI_APPLY_OVERLAP": request.param})
+    resample, k_crop_apply3p), =0 (on the batch stream, k_crop_apply3), and
+    FI_SC_CX=3 (the whole smartcrop stage -- k_sc_hx, k_sc_vx, score, apply --
+    on the apply stream beside the next batch's resample)."""
+    c = _context_with({"FI_APPLY_OVERLAP": request.param[0], "FI_SC_CX": request.param[1]})
+    c.beside = request.param[1] == "3"
     yield c
     c.close()
 
 
 def test_pipelined_submit_matches_synchronous(octx):
-    """fi_submit_batch_device x3 + fi_wait (two pinned slots, a third submit
-    waits for the oldest) gives the same pixels and records as the
+    """fi_submit_batch_device x4 + fi_wait (three pinned slots, a fourth
+    submit waits for the oldest) gives the same pixels and records as the
     synchronous fi_process_batch_device, batch by batch -- with the crop apply
-    overlapped and serial."""
+    overlapped and serial, and with the smartcrop stage beside the resample."""
     from flyimg_amd.processor import ImageProcessor, OptionsBag
     from flyimg_amd.runtime import plan as fi_plan
 
@@ -599,7 +607,7 @@ def test_pipelined_submit_matches_synchronous(octx):
     ow, oh, oc = fi_plan(W, H, op)
     cap = ow * oh * oc
     pool = ctx.malloc(stride * H * n)
-    dst = ctx.malloc(cap * n * 4)
+    dst = ctx.malloc(cap * n * 5)
     try:
         for i in range(n):
             ctx.fill_synthetic(pool + i * stride * H, W, H, stride, 900 + i)
@@ -616,10 +624,13 @@ def test_pipelined_submit_matches_synchronous(octx):
         sync = arr_for(0)
         L.check(ctx.process_device(sync, n))
         ref_px = ctx.d2h(dst, cap * n)
-        arrs = [arr_for(b) for b in (1, 2, 3)]
+        arrs = [arr_for(b) for b in (1, 2, 3, 4)]
+        cx0 = ctx.stats("sc_path_cx")[1]
         for a in arrs:
             L.check(ctx.submit_device(a, n))
         L.check(ctx.wait(0))
+        if ctx.beside:  # the co-resident kernels ran (no silent fallback)
+            assert ctx.stats("sc_path_cx")[1] - cx0 == len(arrs) * n
         for b, a in enumerate(arrs, start=1):
             got = ctx.d2h(dst + b * n * cap, cap * n)
             for i in range(n):

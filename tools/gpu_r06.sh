@@ -22,11 +22,12 @@ for s in ${STEP:-tests bench trace}; do
       --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1; rc=$?
     echo "pytest rc=$rc"; tail -4 "$OUT/pytest.log"; [ $rc -eq 0 ] || exit $rc ;;
   bench)
-    for ft in ${FTS:-1 2}; do
-      FI_SC_FT=$ft timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-20} > "$OUT/bench_ft$ft.json" \
-        2> "$OUT/bench_ft$ft.err"; rc=$?
-      [ $rc -eq 0 ] || { echo "bench ft=$ft rc=$rc"; tail -5 "$OUT/bench_ft$ft.err"; exit $rc; }
-      python3 -c "import json;d=json.load(open('$OUT/bench_ft$ft.json'));print('ft=$ft', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['stages_ms_per_step'], d['smartcrop_kernels'], d['verified'][:5])"
+    # FI_SC_CX=1: smartcrop prescale beside the next resample (default); 0: k_sc_fd serial
+    for cx in ${CXS:-1 0}; do
+      FI_SC_CX=$cx timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-20} ${WL:+--workload $WL} \
+        > "$OUT/bench_cx$cx.json" 2> "$OUT/bench_cx$cx.err"; rc=$?
+      [ $rc -eq 0 ] || { echo "bench cx=$cx rc=$rc"; tail -5 "$OUT/bench_cx$cx.err"; exit $rc; }
+      python3 -c "import json;d=json.load(open('$OUT/bench_cx$cx.json'));print('cx=$cx', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['stages_ms_per_step'], d['smartcrop_kernels'], d['verified'][:5])"
     done ;;
   cfg4)
     timeout -k 10 600 python bench.py --workload cfg4 --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/cfg4.json" \

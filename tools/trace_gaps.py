@@ -19,7 +19,7 @@ prev_end = None
 busy = 0
 for s, e, n in ev:
     gap = (s - prev_end) / 1e3 if prev_end else 0.0
-    print(f"{(e - s) / 1e3:10.1f} us  gap {gap:9.1f} us  {n}")
+    print(f"{(s - ev[0][0]) / 1e3:10.1f} .. {(e - ev[0][0]) / 1e3:10.1f} us {(e - s) / 1e3:9.1f} us  gap {gap:9.1f} us  {n}")
     prev_end = max(prev_end or e, e)
     busy += e - s
 if ev:
