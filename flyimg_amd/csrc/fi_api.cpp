@@ -294,9 +294,9 @@ struct fi_ctx {
   // over 224 px, LDS): FI_SC_FT=0 never, 1 there (default), 2 in place of k_sc_fd too
   int sc_ft = 1;
   // k_sc_hx + k_sc_vx (no LDS, <= 64 VGPRs; gray sources, two-k-step
-  // vertical windows): FI_SC_CX=0 never; 1 (default) for the images neither
-  // k_sc_fd nor k_sc_ft takes (cfg5's gray 400 -> 111, which otherwise runs
-  // k_sc_hmfma + k_sc_vmaps); 2 for every image it fits; 3 the same, and a
+  // vertical windows): FI_SC_CX=0 never; 1 (default) for the gray images none
+  // of k_sc_fd / k_sc_ft / k_sc_fz takes (cfg5's 400 -> 111, which otherwise
+  // runs k_sc_hmfma + k_sc_vmaps); 2 for every image it fits; 3 the same, and a
   // batch whose smartcrop images all take them runs the stage on ap_stream
   // beside the next batch's resample (measured a loss on cfg2: DESIGN.md §3.2)
   int sc_cx = 1;
@@ -1127,10 +1127,13 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
     const bool fd_ok = d.fz && d.fd && aligned;
     // k_sc_fd where it streams the image (cfg2: 0.353 vs k_sc_ft's 0.363 and
     // k_sc_hx + k_sc_vx's 0.44 ms per 1024 images), k_sc_ft where it does not
-    // (FI_SC_FT=2: k_sc_ft first), k_sc_hx + k_sc_vx where neither fits
-    // (FI_SC_CX=2, 3: first)
+    // (FI_SC_FT=2: k_sc_ft first), k_sc_fz where neither fits, k_sc_hx +
+    // k_sc_vx for gray sources in place of the k_sc_hmfma + k_sc_vq /
+    // k_sc_vmaps pair (cfg5: 0.137 vs 0.586 ms per 1024 images; their
+    // 3-channel two-k-step forms spill at 64 VGPRs: cfg4 27.3 vs 7.6 ms per two
+    // steps, so RGB keeps the pair; FI_SC_CX=2, 3: first)
     const bool ft_ok = d.ft && aligned;
-    if (d.cx && aligned && (c->sc_cx >= 2 || !(fd_ok || ft_ok))) {
+    if (d.cx && aligned && (c->sc_cx >= 2 || (d.C == 1 && !(fd_ok || ft_ok || d.fz)))) {
       cx.push_back(d);
     } else if (ft_ok && (!fd_ok || c->sc_ft == 2)) {
       ft.push_back(d);
