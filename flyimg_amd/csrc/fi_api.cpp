@@ -282,6 +282,7 @@ struct fi_ctx {
   bool vr_rs = true;     // images with block-major tables take the persistent k_rs_vr (FI_VR_RS=0: k_rs_vm)
   int vr_nl = 0;         // k_rs_vr loader waves forced (FI_VR_NL=2 / 4; 0: by geometry)
   bool vr_split = true;  // k_rs_vr: one-block strips in a launch of their own (FI_VR_SPLIT=0: one launch)
+  bool vr_narrow = true;  // 48-px strips where 64-px ones would have four blocks (FI_VR_NARROW=0: off)
   int vr_pbuf = 0;       // k_rs_vr plane buffers forced (FI_VR_PBUF=1 / 2; 0: by ring room)
   int vr_max_classes = 1 << 30;  // batches with more vertical tables stay on k_rs_vm (FI_VR_MAX_CLASSES)
   bool vm_lpt = true;      // k_rs_vm tiles: LPT images -> XCDs, longest tiles first (FI_VM_LPT=0: round robin)
@@ -1439,8 +1440,19 @@ static const MfmaH *vm_strips(fi_ctx *c, const AxisTable *ht, bool q16) {
         m = MfmaH();
         break;
       }
-      bool fits = true;
-      for (const MfmaStrip &st : m.strips) fits = fits && vm_lds_bytes(st.vpitch, st.nocb, st.ks, q16) <= kVmMaxLds;
+      bool fits = true, wide = false;
+      for (const MfmaStrip &st : m.strips) {
+        fits = fits && vm_lds_bytes(st.vpitch, st.nocb, st.ks, q16) <= kVmMaxLds;
+        wide = wide || st.nocb > 3;
+      }
+      // strips of four 16-px blocks (factors below ~2.7) at 48 px instead, so
+      // k_rs_vr (<= 3 blocks a strip) takes the image (FI_VR_NARROW=0: keep 64)
+      if (fits && wide && c->vr_narrow && c->vr_rs && mx == first_nx) {
+        MfmaH n;
+        bool nfits = build_mfma_h(*ht, &n, 48);
+        for (const MfmaStrip &st : n.strips) nfits = nfits && vm_lds_bytes(st.vpitch, st.nocb, st.ks, q16) <= kVmMaxLds;
+        if (nfits && !n.strips.empty()) m = std::move(n);
+      }
       if (fits) break;
       m = MfmaH();
     }
@@ -1926,7 +1938,10 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
       const int b0 = (int)((int64_t)nblk * bnd / bands), b1 = (int)((int64_t)nblk * (bnd + 1) / bands);
       if (b1 <= b0) continue;
       const Span &sp = span_of(*w.V, b0, b1);
-      if (sp.inner > L.R) return false;
+      if (sp.inner > L.R) {
+        if (getenv("FI_VR_DEBUG")) fprintf(stderr, "vr reject: inner %d > R %d\n", sp.inner, L.R);
+        return false;
+      }
       const int64_t cost = sp.glen + 16 * (b1 - b0);
       grps.push_back(Grp{cost, (int32_t)all.size(), w.nstrips});
       for (int st = 0; st < w.nstrips; st++)
@@ -2047,9 +2062,15 @@ static bool build_vr_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp, const std::vector<
     return true;
   };
   if (!streams(L.R)) {
-    if (L.pbuf != 2) return false;
+    if (L.pbuf != 2) {
+      if (getenv("FI_VR_DEBUG")) fprintf(stderr, "vr reject: seam, R %d\n", L.R);
+      return false;
+    }
     L = L1;  // a seam needs the bigger ring
-    if (!streams(L.R)) return false;
+    if (!streams(L.R)) {
+      if (getenv("FI_VR_DEBUG")) fprintf(stderr, "vr reject: seam, R %d (one plane buffer)\n", L.R);
+      return false;
+    }
   }
   static const bool vr_debug = getenv("FI_VR_DEBUG") != nullptr;
   if (vr_debug) {
@@ -2226,6 +2247,9 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
     // k_rs_vr than on k_rs_vm in round 4 (432 vs 385 ms), hence a class cap
     // (FI_VR_MAX_CLASSES); since round 5 (4 loader waves for one-block strips,
     // their own launch) k_rs_vr takes them: cfg4 resize 363 -> 329 ms per step
+    // a table's first / last (+ pad) / widest block windows and its
+    // widest two consecutive blocks' rows (build_vr_tiles' `inner`)
+    HashMap<const VrV *, std::array<int, 4>> wmax_of;
     std::vector<const VrV *> classes;
     classes.reserve(vr.size());
     for (const VrWork &w : vr) classes.push_back(w.V);
@@ -2251,7 +2275,74 @@ static void build_vm_tiles(fi_ctx *c, Exec &E, BatchPlan &Bp) {
             part.push_back(vr[k]);
             part_w.push_back(vr_w[k]);
           }
-        if (!build_vr_tiles(c, E, Bp, part)) rest.insert(rest.end(), part_w.begin(), part_w.end());
+        // consecutive tiles of a workgroup's stream hold the last block window
+        // of one and the first of the next in the ring together (the seam,
+        // build_vr_tiles), and one failing seam sends the whole launch to
+        // k_rs_vm.  Images leave (largest windows first) until the largest
+        // first window plus the largest last window fit the ring, so the rest
+        // chain in any order: whole-image tiles (>= 2048 strips: one band) by
+        // their edge blocks' windows, banded ones by their widest window
+        {
+          int vpitch = 0;
+          bool q16 = false;
+          int64_t nstp = 0;
+          for (const VrWork &w : part) {
+            for (int st = 0; st < w.nstrips; st++) vpitch = std::max(vpitch, Bp.vstrips[w.first_strip + st].vpitch);
+            q16 = q16 || Bp.vdescs[w.img].gray || Bp.vdescs[w.img].rot != 0;
+            nstp += w.nstrips;
+          }
+          const int R = vr_lds_layout(vpitch, q16, 1).R;
+          const bool whole = nstp >= 2048;
+          std::vector<std::array<int, 3>> hl(part.size());  // head, last window, index
+          for (size_t k = 0; k < part.size(); k++) {
+            const VrV &V = *part[k].V;
+            auto wm = wmax_of.find(&V);
+            if (wm == wmax_of.end()) {
+              const int32_t *bm = V.bmeta.data();
+              const int nb = V.nblk;
+              int w = 0, inner = bm[2] - bm[0];
+              for (int b = 0; b < nb; b++) w = std::max(w, bm[4 * b + 2] - bm[4 * b]);
+              for (int b = 0; b + 1 < nb; b++) inner = std::max(inner, bm[4 * (b + 1) + 2] - bm[4 * b]);
+              const int glen = (bm[4 * (nb - 1) + 2] - bm[0] + 15) / 16 * 16;
+              wm = wmax_of
+                       .emplace(&V, std::array<int, 4>{bm[2] - bm[0], glen - (bm[4 * (nb - 1)] - bm[0]), w, inner})
+                       .first;
+            }
+            const auto &a = wm->second;
+            // a tile's first window is its first block's, its last one (K0s are
+            // multiples of 16) its last block's rounded up to 16 rows
+            hl[k] = whole ? std::array<int, 3>{a[0], a[1], (int)k} : std::array<int, 3>{a[2], (a[2] + 15) / 16 * 16, (int)k};
+            if (a[3] > R) hl[k] = {R + 1, R + 1, (int)k};  // a block pair alone exceeds the ring: always out
+          }
+          std::sort(hl.begin(), hl.end(), [](const std::array<int, 3> &x, const std::array<int, 3> &y) {
+            return std::max(x[0], x[1]) > std::max(y[0], y[1]);
+          });
+          // the fewest leading (largest) images to drop: suffix maxima of both windows
+          std::vector<int> sh(hl.size() + 1, 0), sl(hl.size() + 1, 0);
+          for (size_t k = hl.size(); k-- > 0;) {
+            sh[k] = std::max(sh[k + 1], hl[k][0]);
+            sl[k] = std::max(sl[k + 1], hl[k][1]);
+          }
+          size_t drop = 0;
+          while (drop < hl.size() && sh[drop] + sl[drop] > R) drop++;
+          if (drop > 0) {
+            std::vector<char> out(part.size(), 0);
+            for (size_t k = 0; k < drop; k++) out[hl[k][2]] = 1;
+            std::vector<VrWork> keep;
+            std::vector<Work1> keep_w;
+            for (size_t k = 0; k < part.size(); k++) {
+              if (out[k]) {
+                rest.push_back(part_w[k]);
+              } else {
+                keep.push_back(part[k]);
+                keep_w.push_back(part_w[k]);
+              }
+            }
+            part.swap(keep);
+            part_w.swap(keep_w);
+          }
+        }
+        if (!part.empty() && !build_vr_tiles(c, E, Bp, part)) rest.insert(rest.end(), part_w.begin(), part_w.end());
       }
       work.swap(rest);
     }
@@ -3328,6 +3419,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_VR_RS")) c->vr_rs = e[0] == '1';
   if (const char *e = getenv("FI_VR_NL")) c->vr_nl = atoi(e);
   if (const char *e = getenv("FI_VR_SPLIT")) c->vr_split = e[0] == '1';
+  if (const char *e = getenv("FI_VR_NARROW")) c->vr_narrow = e[0] == '1';
   if (const char *e = getenv("FI_VR_PBUF")) c->vr_pbuf = atoi(e);
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';
@@ -3531,6 +3623,12 @@ int fi_debug_host_plan(const fi_image *imgs, int32_t n, int32_t iters, double *m
     const double t4 = now_ms();
     build_hv_tiles(c, E, Bp);
     const double t5 = now_ms();
+    // images per resample kernel (FI_PLAN_PROF lists them as "plan_path_*")
+    int nvr = 0;
+    for (const BatchPlan::VrLaunch &V : Bp.vrl) nvr += V.images;
+    c->stats["plan_path_vr"].launches += nvr;
+    c->stats["plan_path_vm"].launches += (int64_t)Bp.vdescs.size() - nvr;
+    c->stats["plan_vr_launches"].launches += (int64_t)Bp.vrl.size();
     Packed K;
     pack_batch(c, E, Bp, K);
     const double t6 = now_ms();

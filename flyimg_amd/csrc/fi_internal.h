@@ -116,7 +116,7 @@ struct ScDesc {
   int32_t cx_kv, cx_tp;    // their vertical k-steps, transposed H-stage row pitch (ScPlan::cx_*)
   int32_t cxA, cxK0;       // arena offsets (int32 units; cxA 16-B aligned)
   int32_t cx_pad;
-  uint8_t *tbuf;       // k_sc_hx's transposed H-stage: [hm_nb][C][16][cx_tp] bytes
+  uint8_t *tbuf;       // k_sc_hx's H stage: 256-B tiles [hm_nb][C][cx_tp / 16][16 columns][16 rows]
   uint8_t *red;        // reduce scratch rw*rh*3
   uint8_t *hbuf;       // H-pass scratch aw*hrows*3
   uint8_t *pre;        // prescaled image aw*ah*3

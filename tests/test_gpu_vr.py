@@ -41,13 +41,13 @@ CASES = [
     (3000, 2000, "w_300,h_250,c_1", 3),  # cfg1: 1250 of 2000 rows at gaps of 1 and 2
     (3840, 2160, "w_512,h_512,c_1", 300),
     (1920, 1080, "w_500", 300),
-    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", 24),
-    (640, 480, "w_320", 7),  # 1/2: 85 output px per 512-B strip, more than k_rs_vr's 3 16-px blocks
+    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", 12),
+    (640, 480, "w_320", 7),  # 1/2: 64-px strips would carry four 16-px blocks; built at 48 px for k_rs_vr
 ]
 
 
-# k_rs_vm's class: strips wider than three 16-px output blocks
-NOT_VR = {(640, 480, "w_320")}
+# k_rs_vm's class (FI_VR_NARROW=0 puts the 1/2 case back there: test_narrow_strips_switch)
+NOT_VR = set()
 
 
 @pytest.fixture(scope="module")
@@ -146,12 +146,27 @@ def test_output_independent_of_cobatched_images(pair):
 
 ROLE_CASES = [
     (1920, 1080, "w_500", 6),  # cfg2: 3 output blocks a strip (4 loaders need <= 2: stays at 2)
-    (3840, 2160, "w_512,h_512,c_1", 4),
-    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", 3),
-    (4000, 3000, "w_150", 3),  # uneven rows: the 8-row pair classes with 4 loaders
-    (3000, 2000, "w_300,h_250,c_1", 5),
+    (3840, 2160, "w_512,h_512,c_1", 2),
+    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray", 2),
+    (4000, 3000, "w_150", 2),  # uneven rows: the 8-row pair classes with 4 loaders
+    (3000, 2000, "w_300,h_250,c_1", 3),
     (333, 517, "w_97", 4),
 ]
+
+
+_VM_REF = {}
+
+
+def _vm_ref(vm, W, H, opts, n):
+    """k_rs_vm's outputs of a ROLE_CASES entry, computed once per module (the
+    four role splits compare against the same bytes)"""
+    key = (W, H, opts, n)
+    if key not in _VM_REF:
+        op = ImageProcessor(OptionsBag(opts), W, H).to_op()
+        oa, _, rca = vm.process([synth_rgb(W, H, 900 + k) for k in range(n)], [op] * n)
+        assert rca == 0
+        _VM_REF[key] = oa
+    return _VM_REF[key]
 
 
 @pytest.mark.parametrize("nl,pbuf", [(2, 1), (2, 2), (4, 1), (4, 2)])
@@ -168,8 +183,7 @@ def test_vr_role_splits_and_plane_buffers(pair, nl, pbuf):
             ob, rb, rc = ctx.process(srcs, [op] * n)
             assert rc == 0 and all(r.status == 0 for r in rb), L.lib().fi_last_error()
             assert ctx.stats("path_vr")[1] == before + n
-            oa, _, rca = vm.process(srcs, [op] * n)
-            assert rca == 0
+            oa = _vm_ref(vm, W, H, opts, n)
             for k in range(n):
                 assert np.array_equal(ob[k], oa[k]), f"{opts} nl {nl} pbuf {pbuf} image {k}"
     finally:
@@ -200,3 +214,28 @@ def test_vr_split_launches(pair):
         for k in range(len(srcs)):
             if gk[k][0] == g:
                 assert np.array_equal(ob[k], oa[gk[k][1]]), f"{g} image {k}: split k_rs_vr != k_rs_vm"
+
+
+def test_narrow_strips_switch(pair):
+    """FI_VR_NARROW=0 keeps 64-px strips (four 16-px blocks at 1/2) on k_rs_vm;
+    the default builds them at 48 px for k_rs_vr; both give k_rs_vm's bytes of
+    the default context's 64-px tables (the pixels do not depend on the strip
+    width)."""
+    vr, vm = pair
+    W, H, opts = 640, 480, "w_320"
+    op = ImageProcessor(OptionsBag(opts), W, H).to_op()
+    srcs = [synth_rgb(W, H, 4100 + k) for k in range(3)]
+    wide = _context_with({"FI_VR_RS": "1", "FI_FORCE_GENERIC": "0", "FI_VR_NARROW": "0"})
+    try:
+        b = wide.stats("path_vm")[1]
+        ow, rw, rcw = wide.process(srcs, [op] * 3)
+        assert rcw == 0 and wide.stats("path_vm")[1] == b + 3
+        b = vr.stats("path_vr")[1]
+        on, rn, rcn = vr.process(srcs, [op] * 3)
+        assert rcn == 0 and vr.stats("path_vr")[1] == b + 3
+        om, _, rcm = vm.process(srcs, [op] * 3)
+        assert rcm == 0
+        for k in range(3):
+            assert np.array_equal(on[k], om[k]) and np.array_equal(ow[k], om[k])
+    finally:
+        wide.close()
