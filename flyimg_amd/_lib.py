@@ -168,6 +168,7 @@ def lib():
     L.fi_debug_monochrome.argtypes = [vp, vp, i32, i32, i32, vp, i32]
     L.fi_debug_convolve.argtypes = [vp, vp, i32, i32, i32, vp, ctypes.c_uint32, vp]
     L.fi_debug_skinsat.argtypes = [vp, vp, vp]
+    L.fi_debug_host_plan.argtypes = [ctypes.POINTER(FiImage), i32, i32, ctypes.POINTER(ctypes.c_double)]
     L.fi_jpeg_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t, P(i32), P(i32), P(i32)]
     L.fi_jpeg_decode_device.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp]
     _lib = L

@@ -3584,6 +3584,16 @@ int fi_debug_host_plan(const fi_image *imgs, int32_t n, int32_t iters, double *m
     if (c) c->stats.clear();
     return FI_OK;
   }
+  if (!imgs && n == 2) {  // (NULL, 2, 0, ms): the resample plan's counters
+    if (!ms) return set_err(FI_EINVAL, "ms is NULL");
+    ms[0] = ms[1] = ms[2] = 0;
+    if (c) {
+      ms[0] = (double)c->stats["plan_path_vr"].launches;
+      ms[1] = (double)c->stats["plan_vertical_first"].launches;
+      ms[2] = (double)c->stats["plan_vr_launches"].launches;
+    }
+    return FI_OK;
+  }
   if (!imgs || n <= 0 || iters <= 0 || !ms) return set_err(FI_EINVAL, "bad arguments");
   if (!c) {
     c = new fi_ctx();
@@ -3623,11 +3633,12 @@ int fi_debug_host_plan(const fi_image *imgs, int32_t n, int32_t iters, double *m
     const double t4 = now_ms();
     build_hv_tiles(c, E, Bp);
     const double t5 = now_ms();
-    // images per resample kernel (FI_PLAN_PROF lists them as "plan_path_*")
+    // images per resample kernel (FI_PLAN_PROF lists them; (NULL, 2, ...) reads them)
     int nvr = 0;
     for (const BatchPlan::VrLaunch &V : Bp.vrl) nvr += V.images;
     c->stats["plan_path_vr"].launches += nvr;
-    c->stats["plan_path_vm"].launches += (int64_t)Bp.vdescs.size() - nvr;
+    // (build_vr_tiles appends a second descriptor for each of its images)
+    c->stats["plan_vertical_first"].launches += (int64_t)Bp.vdescs.size() - nvr;
     c->stats["plan_vr_launches"].launches += (int64_t)Bp.vrl.size();
     Packed K;
     pack_batch(c, E, Bp, K);

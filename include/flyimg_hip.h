@@ -319,6 +319,17 @@ int fi_jpeg_decode_device(fi_ctx *ctx, const uint8_t *const *data, const size_t 
  * every colour with the oracle's detect_skin / detect_saturation. */
 int fi_debug_skinsat(fi_ctx *ctx, const fi_smartcrop_params *params, uint16_t *out);
 
+/* Test hook (not a reference interface): the batch planner alone, on the
+ * host -- no device: the image pointers are planned, never dereferenced --
+ * over `iters` passes of the n images; ms[0..6] += per-stage host
+ * milliseconds (images, smartcrop, workspace, vm + vr tiles, of which vr, hv
+ * tiles, blob).  One host-only context persists across calls (its caches, as
+ * a serving context's): (NULL, 0, ...) drops it, (NULL, 1, ...) clears its
+ * statistics, (NULL, 2, 0, ms) reads the resample plan's counters since:
+ * ms[0] images planned onto k_rs_vr, ms[1] vertical-first images, ms[2]
+ * k_rs_vr launches. */
+int fi_debug_host_plan(const fi_image *imgs, int32_t n, int32_t iters, double *ms);
+
 #ifdef __cplusplus
 }
 #endif
