@@ -1130,9 +1130,10 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
     // k_sc_hx + k_sc_vx's 0.44 ms per 1024 images), k_sc_ft where it does not
     // (FI_SC_FT=2: k_sc_ft first), k_sc_fz where neither fits, k_sc_hx +
     // k_sc_vx for gray sources in place of the k_sc_hmfma + k_sc_vq /
-    // k_sc_vmaps pair (cfg5: 0.137 vs 0.586 ms per 1024 images; their
-    // 3-channel two-k-step forms spill at 64 VGPRs: cfg4 27.3 vs 7.6 ms per two
-    // steps, so RGB keeps the pair; FI_SC_CX=2, 3: first)
+    // k_sc_vmaps pair (cfg5: 0.137 vs 0.586 ms per 1024 images); RGB keeps the
+    // pair (cfg4 sc_prep 20.1 vs 22.6 ms per step with the RGB forms at 128
+    // VGPRs and row-segmented tiles; 30.0 when they spilled at 64)
+    // (FI_SC_CX=2, 3: first)
     const bool ft_ok = d.ft && aligned;
     if (d.cx && aligned && (c->sc_cx >= 2 || (d.C == 1 && !(fd_ok || ft_ok || d.fz)))) {
       cx.push_back(d);
@@ -1218,7 +1219,7 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
     X->ftt_off[ks - 1] = B.addv(tl);
     X->ft_tiles[ks - 1] = (int)(tl.size() / 2);
   }
-  // k_sc_hx tiles (descriptor, first of 4 column blocks), k_sc_vx tiles
+  // k_sc_hx tiles (descriptor, first of 4 column blocks, first of kHxRb row blocks), k_sc_vx tiles
   // (descriptor, chunk) four to a workgroup, one list per variant
   X->cx_off = B.addv(cx);
   X->ncx = (int)cx.size();
@@ -1229,10 +1230,12 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
       const ScDesc &d = cx[k];
       if (d.C != nch) continue;
       if (d.hm_ks == ks)
-        for (int b = 0; b < d.hm_nb; b += 4) {
-          ht.push_back((int32_t)k);
-          ht.push_back(b);
-        }
+        for (int r = 0; r < d.cx_tp / 16 - 1; r += kHxRb)
+          for (int b = 0; b < d.hm_nb; b += 4) {
+            ht.push_back((int32_t)k);
+            ht.push_back(b);
+            ht.push_back(r);
+          }
       if (d.cx_kv == ks)
         for (int ch = 0; ch < (d.ah + kVqRows - 1) / kVqRows; ch++) {
           vt.push_back((int32_t)k);
@@ -1244,7 +1247,7 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
       vt.push_back(0);
     }
     X->hxt_off[v] = B.addv(ht);
-    X->hx_tiles[v] = (int)(ht.size() / 2);
+    X->hx_tiles[v] = (int)(ht.size() / 3);
     X->vxt_off[v] = B.addv(vt);
     X->vx_tiles[v] = (int)(vt.size() / 2);
   }

@@ -140,6 +140,9 @@ constexpr int kPrepMaxLds = 64 * 1024;
 // k_sc_ft (fi_smartcrop.hip): one 8-wave workgroup per kFtChunks consecutive
 // analysed-row chunks of an image; LDS <= kFtMaxLds keeps two per CU
 constexpr int kFtChunks = 2;
+// k_sc_hx (fi_smartcrop.hip): 16-row blocks of the H stage one wave walks (a
+// tile = image x 4 column blocks x kHxRb row blocks)
+constexpr int kHxRb = 8;
 constexpr int kFtMaxLds = 80 * 1024;
 // k_sc_fz (fi_smartcrop.hip): the fused per-image prescale + maps; LDS =
 // kFzRing (80) H-stage rows + max(3 source planes of 16 rows, 16 prescaled rows

@@ -1459,15 +1459,18 @@ __global__ __launch_bounds__(kFtThreads, KS == 1 ? 4 : 2) void k_sc_ft(const ScD
 //    estimator, k_sc_skinsat's table for what it leaves open.
 // The host runs both on the apply stream behind the batch's resample, so they
 // overlap the next batch's k_rs_vr (fi_api.cpp launch_batch).
+// (the RGB two-k-step forms at 128 VGPRs: at 64 they spill, and they never
+// run beside k_rs_vr -- FI_SC_CX=3 is for uniform cfg2-like batches)
 template <int KS, int NCH>
-__global__ __launch_bounds__(256, 8) void k_sc_hx(const ScDesc *__restrict__ descs, const int32_t *__restrict__ tiles,
-                                                  const int32_t *__restrict__ ai) {
+__global__ __launch_bounds__(256, KS == 2 && NCH == 3 ? 4 : 8) void k_sc_hx(const ScDesc *__restrict__ descs,
+                                                                          const int32_t *__restrict__ tiles,
+                                                                          const int32_t *__restrict__ ai) {
   typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int di = tiles[2 * blockIdx.x];
+  const int di = tiles[3 * blockIdx.x];
   if (di < 0) return;
   const ScDesc &D = descs[di];
-  const int b = tiles[2 * blockIdx.x + 1] + wave;
+  const int b = tiles[3 * blockIdx.x + 1] + wave, rb0 = tiles[3 * blockIdx.x + 2];
   if (b >= D.hm_nb) return;
   const int g = lane >> 4, r = lane & 15;
   const int aw = D.aw, hrows = D.hrows, yoff = D.ybox_first, tp = D.cx_tp;
@@ -1508,13 +1511,15 @@ __global__ __launch_bounds__(256, 8) void k_sc_hx(const ScDesc *__restrict__ des
         q[t][i] = v;
       }
   };
-  const int nrb = nrbt - 1;  // (the last tile row block: the V pass's straddle margin, never read as data)
+  // row blocks [rb0, rb0 + kHxRb) of the H stage (the last tile row block is
+  // the V pass's straddle margin, never read as data)
+  const int nrb = min(nrbt - 1, rb0 + kHxRb);
   constexpr bool kPre = KS * NQ <= 3;  // the next row block's loads in flight (within 64 VGPRs)
   u32x4a cur[KS][NQ], nxt[KS][NQ];
-  load(0, cur);
+  load(rb0, cur);
 #pragma unroll 1
-  for (int rb = 0; rb < nrb; rb++) {
-    if (!kPre && rb > 0) load(rb, cur);
+  for (int rb = rb0; rb < nrb; rb++) {
+    if (!kPre && rb > rb0) load(rb, cur);
     if (kPre && rb + 1 < nrb) load(rb + 1, nxt);
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
@@ -1557,7 +1562,7 @@ __global__ __launch_bounds__(256, 8) void k_sc_hx(const ScDesc *__restrict__ des
 __device__ __forceinline__ uint32_t vx_byte(uint32_t v, int i) { return (v >> (8 * i)) & 255u; }
 
 template <int KV, int NCH>
-__global__ __launch_bounds__(256, 8) void k_sc_vx(const ScDesc *__restrict__ descs, const int32_t *__restrict__ tiles,
+__global__ __launch_bounds__(256, KV == 2 && NCH == 3 ? 4 : 8) void k_sc_vx(const ScDesc *__restrict__ descs, const int32_t *__restrict__ tiles,
                                                   const int32_t *__restrict__ ai, const ScFast F,
                                                   const uint16_t *__restrict__ skinsat) {
   typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
