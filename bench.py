@@ -80,7 +80,6 @@ KERNEL_OF_PATH = {
 # smartcrop prescale + maps kernel per image (counts kept by the library)
 SC_KERNEL_OF_PATH = {
     "sc_path_cx": "k_sc_hx + k_sc_vx (prescale + maps, co-resident beside the next batch's resample)",
-    "sc_path_ft": "k_sc_ft (prescale + maps, one workgroup per analysed-row chunk)",
     "sc_path_fd": "k_sc_fd (prescale + maps, source rows by LDS-DMA)",
     "sc_path_fz": "k_sc_fz (prescale + maps, register-staged source rows)",
 }

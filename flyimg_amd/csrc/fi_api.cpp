@@ -54,8 +54,6 @@ int launch_sc_fz(hipStream_t s, const ScDesc *descs, int n, int lds, const int32
                  const uint16_t *skinsat);
 int launch_sc_fd(hipStream_t s, const ScDesc *descs, int n, int lds, const int32_t *ai, const ScParamsDev &P,
                  const uint16_t *skinsat);
-int launch_sc_ft(hipStream_t s, int ks, const ScDesc *descs, const int32_t *tiles, int ntiles, int lds,
-                 const int32_t *ai, const ScParamsDev &P, const uint16_t *skinsat);
 int launch_sc_hx(hipStream_t s, int ks, int nch, const ScDesc *descs, const int32_t *tiles, int ntiles,
                  const int32_t *ai);
 int launch_sc_vx(hipStream_t s, int kv, int nch, const ScDesc *descs, const int32_t *tiles, int ntiles,
@@ -291,12 +289,9 @@ struct fi_ctx {
   int n_cu = 256;        // compute units (k_rs_vr: one persistent workgroup per CU)
   bool sc_fz = true;        // FI_DISABLE_SC_FZ=1: k_sc_hmfma + k_sc_vq instead of the fused k_sc_fz
   bool sc_fd = true;        // FI_SC_FD=0: k_sc_fz instead of its LDS-DMA form k_sc_fd
-  // k_sc_ft (chunk tiles) for the images k_sc_fd cannot stream (analysed widths
-  // over 224 px, LDS): FI_SC_FT=0 never, 1 there (default), 2 in place of k_sc_fd too
-  int sc_ft = 1;
   // k_sc_hx + k_sc_vx (no LDS, <= 64 VGPRs; gray sources, two-k-step
   // vertical windows): FI_SC_CX=0 never; 1 (default) for the gray images none
-  // of k_sc_fd / k_sc_ft / k_sc_fz takes (cfg5's 400 -> 111, which otherwise
+  // of k_sc_fd / k_sc_fz takes (cfg5's 400 -> 111, which otherwise
   // runs k_sc_hmfma + k_sc_vmaps); 2 for every image it fits; 3 the same, and a
   // batch whose smartcrop images all take them runs the stage on ap_stream
   // beside the next batch's resample (measured a loss on cfg2: DESIGN.md §3.2)
@@ -328,7 +323,6 @@ struct fi_ctx {
   struct ScTabs {
     int32_t hb = 0, hk = 0, hkT = 0, vb = 0, vk = 0;
     int32_t hmB = 0, hmC = 0, hmS0 = 0, vqA = 0, vqC = 0, vqK0 = 0;
-    int32_t ftB = -1;
     int32_t cxA = -1, cxK0 = -1;
   };
   HashMap<const AxisTable *, DevAxis> axis_at;
@@ -881,11 +875,6 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
             t.cxK0 = E.oi();
             E.ai.insert(E.ai.end(), P.cxK0.begin(), P.cxK0.end());
           }
-          if (!P.ftB.empty()) {
-            while (E.ai.size() % 4) E.ai.push_back(0);  // 16-B aligned fragments
-            t.ftB = E.oi();
-            E.ai.insert(E.ai.end(), P.ftB.begin(), P.ftB.end());
-          }
         }
         tp = c->sc_at.emplace(&P, t).first;
       }
@@ -1013,16 +1002,6 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
                    fd_lds(it.W, P.hm_pitch, P.aw, P.ah) <= kFdMaxLds
                ? 1
                : 0;
-    // k_sc_ft: the vertical tables (one 64-row window per chunk), the
-    // horizontal ones at <= 2 k-steps, 16-B aligned 3-channel rows readable to
-    // fd_rp(W) (the source's own alignment is checked at launch)
-    d.ft = d.vq && c->sc_ft > 0 && c->sc_fz && c->sc_fd && P.fx == 1 && P.fy == 1 && it.C == 3 && it.stride % 16 == 0 &&
-                   (it.padded || (it.W * 3) % 16 == 0) && P.hm_ks <= 2 && T.ftB >= 0 && P.ft_lds > 0 &&
-                   P.ft_lds <= kFtMaxLds
-               ? 1
-               : 0;
-    d.ftB = T.ftB;
-    d.ft_rows = P.ft_rows;
     d.vqA = T.vqA;
     d.vqC = T.vqC;
     d.vqK0 = T.vqK0;
@@ -1044,8 +1023,6 @@ static void plan_smartcrop(fi_ctx *c, Exec &E, const std::vector<ScItem> &items,
     // workspace (offsets; converted to pointers after allocation)
     auto take = [&](size_t n) { return (uint8_t *)(uintptr_t)(E.work.take(n) + 1); };
     if (P.fx > 1 || P.fy > 1) d.red = take((size_t)P.rw * P.rh * 3);
-    // (k_sc_ft needs none, but a source that turns out unaligned at launch
-    // falls back to k_sc_hmfma + k_sc_vq when k_sc_fz cannot take it)
     if (P.thumb && P.need_h && !d.fz)  // generic kernels: pitch aw*3; k_sc_hmfma: pitch apitch
       d.hbuf = take((size_t)(prep ? (P.aw * 3 + 15) / 16 * 16 : P.aw * 3) * std::max(P.hrows, 1));
     if (P.thumb && (!prep || want_pre)) d.pre = take((size_t)P.aw * P.ah * 3);
@@ -1100,8 +1077,6 @@ struct ScLaunches {
   int nhm = 0, hm_chunks = 0, hm_lds = 0, nvm = 0, v_chunks = 0, v_lds = 0;
   size_t fz_off = 0, fd_off = 0;  // k_sc_fz, k_sc_fd
   int nfz = 0, fz_lds = 0, nfd = 0, fd_lds = 0;
-  size_t ft_off = 0, ftt_off[2] = {0, 0};  // k_sc_ft: descriptors, tile lists per k-step count
-  int nft = 0, ft_tiles[2] = {0, 0}, ft_lds = 0;
   // k_sc_hx / k_sc_vx: descriptors, tile lists per variant v = 2 (k-steps - 1) + (channels == 3)
   size_t cx_off = 0, hxt_off[4] = {0, 0, 0, 0}, vxt_off[4] = {0, 0, 0, 0};
   int ncx = 0, hx_tiles[4] = {0, 0, 0, 0}, vx_tiles[4] = {0, 0, 0, 0};
@@ -1116,8 +1091,7 @@ struct ScLaunches {
 static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const std::vector<int> &sstatus,
                             ScLaunches *X) {
   std::vector<int> sred, shp, svp, smaps;
-  std::vector<ScDesc> hm, sl, sg, vq, vm, fz, fd, s3, ft, cx;
-  std::vector<int> ft_chunks;
+  std::vector<ScDesc> hm, sl, sg, vq, vm, fz, fd, s3, cx;
   for (size_t k = 0; k < SL.descs.size(); k++) {
     if (sstatus[k] != FI_OK) continue;
     X->nok++;
@@ -1126,21 +1100,15 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
     if (d.red) sred.push_back((int)k);
     const bool aligned = ((uintptr_t)d.img & 15) == 0;
     const bool fd_ok = d.fz && d.fd && aligned;
-    // k_sc_fd where it streams the image (cfg2: 0.353 vs k_sc_ft's 0.363 and
-    // k_sc_hx + k_sc_vx's 0.44 ms per 1024 images), k_sc_ft where it does not
-    // (FI_SC_FT=2: k_sc_ft first), k_sc_fz where neither fits, k_sc_hx +
+    // k_sc_fd where it streams the image (cfg2: 0.353 vs k_sc_hx + k_sc_vx's
+    // 0.44 ms per 1024 images), k_sc_fz where it does not, k_sc_hx +
     // k_sc_vx for gray sources in place of the k_sc_hmfma + k_sc_vq /
     // k_sc_vmaps pair (cfg5: 0.137 vs 0.586 ms per 1024 images); RGB keeps the
     // pair (cfg4 sc_prep 20.1 vs 22.6 ms per step with the RGB forms at 128
     // VGPRs and row-segmented tiles; 30.0 when they spilled at 64)
     // (FI_SC_CX=2, 3: first)
-    const bool ft_ok = d.ft && aligned;
-    if (d.cx && aligned && (c->sc_cx >= 2 || (d.C == 1 && !(fd_ok || ft_ok || d.fz)))) {
+    if (d.cx && aligned && (c->sc_cx >= 2 || (d.C == 1 && !(fd_ok || d.fz)))) {
       cx.push_back(d);
-    } else if (ft_ok && (!fd_ok || c->sc_ft == 2)) {
-      ft.push_back(d);
-      ft_chunks.push_back(P.vq_chunks);
-      X->ft_lds = std::max(X->ft_lds, P.ft_lds);
     } else if (fd_ok) {
       fd.push_back(d);
       X->fd_lds = std::max(X->fd_lds, fd_lds(d.W, d.hm_pitch, d.aw, d.ah));
@@ -1189,36 +1157,6 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
   X->nfz = (int)fz.size();
   X->fd_off = B.addv(fd);
   X->nfd = (int)fd.size();
-  // k_sc_ft tiles (descriptor, chunk), one list per k-step count, XCD-aware:
-  // images round robin over the 8 XCDs, each XCD's tiles image by image, and
-  // workgroup g = 8 j + x takes XCD x's j-th tile (dispatch puts workgroup g on
-  // XCD g % 8), so an image's chunks run side by side in one L2
-  X->ft_off = B.addv(ft);
-  X->nft = (int)ft.size();
-  for (int ks = 1; ks <= 2; ks++) {
-    std::vector<int32_t> per[8];
-    int nimg = 0;
-    for (size_t k = 0; k < ft.size(); k++) {
-      if (ft[k].hm_ks != ks) continue;
-      std::vector<int32_t> &q = per[nimg++ % 8];
-      for (int ch = 0; ch < ft_chunks[k]; ch += kFtChunks) {
-        q.push_back((int32_t)k);
-        q.push_back(ch);
-      }
-    }
-    size_t len = 0;
-    for (auto &q : per) len = std::max(len, q.size() / 2);
-    std::vector<int32_t> tl;
-    tl.reserve(16 * len);
-    for (size_t j = 0; j < len; j++)
-      for (int x = 0; x < 8; x++) {
-        const bool have = 2 * j < per[x].size();
-        tl.push_back(have ? per[x][2 * j] : -1);
-        tl.push_back(have ? per[x][2 * j + 1] : 0);
-      }
-    X->ftt_off[ks - 1] = B.addv(tl);
-    X->ft_tiles[ks - 1] = (int)(tl.size() / 2);
-  }
   // k_sc_hx tiles (descriptor, first of 4 column blocks, first of kHxRb row blocks), k_sc_vx tiles
   // (descriptor, chunk) four to a workgroup, one list per variant
   X->cx_off = B.addv(cx);
@@ -1252,7 +1190,7 @@ static void add_sc_launches(fi_ctx *c, Blob &B, const ScLaunchData &SL, const st
     X->vx_tiles[v] = (int)(vt.size() / 2);
   }
   c->stats["sc_path_cx"].launches += X->ncx;
-  c->stats["sc_path_ft"].launches += X->nft;  // images per smartcrop prescale kernel (fi_kernel_stats)
+  // images per smartcrop prescale kernel (fi_kernel_stats)
   c->stats["sc_path_fd"].launches += X->nfd;
   c->stats["sc_path_fz"].launches += X->nfz;
   X->sl_off = B.addv(sl);
@@ -1274,7 +1212,7 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
   // on the stream that reads it, so batches queued before a parameter change
   // have read the old table first
   const uint16_t *skinsat = nullptr;
-  if (X.nfz > 0 || X.nfd > 0 || X.nft > 0 || X.ncx > 0) {
+  if (X.nfz > 0 || X.nfd > 0 || X.ncx > 0) {
     const std::string key(reinterpret_cast<const char *>(&PD), offsetof(ScParamsDev, pad));
     if (!c->skinsat.p || c->skinsat_key != key) {
       const int rc = ensure(c, &c->skinsat, (size_t)2 << 24);
@@ -1294,13 +1232,9 @@ static int enqueue_sc(fi_ctx *c, hipStream_t st, uint8_t *ab, const ScLaunches &
         launch_sc_vq(st, (const ScDesc *)(ab + X.vq_off), X.nvq, X.vq_chunks, X.vq_lds, ai, PD) != 0 ||
         launch_sc_v(st, (const ScDesc *)(ab + X.vm_off), X.nvm, X.v_chunks, X.v_lds, ai, PD) != 0 ||
         launch_sc_fz(st, (const ScDesc *)(ab + X.fz_off), X.nfz, X.fz_lds, ai, PD, skinsat) != 0 ||
-        launch_sc_fd(st, (const ScDesc *)(ab + X.fd_off), X.nfd, X.fd_lds, ai, PD, skinsat) != 0 ||
-        launch_sc_ft(st, 1, (const ScDesc *)(ab + X.ft_off), (const int32_t *)(ab + X.ftt_off[0]), X.ft_tiles[0],
-                     X.ft_lds, ai, PD, skinsat) != 0 ||
-        launch_sc_ft(st, 2, (const ScDesc *)(ab + X.ft_off), (const int32_t *)(ab + X.ftt_off[1]), X.ft_tiles[1],
-                     X.ft_lds, ai, PD, skinsat) != 0)
-      return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d/%d/%d)", X.hm_lds, X.vq_lds,
-                     X.fz_lds, X.fd_lds, X.ft_lds);
+        launch_sc_fd(st, (const ScDesc *)(ab + X.fd_off), X.nfd, X.fd_lds, ai, PD, skinsat) != 0)
+      return set_err(FI_EDEVICE, "smartcrop prescale launch rejected (LDS %d/%d/%d/%d)", X.hm_lds, X.vq_lds,
+                     X.fz_lds, X.fd_lds);
     for (int v = 0; v < 4; v++) {
       const ScDesc *cd = (const ScDesc *)(ab + X.cx_off);
       if (launch_sc_hx(st, v / 2 + 1, (v & 1) ? 3 : 1, cd, (const int32_t *)(ab + X.hxt_off[v]), X.hx_tiles[v],
@@ -3426,7 +3360,6 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (const char *e = getenv("FI_VR_PBUF")) c->vr_pbuf = atoi(e);
   if (const char *e = getenv("FI_DISABLE_SC_FZ")) c->sc_fz = !(e[0] == '1');
   if (const char *e = getenv("FI_SC_FD")) c->sc_fd = e[0] == '1';
-  if (const char *e = getenv("FI_SC_FT")) c->sc_ft = atoi(e);
   if (const char *e = getenv("FI_SC_CX")) c->sc_cx = atoi(e);
   if (const char *e = getenv("FI_SC_MFMA")) c->sc_mf = e[0] == '1';
   if (const char *e = getenv("FI_VR_MAX_CLASSES")) c->vr_max_classes = atoi(e);

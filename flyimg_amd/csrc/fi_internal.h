@@ -108,9 +108,6 @@ struct ScDesc {
   int32_t vq;              // 1: vertical pass + maps by k_sc_vq (tables below)
   int32_t fz;              // 1: both passes + maps by k_sc_fz (hm + vq tables, one workgroup per image)
   int32_t fd;              // 1 (with fz): rows readable to fd_rp(W) bytes, so k_sc_fd may take it
-  int32_t ft;              // 1 (with vq): the same rows, k_sc_ft (chunk tiles) takes it
-  int32_t ftB;             // arena offset (int32 units, 16-B aligned) of k_sc_ft's B fragments (ScPlan::ftB)
-  int32_t ft_rows;         // k_sc_ft's H-stage window rows in LDS (ScPlan::ft_rows)
   int32_t vqA, vqC, vqK0;  // arena offsets (int32 units; vqA 16-B aligned)
   int32_t cx;              // 1: k_sc_hx + k_sc_vx take it (tables below, tbuf)
   int32_t cx_kv, cx_tp;    // their vertical k-steps, transposed H-stage row pitch (ScPlan::cx_*)
@@ -137,13 +134,9 @@ struct ScDesc {
 constexpr int kPrepRows = 16;
 constexpr int kVqRows = 14;  // k_sc_vq: analysed rows per workgroup (16 prescaled rows with the edge halo)
 constexpr int kPrepMaxLds = 64 * 1024;
-// k_sc_ft (fi_smartcrop.hip): one 8-wave workgroup per kFtChunks consecutive
-// analysed-row chunks of an image; LDS <= kFtMaxLds keeps two per CU
-constexpr int kFtChunks = 2;
 // k_sc_hx (fi_smartcrop.hip): 16-row blocks of the H stage one wave walks (a
 // tile = image x 4 column blocks x kHxRb row blocks)
 constexpr int kHxRb = 8;
-constexpr int kFtMaxLds = 80 * 1024;
 // k_sc_fz (fi_smartcrop.hip): the fused per-image prescale + maps; LDS =
 // kFzRing (80) H-stage rows + max(3 source planes of 16 rows, 16 prescaled rows
 // + luma); <= 80 KB keeps two workgroups per CU

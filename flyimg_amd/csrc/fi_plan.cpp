@@ -1155,68 +1155,6 @@ static void plan_sc_vq(ScPlan *p) {
   p->vq_ok = true;
 }
 
-// k_sc_ft tables (fi_plan.h ScPlan::ftB): the horizontal coefficients of each
-// 16-column block in the kernel's coalesced source order.  Lane l of a
-// fragment row (group g = l >> 4) loads the 16-B chunks g, g + 4, g + 8 of the
-// block's 192-byte window (64 source pixels from s0 + 64 t); lane-data byte P
-// is window byte 16 g + 64 (P / 16) + P % 16, whose channel is (g + P) mod 3
-// (16 and 64 are 1 mod 3), so channel c's A fragment dword m takes lane bytes
-// 12 m + c' + 3 i, i = 0..3, c' = (c - g) mod 3 (fd_ch on dwords 3m .. 3m + 2).
-// Fragment byte j = 4 m + i of lane l is K slot mfma_i8_k(l, j) = 16 g + j
-// (FI_MFMA_I8_MAP 1); B holds, at that K slot and column n, the coefficient of
-// the source pixel that byte is a channel of, in three signed-byte limbs.
-static void plan_sc_ft(ScPlan *p) {
-  p->ftB.clear();
-  p->ft_rows = p->ft_lds = 0;
-  if (!p->hm_ok || !p->vq_ok || FI_MFMA_I8_MAP != 1) return;
-  const int nb = p->hm_nb, ks = p->hm_ks, aw = p->aw;
-  p->ftB.assign((size_t)nb * ks * 3 * 3 * 256, 0);
-  for (int b = 0; b < nb; b++)
-    for (int t = 0; t < ks; t++)
-      for (int c = 0; c < 3; c++)
-        for (int l = 0; l < 64; l++)
-          for (int j = 0; j < 16; j++) {
-            const int g = l >> 4, n = l & 15, m = j >> 2, i = j & 3;
-            const int cp = ((c - g) % 3 + 3) % 3;
-            const int P = 12 * m + cp + 3 * i;
-            const int wb = 16 * g + 64 * (P / 16) + P % 16;  // window byte; channel c by construction
-            const int s = p->hmS0[b] + 64 * t + wb / 3, x = 16 * b + n;
-            int32_t k = 0;
-            if (x < aw) {
-              const int xmin = p->hb[2 * x], cnt = p->hb[2 * x + 1];
-              if (s >= xmin && s < xmin + cnt) k = p->hk[(size_t)x * p->ksh + (s - xmin)];
-            }
-            const int32_t l0 = ((k + 128) & 255) - 128;
-            const int32_t k1 = (k - l0) / 256;
-            const int32_t l1 = ((k1 + 128) & 255) - 128;
-            const int32_t l2 = (k1 - l1) / 256;
-            const int32_t limb[3] = {l0, l1, l2};
-            for (int q = 0; q < 3; q++) {
-              uint8_t *frag = reinterpret_cast<uint8_t *>(&p->ftB[((((size_t)b * ks + t) * 3 + c) * 3 + q) * 256]);
-              frag[l * 16 + j] = (uint8_t)(int8_t)limb[q];
-            }
-          }
-  // the window of each tile of kFtChunks chunks: from the first chunk's K0 to
-  // the last tap of its last prescaled row (Pillow's bounds grow with y), and
-  // every chunk's 64-row MFMA window inside the LDS rows
-  const int chunks = p->vq_chunks;
-  int rows = 0;
-  for (int c0 = 0; c0 < chunks; c0 += kFtChunks) {
-    const int c1 = std::min(c0 + kFtChunks, chunks) - 1;
-    const int kbase = p->vqK0[c0];
-    const int pe = std::min(p->ah, std::max(0, kVqRows * c1 - 1) + 16);
-    int kend = 0;
-    for (int y = std::max(0, kVqRows * c0 - 1); y < pe; y++) kend = std::max(kend, p->vb[2 * y] + p->vb[2 * y + 1]);
-    if (p->vb[2 * (pe - 1)] + p->vb[2 * (pe - 1) + 1] != kend) return;  // the kernel reads the last row's
-    int r = (std::min(kend, p->hrows) - kbase + 15) / 16 * 16;
-    for (int c = c0; c <= c1; c++) r = std::max(r, p->vqK0[c] - kbase + 64);
-    rows = std::max(rows, r);
-  }
-  const int apitch = (aw * 3 + 15) / 16 * 16, lpitch = (aw + 3) / 4 * 4;
-  p->ft_rows = rows;
-  p->ft_lds = rows * apitch + 16 * apitch + 16 * lpitch;
-}
-
 // k_sc_hx / k_sc_vx tables (fi_plan.h ScPlan::cx_*): per chunk of kVqRows
 // analysed rows, the 16 prescaled rows [pa, pa + 16) over the H-stage rows
 // [K0, K0 + 64 kv), K0 = the chunk's first tap rounded down to a multiple of 4,
@@ -1314,10 +1252,7 @@ void plan_sc_prep(ScPlan *p) {
       p->fz_ok = true;
     }
   }
-  if (!reduced) {
-    plan_sc_ft(p);
-    plan_sc_cx(p);
-  }
+  if (!reduced) plan_sc_cx(p);
 }
 
 static double thirds(double x) {

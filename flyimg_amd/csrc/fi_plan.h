@@ -212,14 +212,6 @@ struct ScPlan {
   // 16-row MFMA block), its H-stage window starts at vqK0[chunk] (<= 64 rows)
   bool vq_ok = false;
   int vq_chunks = 0, vq_lds = 0;
-  // k_sc_ft (chunk tiles): the horizontal B fragments in the kernel's
-  // coalesced source order -- lane group g of a fragment row loads the 16-B
-  // chunks g, g + 4, g + 8 of the 192-byte window, so its bytes are an RGB
-  // stream whose channel phase is rotated by g: [nb][ks][3 ch][3 limbs] x 256
-  // int32 (fi_plan.cpp sc_ft_tables); ft_rows = the H-stage rows the widest
-  // tile of kFtChunks chunks needs (16-row blocks), ft_lds its LDS
-  std::vector<int32_t> ftB;
-  int ft_rows = 0, ft_lds = 0;
   // k_sc_hx + k_sc_vx (co-resident with the next batch's resample: no LDS,
   // <= 64 VGPRs): the H-stage goes to HBM as 256-B tiles [block][channel][row
   // block][16 columns][16 rows] of p - 128 bytes, cx_tp / 16 row blocks, of

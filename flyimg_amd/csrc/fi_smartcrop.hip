@@ -1132,311 +1132,6 @@ __global__ __launch_bounds__(kFdThreads) void k_sc_fd(const ScDesc *__restrict__
   if (loader) fd_wait_vm(0);  // every DMA landed before the workgroup retires
 }
 
-// ---- k_sc_ft: k_sc_fd's prescale + maps (same arithmetic, bit-identical
-// maps) TILED by analysed-row chunks instead of streamed per image.  One
-// 8-wave workgroup per (image, kFtChunks consecutive chunks of kVqRows
-// analysed rows): 4 per cfg2 image, two resident per CU (LDS: the tile's
-// H-stage window + 16 prescaled rows + luma, <= kFtMaxLds).  Each recomputes
-// the H-stage rows of its window [kbase, kend) from the source, so tiles are
-// independent: no chain of per-block barriers per image (k_sc_fd's ~40 phases
-// on one workgroup per CU); the H pass runs free (no barrier) and the
-// workgroups of a CU cover each other's latency.
-//  * H pass: items (column block b, row block rb), b-major, a contiguous range
-//    per wave (a block's B fragments loaded once per wave).  A fragments come
-//    straight from global memory, coalesced: lane group g of fragment row r
-//    loads the 16-B chunks g, g + 4, g + 8 of the block's 192-byte window
-//    (each instruction reads 64 contiguous bytes of 16 rows), an RGB stream
-//    whose channel phase is rotated by g; channel c's operand takes the
-//    lane's bytes 12 m + c' + 3 i (c' = (c - g) mod 3) and the host's B
-//    fragments (ScPlan::ftB) are laid out in that K order.  The three weight
-//    limbs fold through the accumulator (t = A B2; t = A B1 + (t << 8);
-//    t = A B0 + (t << 8) + C') with C' = Pillow's bias - 2^29, so the H-stage
-//    byte as p - 128 is med3(t >> 22, -128, 127): the same int32 as
-//    k_sc_fd's sum, modulo 2^32.
-//  * per chunk: k_sc_vq's vertical MFMA from the window rows at K0(c) - kbase,
-//    luma, and k_sc_fd's maps pass (estimator, the skin/saturation table only
-//    for the colours it leaves open).
-// The host orders tiles XCD-aware (an image's tiles on one XCD back to back:
-// their windows overlap in its L2).  Needs 3-channel sources with 16-B
-// aligned rows readable to fd_rp(W) bytes (ScDesc.ft).
-constexpr int kFtThreads = 512;
-constexpr int kFtWaves = kFtThreads / 64;
-constexpr int kFtGather = 4;  // maps items per thread per step (table reads in flight together)
-#ifndef FI_FT_ABL
-#define FI_FT_ABL 0
-#endif
-// profiling ablations (wrong maps; tools/build_variant.sh): 1 no source loads,
-// 2 no horizontal pass, 4 no vertical pass, 8 no luma, 16 no maps, 32 no
-// table reads, 64 no map stores
-constexpr int kFtAbl = FI_FT_ABL;
-static_assert(FI_MFMA_I8_MAP == 1, "k_sc_ft's coalesced K order assumes fragment byte j = K slot 16 (l >> 4) + j");
-// channel c of the 12-byte RGB stream (a0, a1, a2) whose bytes start at
-// channel phase `ph` (byte k is channel (ph + k) mod 3): fd_ch's selectors for
-// c' = (c - ph) mod 3, precomputed per lane
-struct FtSel {
-  uint32_t s1[3], s2[3];
-};
-__device__ __forceinline__ FtSel ft_sel(int ph) {
-  FtSel s;
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    const int cp = (c - ph + 3) % 3;
-    s.s1[c] = cp == 0 ? 0x00060300u : cp == 1 ? 0x00070401u : 0x00000502u;
-    s.s2[c] = cp == 0 ? 0x05020100u : cp == 1 ? 0x06020100u : 0x07040100u;
-  }
-  return s;
-}
-__device__ __forceinline__ uint32_t ft_ch(uint32_t s1, uint32_t s2, uint32_t a0, uint32_t a1, uint32_t a2) {
-  return __builtin_amdgcn_perm(a2, __builtin_amdgcn_perm(a1, a0, s1), s2) ^ 0x80808080u;
-}
-template <int KS>
-__global__ __launch_bounds__(kFtThreads, KS == 1 ? 4 : 2) void k_sc_ft(const ScDesc *__restrict__ descs,
-                                                         const int32_t *__restrict__ tiles,
-                                                         const int32_t *__restrict__ ai, const ScParamsDev P,
-                                                         const uint16_t *__restrict__ skinsat) {
-  typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
-  const int di = tiles[2 * blockIdx.x], c0 = tiles[2 * blockIdx.x + 1];
-  if (di < 0) return;  // padding of an XCD's shorter tile list
-  const ScDesc &D = descs[di];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int aw = D.aw, ah = D.ah, hrows = D.hrows, yoff = D.ybox_first;
-  const int apitch = (aw * 3 + 15) & ~15, lpitch = (aw + 3) & ~3;
-  uint8_t *win = lds8;                           // [ft_rows][apitch] H-stage rows kbase .., p - 128
-  uint8_t *prer = lds8 + D.ft_rows * apitch;     // [16][apitch] prescaled rows pa .. pe - 1 of a chunk
-  uint8_t *lum = prer + 16 * apitch;             // [16][lpitch] their luma
-  const int chunks = (ah + kVqRows - 1) / kVqRows, c1 = min(c0 + kFtChunks, chunks);
-  const int kbase = ai[D.vqK0 + c0];
-  // the last tap of the tile's last prescaled row (Pillow's bounds grow with y;
-  // the host checked it is the tile's widest)
-  const int pe_last = min(ah, max(0, kVqRows * (c1 - 1) - 1) + 16);
-  const int kend = ai[D.vb + 2 * (pe_last - 1)] + ai[D.vb + 2 * (pe_last - 1) + 1];
-  const int nb = D.hm_nb, nrb = (min(kend, hrows) - kbase + 15) >> 4, nitems = nrb * nb;
-
-  // ---- H pass
-  {
-    const int g = lane >> 4, r = lane & 15;
-    const FtSel S = ft_sel(g);
-    const int32_t *hmS0 = ai + D.hmS0, *hmC = ai + D.hmC;
-    const i32x4 *fB = reinterpret_cast<const i32x4 *>(ai + D.ftB);
-    const int rp = fd_rp(D.W);
-    const int64_t sstride = D.stride;
-    const int per = (nitems + kFtWaves - 1) / kFtWaves;
-    const int j0 = min(wave * per, nitems), j1 = min(j0 + per, nitems);
-    // source bytes of item j: 3 chunks of 16 B per k-step
-    auto load_src = [&](int j, u32x4a (&q)[KS][3]) {
-      const int b = j / nrb, rb = j - b * nrb;
-      const int hr = min(kbase + 16 * rb + r, hrows - 1);
-      const uint8_t *row = D.img + (int64_t)(hr + yoff) * sstride;
-      const int s0 = hmS0[b];
-      const bool inside = 3 * (s0 + 64 * KS) <= rp;  // wave-uniform: every chunk readable
-#pragma unroll
-      for (int t = 0; t < KS; t++)
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-          const int off = 3 * (s0 + 64 * t) + 16 * g + 64 * i;
-          if (kFtAbl & 1) {
-            q[t][i] = u32x4a{(uint32_t)off, (uint32_t)i, 0u, 0u};
-          } else if (inside) {
-            q[t][i] = *reinterpret_cast<const u32x4a *>(row + off);
-          } else {
-            // the row's last chunks: off is 8-B aligned, rp 16-B aligned
-            u32x4a v = *reinterpret_cast<const u32x4a *>(row + min(off, rp - 16));
-            if (off > rp - 16) v = off == rp - 8 ? u32x4a{v.z, v.w, 0u, 0u} : u32x4a{0u, 0u, 0u, 0u};
-            q[t][i] = v;
-          }
-        }
-    };
-    // one k-step: the next item's source bytes in flight during this item; two:
-    // loaded per item (registers)
-    constexpr bool kPre = KS == 1;
-    u32x4a cur[KS][3], nxt[KS][3];
-    i32x4 Bf[KS][3][3];
-    int bB = -1;
-    int32_t cxp = 0;
-    if (j0 < j1 && !(kFtAbl & 2)) load_src(j0, cur);
-#pragma unroll 1
-    for (int j = j0; j < ((kFtAbl & 2) ? j0 : j1); j++) {
-      const int b = j / nrb, rb = j - b * nrb;
-      if (!kPre && j > j0) load_src(j, cur);
-      if (b != bB) {  // this wave's next column block: its B fragments and bias
-        bB = b;
-#pragma unroll
-        for (int t = 0; t < KS; t++)
-#pragma unroll
-          for (int ch = 0; ch < 3; ch++)
-#pragma unroll
-            for (int q = 0; q < 3; q++) Bf[t][ch][q] = fB[(((b * KS + t) * 3 + ch) * 3 + q) * 64 + lane];
-        const int x = 16 * b + r;
-        cxp = x < aw ? hmC[x] - (1 << 29) : 0;
-      }
-      if (kPre && j + 1 < j1) load_src(j + 1, nxt);
-      i32x4 A[KS][3];
-#pragma unroll
-      for (int t = 0; t < KS; t++) {
-        const uint32_t d[12] = {cur[t][0].x, cur[t][0].y, cur[t][0].z, cur[t][0].w, cur[t][1].x, cur[t][1].y,
-                                cur[t][1].z, cur[t][1].w, cur[t][2].x, cur[t][2].y, cur[t][2].z, cur[t][2].w};
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++)
-          A[t][ch] = i32x4{(int32_t)ft_ch(S.s1[ch], S.s2[ch], d[0], d[1], d[2]),
-                           (int32_t)ft_ch(S.s1[ch], S.s2[ch], d[3], d[4], d[5]),
-                           (int32_t)ft_ch(S.s1[ch], S.s2[ch], d[6], d[7], d[8]),
-                           (int32_t)ft_ch(S.s1[ch], S.s2[ch], d[9], d[10], d[11])};
-      }
-      // limbs folded through the accumulator (modular int32)
-      i32x4 acc[3];
-#pragma unroll
-      for (int ch = 0; ch < 3; ch++) {
-        acc[ch] = i32x4{0, 0, 0, 0};
-#pragma unroll
-        for (int t = 0; t < KS; t++) acc[ch] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[t][ch], Bf[t][ch][2], acc[ch], 0, 0, 0);
-      }
-#pragma unroll
-      for (int ch = 0; ch < 3; ch++) {
-        acc[ch] = acc[ch] << 8;
-#pragma unroll
-        for (int t = 0; t < KS; t++) acc[ch] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[t][ch], Bf[t][ch][1], acc[ch], 0, 0, 0);
-      }
-#pragma unroll
-      for (int ch = 0; ch < 3; ch++) {
-        acc[ch] = (acc[ch] << 8) + i32x4{cxp, cxp, cxp, cxp};
-#pragma unroll
-        for (int t = 0; t < KS; t++) acc[ch] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[t][ch], Bf[t][ch][0], acc[ch], 0, 0, 0);
-      }
-      const int x = 16 * b + r;
-      if (x < aw) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          uint8_t *dst = win + (16 * rb + 4 * g + i) * apitch + 3 * x;
-#pragma unroll
-          for (int ch = 0; ch < 3; ch++) dst[ch] = (uint8_t)min(max(acc[ch][i] >> 22, -128), 127);
-        }
-      }
-      if (kPre)
-#pragma unroll
-        for (int t = 0; t < KS; t++)
-#pragma unroll
-          for (int i = 0; i < 3; i++) cur[t][i] = nxt[t][i];
-    }
-  }
-  __syncthreads();
-  const ScFast F = sc_fast_params(P);
-  const int ng4 = (aw + 3) >> 2;
-  const float rcp_ng4 = 1.0f / (float)ng4;
-#pragma unroll 1
-  for (int c = c0; c < c1; c++) {
-    const int y0 = kVqRows * c, y1 = min(y0 + kVqRows, ah), pa = max(0, y0 - 1), pe = min(ah, pa + 16);
-    // ---- vertical pass (k_sc_vq's) over the chunk's 64-row window at K0(c):
-    // tiles of 16 byte columns over the waves; window rows past the tile's
-    // kend weigh 0 (whatever the LDS holds there)
-    {
-      const i32x4 *af = reinterpret_cast<const i32x4 *>(ai + D.vqA) + (size_t)c * 3 * 64;
-      const i32x4 A0 = af[lane], A1 = af[64 + lane], A2 = af[128 + lane];
-      int32_t cy[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) cy[i] = ai[D.vqC + min(pa + 4 * (lane >> 4) + i, ah - 1)];
-      const int koff = ai[D.vqK0 + c] - kbase;
-      const int rA = 16 * (lane >> 4) + ((lane & 15) >> 1);
-      const uint8_t *pA = win + (koff + rA) * apitch + 8 * (lane & 1), *pB = pA + 8 * apitch;
-      const int nq = apitch >> 4, nbytes = 3 * aw;
-#pragma unroll 1
-      for (int t = wave; t < ((kFtAbl & 4) ? 0 : nq); t += kFtWaves) {
-        const i32x2 lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pA + 16 * t));
-        const i32x2 hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((l_i32x2q *)(pB + 16 * t));
-        const i32x4 B = {lo.x, lo.y, hi.x, hi.y};
-        const i32x4 d2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
-        const i32x4 d1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, B, d2 << 8, 0, 0, 0);
-        const i32x4 d0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
-        const int col = 16 * t + (lane & 15);
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int m = 4 * (lane >> 4) + i;
-          // modular int32: the limbs' partial products may wrap, the sum fits
-          const int32_t sv = (int32_t)((uint32_t)d0[i] + ((uint32_t)d1[i] << 8) + (uint32_t)cy[i]);
-          if (col < nbytes && pa + m < pe) prer[m * apitch + col] = pil_clip8(sv);
-        }
-      }
-    }
-    __syncthreads();
-    // ---- luma of the prescaled rows pa .. pe - 1, four pixels per item (and
-    // the prescaled image when kept)
-    const int nr = pe - pa;
-#pragma unroll 1
-    for (int it = tid; it < ((kFtAbl & 8) ? 0 : nr * ng4); it += kFtThreads) {
-      const int m = fz_div(it, ng4, rcp_ng4), g = it - m * ng4;
-      const uint32_t *q = reinterpret_cast<const uint32_t *>(prer + m * apitch + 12 * g);
-      const uint32_t a0 = q[0], a1 = q[1], a2 = q[2];
-      const uint32_t R = fd_ch(0, a0, a1, a2) ^ 0x80808080u, G = fd_ch(1, a0, a1, a2) ^ 0x80808080u,
-                     B = fd_ch(2, a0, a1, a2) ^ 0x80808080u;
-      uint32_t l4 = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        l4 |= sc_luma((R >> (8 * k)) & 255u, (G >> (8 * k)) & 255u, (B >> (8 * k)) & 255u) << (8 * k);
-      *reinterpret_cast<uint32_t *>(lum + m * lpitch + 4 * g) = l4;
-      const int y = pa + m;
-      if (D.pre && y >= y0 && y < y1) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int x = 4 * g + k;
-          if (x < aw) {
-            uint8_t *o = D.pre + ((int64_t)y * aw + x) * 3;
-            o[0] = (uint8_t)(R >> (8 * k));
-            o[1] = (uint8_t)(G >> (8 * k));
-            o[2] = (uint8_t)(B >> (8 * k));
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // ---- maps of rows y0 .. y1 - 1 (k_sc_fd's pass): skin / saturation by
-    // sc_skin_sat_est, the table read only for the items it leaves open,
-    // kFtGather items per thread in flight together; edge from the luma
-    const int nit = (y1 - y0) * aw;
-    const int stepy = kFtThreads / aw, stepx = kFtThreads - stepy * aw;
-    int yr_w = tid / aw, x_w = tid - (tid / aw) * aw;
-#pragma unroll 1
-    for (int base = tid; base < ((kFtAbl & 16) ? 0 : nit); base += kFtGather * kFtThreads) {
-      uint32_t stv[kFtGather];
-      int yrs[kFtGather], xs[kFtGather];
-#pragma unroll
-      for (int u = 0; u < kFtGather; u++) {
-        while (x_w >= aw) {  // (at most twice: stepx < aw)
-          x_w -= aw;
-          yr_w++;
-        }
-        yrs[u] = yr_w;
-        xs[u] = x_w;
-        yr_w += stepy;
-        x_w += stepx;
-        stv[u] = 0;
-        if (base + u * kFtThreads < nit) {
-          const int m = y0 + yrs[u] - pa;
-          const uint8_t *qq = prer + m * apitch + 3 * xs[u];
-          const uint32_t rr = qq[0], gg = qq[1], bb = qq[2];
-          if (!sc_skin_sat_est(F, rr, gg, bb, lum[m * lpitch + xs[u]], stv[u])) {
-            const uint32_t t = (kFtAbl & 32) ? rr : skinsat[sc_colour_key(rr, gg, bb)];
-            stv[u] = (t & 255u) | ((t >> 8) << 16);
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kFtGather; u++) {
-        if (base + u * kFtThreads >= nit || (kFtAbl & 64)) break;
-        const int x = xs[u], y = y0 + yrs[u], m = y - pa;
-        const uint8_t *lrow = lum + m * lpitch;
-        const uint32_t L = lrow[x];
-        uint32_t E = L;
-        if (aw >= 3 && ah >= 3 && x > 0 && y > 0 && x < aw - 1 && y < ah - 1) {
-          const int v = 4 * (int)L - (int)lrow[x - lpitch] - (int)lrow[x + lpitch] - (int)lrow[x - 1] - (int)lrow[x + 1] + 1;
-          E = (uint32_t)(v <= 0 ? 0 : v >= 255 ? 255 : v);
-        }
-        D.maps[(int64_t)y * aw + x] = stv[u] | (E << 8);
-      }
-    }
-    if (c + 1 < c1) __syncthreads();  // the next chunk's vertical pass rewrites prer / lum
-  }
-}
-
 // ---- k_sc_hx + k_sc_vx: the same prescale + maps (same integer arithmetic,
 // bit-identical maps) shaped to run BESIDE the next batch's k_rs_vr: no LDS,
 // <= 64 VGPRs (launch_bounds(256, 8)), so their waves take the one wave slot
@@ -1445,7 +1140,9 @@ __global__ __launch_bounds__(kFtThreads, KS == 1 ? 4 : 2) void k_sc_ft(const ScD
 //  * k_sc_hx: one wave per (image, 16-column block b), looping over 16-row
 //    blocks of the H stage (k_sc_hmfma's B fragments stay in registers).  A
 //    lane's A operand is 16 consecutive source pixels (48 contiguous bytes);
-//    limbs fold through the accumulator as in k_sc_ft.  The MFMA result lane
+//    limbs fold through the accumulator (t = A B2; t = A B1 + (t << 8);
+//    t = A B0 + (t << 8) + C', C' = Pillow's bias - 2^29, so the H-stage byte
+//    as p - 128 is med3(t >> 22, -128, 127)).  The MFMA result lane
 //    (g, n) holds rows 4g .. 4g + 3 of column n: one dword store per channel
 //    into the TRANSPOSED H stage tbuf[b][ch][n][row] (p - 128 bytes).
 //  * k_sc_vx: one wave per (image, chunk of kVqRows analysed rows): per
@@ -1536,7 +1233,7 @@ __global__ __launch_bounds__(256, KS == 2 && NCH == 3 ? 4 : 8) void k_sc_hx(cons
                        (int32_t)(cur[t][0].z ^ 0x80808080u), (int32_t)(cur[t][0].w ^ 0x80808080u)};
         }
       }
-      // limbs folded through the accumulator (modular int32; k_sc_ft's C')
+      // limbs folded through the accumulator (modular int32)
       i32x4 acc = {0, 0, 0, 0};
 #pragma unroll
       for (int t = 0; t < KS; t++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[t], bfrag(t, 2), acc, 0, 0, 0);
@@ -1562,10 +1259,10 @@ __global__ __launch_bounds__(256, KS == 2 && NCH == 3 ? 4 : 8) void k_sc_hx(cons
 __device__ __forceinline__ uint32_t vx_byte(uint32_t v, int i) { return (v >> (8 * i)) & 255u; }
 
 template <int KV, int NCH>
-__global__ __launch_bounds__(256, KV == 2 && NCH == 3 ? 4 : 8) void k_sc_vx(const ScDesc *__restrict__ descs, const int32_t *__restrict__ tiles,
-                                                  const int32_t *__restrict__ ai, const ScFast F,
-                                                  const uint16_t *__restrict__ skinsat) {
-  typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+__global__ __launch_bounds__(256, KV == 2 && NCH == 3 ? 4 : 8) void k_sc_vx(const ScDesc *__restrict__ descs,
+                                                                          const int32_t *__restrict__ tiles,
+                                                                          const int32_t *__restrict__ ai, const ScFast F,
+                                                                          const uint16_t *__restrict__ skinsat) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tix = 4 * blockIdx.x + wave;
   const int di = tiles[2 * tix], c = tiles[2 * tix + 1];
@@ -2467,16 +2164,6 @@ int launch_sc_fd(hipStream_t s, const ScDesc *descs, int n, int lds, const int32
   if (n <= 0) return 0;
   if (lds > kFdMaxLds || !skinsat) return -1;
   hipLaunchKernelGGL(k_sc_fd, dim3(n), dim3(kFdThreads), lds, s, descs, ai, P, skinsat);
-  return 0;
-}
-int launch_sc_ft(hipStream_t s, int ks, const ScDesc *descs, const int32_t *tiles, int ntiles, int lds,
-                 const int32_t *ai, const ScParamsDev &P, const uint16_t *skinsat) {
-  if (ntiles <= 0) return 0;
-  if (lds > kFtMaxLds || !skinsat || (ks != 1 && ks != 2)) return -1;
-  if (ks == 1)
-    hipLaunchKernelGGL(k_sc_ft<1>, dim3(ntiles), dim3(kFtThreads), lds, s, descs, tiles, ai, P, skinsat);
-  else
-    hipLaunchKernelGGL(k_sc_ft<2>, dim3(ntiles), dim3(kFtThreads), lds, s, descs, tiles, ai, P, skinsat);
   return 0;
 }
 int launch_sc_vq(hipStream_t s, const ScDesc *descs, int n, int chunks, int lds, const int32_t *ai,

@@ -55,13 +55,13 @@ def _context_with(env):
                 os.environ[k] = v
 
 
-_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_SC_FD": "1", "FI_SC_FT": "1",
+_ENV = {"FI_FORCE_GENERIC": "0", "FI_VR_RS": "1", "FI_DISABLE_SC_FZ": "0", "FI_SC_FD": "1",
         "FI_SC_CX": "1"}
 PATHS = {
     # default kernels: k_rs_vr (block-major persistent MFMA resample; k_rs_vm
     # where its tables do not fit) / k_rs_hv; k_sc_fd streamed prescale + maps
-    # (k_sc_ft chunk tiles where it cannot stream, k_sc_hx + k_sc_vx where
-    # neither fits); k_sc_score3 (exact-integer MFMA score fast pass)
+    # (k_sc_fz where it cannot stream, k_sc_hx + k_sc_vx for gray sources
+    # neither takes); k_sc_score3 (exact-integer MFMA score fast pass)
     "vr": dict(_ENV),
     # the same with k_sc_fz (register-staged source rows, two workgroups per CU)
     "fz": dict(_ENV, FI_SC_FD="0", FI_SC_CX="0"),
@@ -84,11 +84,11 @@ def rctx(request):
 
 EXPECTED_PATH = {"vr": "path_vr", "fz": "path_vr", "vm": "path_vm", "generic": "path_generic_v"}
 # smartcrop prescale kernel of each path (images counted by fi_kernel_stats)
-EXPECTED_SC = {"vr": "sc_path_fd", "cx": "sc_path_cx", "ft": "sc_path_ft", "fz": "sc_path_fz", "vm": None,
+EXPECTED_SC = {"vr": "sc_path_fd", "cx": "sc_path_cx", "fz": "sc_path_fz", "vm": None,
                "generic": None}
-# the smartcrop tests also run k_sc_ft (chunk tiles) and k_sc_hx + k_sc_vx
+# the smartcrop tests also run k_sc_hx + k_sc_vx
 # (H stage through HBM as 256-B tiles, no LDS) on every image
-SC_PATHS = dict(PATHS, ft=dict(_ENV, FI_SC_FT="2", FI_SC_CX="0"), cx=dict(_ENV, FI_SC_CX="2"))
+SC_PATHS = dict(PATHS, cx=dict(_ENV, FI_SC_CX="2"))
 
 
 @pytest.mark.parametrize("W,H,opts,even_rows", [
@@ -236,13 +236,13 @@ def test_score3_runs_and_agrees_with_score2(ctx, s2ctx, w, h):
 def test_smartcrop_prescale_kernel_of_path(sctx, w, h):
     """fi_smartcrop runs its prescale + maps on the kernel the path names
     (k_sc_fd on the default path for 3-channel images at the staged 16-B
-    rounded pitch, k_sc_ft with FI_SC_FT=2, k_sc_hx + k_sc_vx with
+    rounded pitch, k_sc_hx + k_sc_vx with
     FI_SC_CX=2, k_sc_fz with FI_SC_FD=0; no silent fallback), and the result
     is the oracle's: every crop's scores
     bit-exact (exact_all).  The sizes prescale by 1.8-3 (a 14-row chunk's
     window within 64 H-stage rows)."""
     src = synth_rgb(w, h, 0x5C + w)
-    names = ("sc_path_cx", "sc_path_ft", "sc_path_fd", "sc_path_fz")
+    names = ("sc_path_cx", "sc_path_fd", "sc_path_fz")
     before = {k: sctx.stats(k)[1] for k in names}
     r = sctx.smartcrop_ex(src, 100, 100, options=_opts(True), want_images=True)
     ran = {k: sctx.stats(k)[1] - before[k] for k in names}

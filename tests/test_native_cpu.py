@@ -67,7 +67,6 @@ def test_vr_two_limb_quantisation_bound():
 @pytest.mark.parametrize("src,kernels", [
     ("fi_vr.hip", ["_ZN2fi7k_rs_vrILi0ELi2EE", "_ZN2fi7k_rs_vrILi0ELi4EE"]),
     ("fi_smartcrop.hip", ["_ZN2fi11k_sc_score2ILi1EE", "_ZN2fi11k_sc_score3E", ("_ZN2fi7k_sc_fdE", 12),
-                          "_ZN2fi7k_sc_ftILi1EE", "_ZN2fi7k_sc_ftILi2EE",
                           # k_sc_hx / k_sc_vx: the gray forms (cfg5's default) and the RGB two-k-step ones
                           "_ZN2fi7k_sc_hxILi2ELi1EE", "_ZN2fi7k_sc_vxILi2ELi1EE", "_ZN2fi7k_sc_hxILi1ELi1EE",
                           "_ZN2fi7k_sc_vxILi1ELi1EE", "_ZN2fi7k_sc_hxILi2ELi3EE", "_ZN2fi7k_sc_vxILi2ELi3EE",

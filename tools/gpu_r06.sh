@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 iteration run (one gpurun call).  STEP selects what runs:
 #   tests  : the new stream-ordering tests + the smartcrop / pipeline parity subset
-#   bench  : cfg2 bench line (stage split) with FI_SC_FT=1 and =0
+#   bench  : cfg2 bench line (stage split) with FI_SC_CX=1 and =0 (CXS)
 #   trace  : rocprofv3 kernel trace + stats of a short cfg2 bench
 # default: tests bench trace
 set -u
