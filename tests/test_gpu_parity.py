@@ -511,6 +511,51 @@ def test_full_size_pipeline_smartcrop_box_bit_exact(rctx, W, H, opts):
     _cmp(resized, ref_img, opts, MIN_EXACT_BASELINE)
 
 
+@pytest.mark.parametrize("W,H,opts", [
+    (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray,smc_1"),  # cfg5: two k-steps each way
+    (2400, 1600, "w_600,clsp_Gray,smc_1"),
+    (1600, 1200, "w_300,h_300,c_1,clsp_Gray,smc_1"),
+])
+def test_gray_smartcrop_on_hx_vx(W, H, opts):
+    """Gray smartcrop prescale on k_sc_hx + k_sc_vx (FI_SC_CX=2 forces them;
+    the default takes them for the gray images k_sc_fz cannot, cfg5's case,
+    asserted by the first parametrization), in the apply pipeline (the
+    resized image kept at a 16-B rounded pitch): the crop box and its exact
+    score equal the oracle's smartcrop on the GPU-resized pixels, the applied
+    crop is that box of them, and the other kernels (FI_SC_CX=0) agree."""
+    from flyimg_amd.processor import ImageProcessor, OptionsBag
+
+    src = _fast_rgb(W, H, 0x6A + W)
+    op = ImageProcessor(OptionsBag(opts), W, H).to_op()
+    op_noapply = Op(op.target_w, op.target_h, op.flags & ~L.FI_OP_SMARTCROP_APPLY, op.gravity, op.rotate, 100, 100)
+    c = _context_with(dict(_ENV))
+    try:
+        outs, _, rc = c.process([src], [op_noapply])
+        assert rc == 0, L.lib().fi_last_error()
+    finally:
+        c.close()
+    resized = outs[0]
+    assert resized.ndim == 2  # clsp_Gray: one channel into the smartcrop stage
+    ref = orc.sc_crop(np.repeat(resized[:, :, None], 3, axis=2), 100, 100)
+    t = ref["top_crop"]
+    ow, oh = min(t["width"] + t["x"], resized.shape[1] - t["x"]), min(t["height"] + t["y"], resized.shape[0] - t["y"])
+    exp = resized[t["y"]:t["y"] + oh, t["x"]:t["x"] + ow]
+    for cx in ("1", "2", "0"):
+        c = _context_with(dict(_ENV, FI_SC_CX=cx))
+        try:
+            b = c.stats("sc_path_cx")[1]
+            outs, recs, rc = c.process([src], [op])
+            assert rc == 0, L.lib().fi_last_error()
+            ran = c.stats("sc_path_cx")[1] - b
+        finally:
+            c.close()
+        assert ran == {"1": 1 if W == 6000 else ran, "2": 1, "0": 0}[cx], (cx, ran)
+        r = recs[0]
+        assert (r.crop_x, r.crop_y, r.crop_w, r.crop_h) == (t["x"], t["y"], t["width"], t["height"]), cx
+        assert r.crop_score.hex() == t["score"]["total"].hex() or r.n_candidates == 1
+        assert outs[0].shape == exp.shape and np.array_equal(outs[0], exp), cx
+
+
 def _fast_rgb(W, H, seed):
     """Cheap synthetic RGB8 for large cfg4 sizes (16-px blocks + noise: edges,
     flat areas and skin-like tones all occur); synth_rgb takes ~20 s at 24 MP."""
