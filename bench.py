@@ -517,10 +517,15 @@ def main():
         sys.exit(1)
 
 
+def cfg4_batch(shard_len):
+    """Images per cfg4 batch for a shard of shard_len images."""
+    return min(4096, max(1024, 1 << (max(shard_len // 16, 1).bit_length() - 1)))
+
+
 def run_cfg4(args, rank, world, local_rank, comm):
     """cfg4: the 65536-image mixed list, LPT-sharded by input bytes across the
     ranks (strong scaling: the total is fixed), each rank running its shard as
-    pipelined batches of 1024.  One step = every rank's whole shard.  Sources:
+    pipelined batches of cfg4_batch(shard) images.  One step = every rank's whole shard.  Sources:
     synthetic images in a device pool, k copies per size class so that no two
     descriptors of one batch share source bytes."""
     import numpy as np
@@ -545,7 +550,11 @@ def run_cfg4(args, rank, world, local_rank, comm):
     shard = shard_lpt([float(max(b_of[it], 1)) for it in items], world)[rank]
     ctx = Context(int(os.environ.get("FI_BENCH_DEVICE", local_rank)))  # override: rehearsal of N ranks on one GPU
     gather = RecordGather(comm, ctx)
-    B = 1024
+    # batch size: the largest power of two that still leaves the rank >= 16
+    # batches to pipeline, within [1024, 4096] -- fewer, larger batches cut the
+    # persistent launches' tails (one GPU: 1024 -> 4096 is 365 -> 342 ms per
+    # step, profiles/r06/cfg4_batch_ab.txt); 8 ranks keep 1024
+    B = int(os.environ.get("FI_BENCH_CFG4_BATCH", 0)) or cfg4_batch(len(shard))
     batches = [shard[j:j + B] for j in range(0, len(shard), B)]
     # distinct source bytes inside a batch, so repeat reads cannot
     # hit L2 / MALL -- each size class gets as many synthetic copies as the most

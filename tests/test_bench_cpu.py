@@ -175,3 +175,14 @@ def test_bench_launcher_fails_when_a_rank_fails():
     waiting in the rendezvous), and no JSON line is printed"""
     r = _bench(["--gpus", "2", "--dry-run"], FI_DRY_RUN_FAIL_RANK="1")
     assert r.returncode != 0 and r.stdout == ""
+
+
+def test_cfg4_batch_size_leaves_every_rank_a_pipeline():
+    """One GPU runs 4096-image batches (fewer persistent-launch tails), two
+    ranks 2048, four and eight ranks 1024: every rank keeps >= 8 batches so
+    batch k+1's host planning overlaps batch k."""
+    assert [bench.cfg4_batch(65536 // n) for n in (1, 2, 4, 8)] == [4096, 2048, 1024, 1024]
+    for n in (1, 2, 4, 8):
+        shard = 65536 // n
+        assert shard // bench.cfg4_batch(shard) >= 8
+    assert bench.cfg4_batch(10) == 1024

@@ -6,6 +6,7 @@
 #           -> gpurun_out/final/ (copy traffic_*.json into profiles/ before
 #           PART=2, so the bench lines report them)
 #   PART=3: the cfg4 PMC passes (every resample kernel) -> traffic_cfg4_resize.json
+#   PART=4: cfg4's kernel stats and bench line alone
 #   PART=2: rocprofv3 kernel stats of cfg2 / cfg3 / cfg4 / cfg5, the default
 #           bench line, the cfg1 / cfg3 / cfg4 / cfg5 lines -> gpurun_out/final/
 set -u
@@ -57,6 +58,15 @@ if [ "${PART:-1}" = 3 ]; then
   python3 "$ROOT/tools/pmc_to_json.py" "$OUT/pmc_cfg4" k_rs_ total:$n4 "$OUT/traffic_cfg4_resize.json" || exit 4
   echo "pmc cfg4 ok ($n4 images)"
   cd "$ROOT"
+fi
+if [ "${PART:-1}" = 4 ]; then
+  # cfg4 alone (after the bench's batch size changed): kernel stats + the line
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_cfg4" -o run -- \
+    python3 "$ROOT/bench.py" --workload cfg4 --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/prof_cfg4.json" 2> "$OUT/prof_cfg4.err" || exit 6
+  cd "$ROOT"
+  timeout -k 10 900 python bench.py --workload cfg4 --steps 1 --warmup 1 > "$OUT/cfg4.json" 2> "$OUT/cfg4.err" || { echo "cfg4 failed"; tail -3 "$OUT/cfg4.err"; exit 3; }
+  python3 -c "import json;d=json.load(open('$OUT/cfg4.json'));print('cfg4', d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline'].get('traffic'), d.get('verified','')[:5])"
 fi
 if [ "${PART:-1}" = 2 ]; then
   cd /tmp && export TMPDIR=/tmp
