@@ -244,6 +244,14 @@ struct fi_ctx {
   // CU, no LDS: it fits next to k_rs_vr's); FI_APPLY_OVERLAP=0: on sc_stream
   hipStream_t ap_stream = nullptr;
   bool apply_overlap = true;
+  // a batch with two or more k_rs_vr launches (mixed strip widths) runs the
+  // second and later ones on rs2_stream, forked from and joined back into
+  // `stream` inside the resize stage, so each persistent launch's tail (its
+  // unevenly loaded workgroups finishing) is filled by the other's workgroups
+  // instead of idling the CUs it frees; FI_VR_FORK=0: all on `stream`
+  hipStream_t rs2_stream = nullptr;
+  hipEvent_t rs_fork = nullptr, rs_join = nullptr;
+  bool vr_fork = true;
   // recorded on ap_stream after every overlapped apply: entry points that
   // launch on `stream` and may touch a batch's dst (face-blur, JPEG decode,
   // synthetic fill, a later batch whose sources are an earlier batch's
@@ -359,6 +367,7 @@ static void sync_streams(fi_ctx *c) {
   if (c->up_stream) (void)hipStreamSynchronize(c->up_stream);
   if (c->rb_stream) (void)hipStreamSynchronize(c->rb_stream);
   if (c->ap_stream) (void)hipStreamSynchronize(c->ap_stream);
+  if (c->rs2_stream) (void)hipStreamSynchronize(c->rs2_stream);
   if (c->gx_stream) (void)hipStreamSynchronize(c->gx_stream);
 }
 // Work about to run on c->stream that may read or write an earlier batch's
@@ -2550,8 +2559,16 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
     if (K.L0.tiles)
       hipLaunchKernelGGL(k_rs_copy, dim3(K.L0.tiles), dim3(256), 0, c->stream, (const ResizeDesc *)desc_p(K.L0),
                          pre_p(K.L0), K.L0.n);
+    const bool fork = c->vr_fork && c->rs2_stream && Bp.vrl.size() >= 2;
+    if (fork) {
+      if (!c->rs_fork) HIP_TRY(hipEventCreateWithFlags(&c->rs_fork, hipEventDisableTiming));
+      if (!c->rs_join) HIP_TRY(hipEventCreateWithFlags(&c->rs_join, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(c->rs_fork, c->stream));
+      HIP_TRY(hipStreamWaitEvent(c->rs2_stream, c->rs_fork, 0));
+    }
     for (const BatchPlan::VrLaunch &V : Bp.vrl) {
-      const int vrc = launch_vr(c->stream, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
+      hipStream_t vs = fork && &V != &Bp.vrl[0] ? c->rs2_stream : c->stream;
+      const int vrc = launch_vr(vs, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
                                 (const VrTile *)(ab + K.vrtile_off) + V.tile0, V.ntiles,
                                 (const int32_t *)(ab + K.vrinfo_off) + V.info0, V.G, ai, V.L);
       if (vrc < 0) return set_err(FI_EDEVICE, "block-major MFMA resample launch rejected (LDS %d)", V.L.total);
@@ -2593,6 +2610,10 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
                            pre_p(K.L2a), K.L2a.n, ai, af);
       hipLaunchKernelGGL(k_rs_v_final, dim3(K.L2b.tiles), dim3(256), 0, c->stream,
                          (const ResizeDesc *)desc_p(K.L2b), pre_p(K.L2b), K.L2b.n, ai, af);
+    }
+    if (fork) {
+      HIP_TRY(hipEventRecord(c->rs_join, c->rs2_stream));
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->rs_join, 0));
     }
   }
   if (!Bp.conv_items.empty()) {
@@ -3385,6 +3406,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   }
   c->sc_stream = c->stream;
   if (const char *e = getenv("FI_APPLY_OVERLAP")) c->apply_overlap = e[0] == '1';
+  if (const char *e = getenv("FI_VR_FORK")) c->vr_fork = e[0] == '1';
   // ap_stream at the higher priority: its score / apply take the CUs the
   // resample frees before the next resample's workgroups do
   int prio_lo = 0, prio_hi = 0;
@@ -3392,6 +3414,7 @@ int fi_create(fi_ctx **out, int32_t device) {
   if (hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->rb_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithPriority(&c->ap_stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->rs2_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->gx_stream, hipStreamNonBlocking) != hipSuccess) {
     fi_destroy(c);
     return set_err(FI_EDEVICE, "hipStreamCreate failed");
@@ -3429,7 +3452,10 @@ void fi_destroy(fi_ctx *c) {
   if (c->up_stream) (void)hipStreamDestroy(c->up_stream);
   if (c->rb_stream) (void)hipStreamDestroy(c->rb_stream);
   if (c->ap_stream) (void)hipStreamDestroy(c->ap_stream);
+  if (c->rs2_stream) (void)hipStreamDestroy(c->rs2_stream);
   if (c->gx_stream) (void)hipStreamDestroy(c->gx_stream);
+  if (c->rs_fork) (void)hipEventDestroy(c->rs_fork);
+  if (c->rs_join) (void)hipEventDestroy(c->rs_join);
   if (c->ap_tail) (void)hipEventDestroy(c->ap_tail);
   if (c->gx_done) (void)hipEventDestroy(c->gx_done);
   if (c->gx_pin) (void)hipHostFree(c->gx_pin);
