@@ -2565,6 +2565,7 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
       if (!c->rs_join) HIP_TRY(hipEventCreateWithFlags(&c->rs_join, hipEventDisableTiming));
       HIP_TRY(hipEventRecord(c->rs_fork, c->stream));
       HIP_TRY(hipStreamWaitEvent(c->rs2_stream, c->rs_fork, 0));
+      c->stats["vr_fork"].launches += 1;
     }
     for (const BatchPlan::VrLaunch &V : Bp.vrl) {
       hipStream_t vs = fork && &V != &Bp.vrl[0] ? c->rs2_stream : c->stream;

@@ -256,7 +256,8 @@ int fi_fill_synthetic(fi_ctx *ctx, uint8_t *dev, int32_t w, int32_t h, int32_t s
  * adds a few microseconds between dependent kernels).  fi_kernel_stats also
  * reports host timings ("host_*", "host_total") and per-path image counters
  * ("path_vr", "path_vm", "path_hv", "path_generic_v", "path_generic_h",
- * "path_copy", "sc_path_fd", "sc_path_fz").  bytes = algorithmic bytes
+ * "path_copy", "sc_path_fd", "sc_path_fz", "sc_path_cx"; "vr_fork": batches
+ * whose later k_rs_vr launches ran on the forked stream).  bytes = algorithmic bytes
  * accounted to that stage. */
 int fi_set_timing(fi_ctx *ctx, int32_t enable);
 int fi_reset_stats(fi_ctx *ctx);

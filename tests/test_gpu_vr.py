@@ -192,8 +192,8 @@ def test_vr_role_splits_and_plane_buffers(pair, nl, pbuf):
 
 def test_vr_split_launches(pair):
     """a batch that mixes one-block strips (4 loader waves) with wider ones in
-    numbers that fill the chip twice runs as two k_rs_vr launches; every image
-    equals k_rs_vm's bytes"""
+    numbers that fill the chip twice runs as two k_rs_vr launches, the second
+    on the forked stream beside the first; every image equals k_rs_vm's bytes"""
     vr, vm = pair
     geo = [(1920, 1080, "w_500"), (4000, 3000, "w_150"), (1920, 1080, "w_500"), (6000, 4000, "w_400,h_400,c_1,r_90,clsp_Gray")]
     uniq = sorted(set(geo))
@@ -204,10 +204,11 @@ def test_vr_split_launches(pair):
         srcs.append(base[g][(k // len(geo)) % 2])
         ops.append(ImageProcessor(OptionsBag(g[2]), g[0], g[1]).to_op())
         gk.append((g, (k // len(geo)) % 2))
-    before = vr.stats("path_vr")[1]
+    before, forks = vr.stats("path_vr")[1], vr.stats("vr_fork")[1]
     ob, rb, rc = vr.process(srcs, ops)
     assert rc == 0 and all(r.status == 0 for r in rb), L.lib().fi_last_error()
     assert vr.stats("path_vr")[1] == before + len(srcs)
+    assert vr.stats("vr_fork")[1] == forks + 1  # the second launch ran on the forked stream (FI_VR_FORK)
     for g in uniq:
         oa, _, rca = vm.process(base[g], [ImageProcessor(OptionsBag(g[2]), g[0], g[1]).to_op()] * 2)
         assert rca == 0
