@@ -2567,6 +2567,18 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
       HIP_TRY(hipStreamWaitEvent(c->rs2_stream, c->rs_fork, 0));
       c->stats["vr_fork"].launches += 1;
     }
+    // the join, at the end of the resize scope (before its timer's end event)
+    // and on every early error return, so no forked launch outlives the stage
+    struct Join {
+      fi_ctx *c;
+      bool on;
+      ~Join() {
+        if (!on) return;
+        if (hipEventRecord(c->rs_join, c->rs2_stream) != hipSuccess ||
+            hipStreamWaitEvent(c->stream, c->rs_join, 0) != hipSuccess)
+          (void)hipStreamSynchronize(c->rs2_stream);
+      }
+    } join{c, fork};
     for (const BatchPlan::VrLaunch &V : Bp.vrl) {
       hipStream_t vs = fork && &V != &Bp.vrl[0] ? c->rs2_stream : c->stream;
       const int vrc = launch_vr(vs, (const VDesc *)(ab + K.vdesc_off), (const MStrip *)(ab + K.vstrip_off),
@@ -2611,10 +2623,6 @@ static int launch_batch(fi_ctx *c, const Exec &E, const BatchPlan &Bp, const Pac
                            pre_p(K.L2a), K.L2a.n, ai, af);
       hipLaunchKernelGGL(k_rs_v_final, dim3(K.L2b.tiles), dim3(256), 0, c->stream,
                          (const ResizeDesc *)desc_p(K.L2b), pre_p(K.L2b), K.L2b.n, ai, af);
-    }
-    if (fork) {
-      HIP_TRY(hipEventRecord(c->rs_join, c->rs2_stream));
-      HIP_TRY(hipStreamWaitEvent(c->stream, c->rs_join, 0));
     }
   }
   if (!Bp.conv_items.empty()) {
