@@ -97,6 +97,28 @@ class FiRecord(ctypes.Structure):
                 ("image", "status", "out_w", "out_h", "crop_x", "crop_y", "crop_w", "crop_h")]
 
 
+def struct_view(arr):
+    """A ctypes array of a Structure as a numpy structured array over the same
+    memory (scalar and fixed-array fields at their ctypes offsets), so a batch's
+    fields are read or written column-wise instead of one attribute at a time."""
+    import numpy as np
+
+    st = arr._type_
+    kinds = {ctypes.c_int32: "<i4", ctypes.c_uint32: "<u4", ctypes.c_int64: "<i8", ctypes.c_double: "<f8",
+             ctypes.c_void_p: "<u8"}
+    names, formats, offsets = [], [], []
+    for name, ty in st._fields_:
+        if ty in kinds:
+            fmt = kinds[ty]
+        else:  # ctypes.c_double * k
+            fmt = (kinds[ty._type_], (ty._length_,))
+        names.append(name)
+        formats.append(fmt)
+        offsets.append(getattr(st, name).offset)
+    dt = np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": ctypes.sizeof(st)})
+    return np.frombuffer((ctypes.c_char * ctypes.sizeof(arr)).from_buffer(arr), dtype=dt, count=len(arr))
+
+
 class FiError(RuntimeError):
     """A non-zero status from libflyimg_hip (Processor.php:53-59's
     ExecFailedException analogue)."""

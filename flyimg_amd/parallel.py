@@ -168,7 +168,8 @@ class RecordGather:
             self.backend = "comm"
 
     def gather(self, records):
-        """records: list of 8-int tuples (fi_record).  Rank 0 gets all ranks'."""
+        """records: list of 8-int tuples (fi_record), or an (n, 8) int32 array.
+        Rank 0 gets all ranks' (as an (n * world, 8) array for an array input)."""
         self.start(records)
         return self.finish()
 
@@ -181,21 +182,30 @@ class RecordGather:
     def start(self, records):
         if self._pending is not None:
             self.finish()
+        import numpy as np
+
+        as_array = isinstance(records, np.ndarray)
         if self.backend == "local":
-            self._pending = ("local", list(records))
+            self._pending = ("local", records.copy() if as_array else list(records))
             return
         if self.backend == "rccl":
+            import ctypes
+
             from . import _lib as L
 
             n = len(records)
             send = (L.FiRecord * max(n, 1))()
-            for i, r in enumerate(records):
-                send[i] = L.FiRecord(*r)
+            if as_array:
+                rec = np.ascontiguousarray(records, dtype=np.int32).reshape(n, 8)
+                ctypes.memmove(send, rec.ctypes.data, rec.nbytes)
+            else:
+                for i, r in enumerate(records):
+                    send[i] = L.FiRecord(*r)
             recv = (L.FiRecord * max(n * self.comm.world, 1))() if self.comm.rank == 0 else None
             L.check(L.lib().fi_rccl_gather_start(self.ctx.h, send, n, recv))
-            self._pending = ("rccl", (n, recv))
+            self._pending = ("rccl", (n, recv, as_array))
             return
-        self._pending = ("comm", [list(r) for r in records])
+        self._pending = ("comm", (records.tolist() if as_array else [list(r) for r in records], as_array))
 
     def finish(self):
         if self._pending is None:
@@ -208,10 +218,21 @@ class RecordGather:
             from . import _lib as L
 
             L.check(L.lib().fi_rccl_gather_finish(self.ctx.h))
-            n, recv = data
+            n, recv, as_array = data
             if self.comm.rank != 0:
                 return None
+            if as_array:
+                import numpy as np
+
+                return np.frombuffer(recv, dtype=np.int32, count=n * self.comm.world * 8).reshape(-1, 8).copy()
             return [tuple(getattr(recv[i], f) for f, _ in L.FiRecord._fields_) for i in range(n * self.comm.world)]
         # the control-plane gather is a rendezvous: it runs at finish()
-        allr = self.comm.allgather_obj(data)
-        return [tuple(r) for part in allr for r in part] if self.comm.rank == 0 else None
+        rows, as_array = data
+        allr = self.comm.allgather_obj(rows)
+        if self.comm.rank != 0:
+            return None
+        if as_array:
+            import numpy as np
+
+            return np.asarray([r for part in allr for r in part], dtype=np.int32).reshape(-1, 8)
+        return [tuple(r) for part in allr for r in part]

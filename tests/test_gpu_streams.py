@@ -179,3 +179,31 @@ def test_gather_returns_while_batches_run():
             ctx.free(dst)
     finally:
         ctx.close()
+
+
+def test_record_gather_rccl_array_form():
+    """RecordGather over RCCL (one rank) takes bench.py's cfg4 form -- an
+    (n, 8) int32 block, copied into the fi_record send buffer in one move --
+    and hands rank 0 the same rows back as an array; the tuple form still
+    gives tuples."""
+    from flyimg_amd.parallel import RecordGather
+
+    ctx = Context(0)
+    try:
+        lib = L.lib()
+        uid = ctypes.create_string_buffer(128)
+        L.check(lib.fi_rccl_get_unique_id(uid))
+        L.check(lib.fi_rccl_init(ctx.h, 0, 1, uid.raw))
+
+        class One:
+            rank, world = 0, 1
+
+        g = RecordGather(One())
+        g.ctx, g.backend = ctx, "rccl"  # the world > 1 backend, on this one rank's communicator
+        recs = np.arange(300 * 8, dtype=np.int32).reshape(300, 8)
+        got = g.gather(recs)
+        assert isinstance(got, np.ndarray) and got.dtype == np.int32 and np.array_equal(got, recs)
+        rows = [tuple(int(x) for x in r) for r in recs[:5]]
+        assert g.gather(rows) == rows
+    finally:
+        ctx.close()

@@ -98,7 +98,7 @@ class GlooComm:
         self.dist.barrier()
 
 
-def _gloo_rank(rank, world, port, q):
+def _gloo_rank(rank, world, port, as_array, q):
     try:
         import torch.distributed as dist
 
@@ -108,7 +108,15 @@ def _gloo_rank(rank, world, port, q):
         uid = comm.bcast_bytes(b"unique-id-bytes" if rank == 0 else None)
         comm.barrier()
         shard = list(shard_contiguous(N_IMAGES, world)[rank])
-        got = RecordGather(comm).gather(_records(rank, shard))
+        if as_array:  # bench.py's cfg4 form: an (n, 8) int32 block in, an array out on rank 0
+            import numpy as np
+
+            got = RecordGather(comm).gather(np.asarray(_records(rank, shard), dtype=np.int32))
+            if got is not None:
+                assert isinstance(got, np.ndarray) and got.dtype == np.int32 and got.shape[1] == 8
+                got = [tuple(int(x) for x in r) for r in got]
+        else:
+            got = RecordGather(comm).gather(_records(rank, shard))
         comm.close()
         dist.destroy_process_group()
         q.put((rank, g, uid, got, None))
@@ -124,9 +132,10 @@ def _free_port():
     return p
 
 
-def test_gloo_world2_same_shard_and_gather_logic():
+@pytest.mark.parametrize("as_array", [False, True], ids=["tuples", "array"])
+def test_gloo_world2_same_shard_and_gather_logic(as_array):
     pytest.importorskip("torch")
-    out = _run(_gloo_rank, 2, _free_port())
+    out = _run(_gloo_rank, 2, _free_port(), as_array)
     _check(out, 2)
 
 
