@@ -186,3 +186,13 @@ def test_cfg4_batch_size_leaves_every_rank_a_pipeline():
         shard = 65536 // n
         assert shard // bench.cfg4_batch(shard) >= 8
     assert bench.cfg4_batch(10) == 1024
+
+
+def test_cfg4_batches_cover_the_shard_with_a_short_first_batch():
+    for n, B in ((65536, 4096), (8192, 1024), (1000, 1024), (5000, 1024)):
+        shard = list(range(n))
+        bs = bench.cfg4_batches(shard, B)
+        assert [i for b in bs for i in b] == shard
+        assert all(len(b) <= B for b in bs)
+        if n > B:
+            assert len(bs[0]) == B // 4
