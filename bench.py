@@ -722,7 +722,7 @@ def run_cfg4(args, rank, world, local_rank, comm):
                 "workload": f"cfg4: {WORKLOADS['cfg4'][4]}",
                 "images_total": n_total, "size_classes": len(sizes),
                 "mean_mpix_per_image": round(mpix / args.steps / n_total, 3),
-                "ops": CFG4_OPS, "batch": B,
+                "ops": CFG4_OPS, "batch": B, "first_batch": len(batches[0]) if batches else 0,
                 "parallelism": f"dp{world} (LPT shards by B_img, RCCL gather of result records)",
                 "record_gather": gather.backend,
             },
